@@ -1,0 +1,125 @@
+"""ctypes binding of libautomerge_amd.so (include/automerge_amd.h).
+
+There is no CPU fallback: importing this module raises if the library is missing, and creating
+an engine raises if no HIP device is visible.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libautomerge_amd.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        "automerge_amd: native library %s is missing; build it with "
+        "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)" % LIB_PATH)
+
+lib = C.CDLL(LIB_PATH)
+
+u8p = C.POINTER(C.c_uint8)
+
+
+class ChunkDesc(C.Structure):
+    _fields_ = [("off", C.c_uint64), ("len", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class DocDesc(C.Structure):
+    _fields_ = [("base_chunk", C.c_int64), ("chg_begin", C.c_uint32), ("chg_count", C.c_uint32),
+                ("known_begin", C.c_uint32), ("known_count", C.c_uint32), ("flags", C.c_uint32),
+                ("pad", C.c_uint32)]
+
+
+class KnownHash(C.Structure):
+    _fields_ = [("hash", C.c_uint8 * 32), ("index", C.c_int64)]
+
+
+class DocResult(C.Structure):
+    _fields_ = [("status", C.c_uint32), ("err_change", C.c_uint32), ("arg0", C.c_int64), ("arg1", C.c_int64),
+                ("arg_actor_off", C.c_uint64), ("arg_actor_len", C.c_uint32), ("napplied", C.c_uint32),
+                ("nqueued", C.c_uint32), ("nheads", C.c_uint32), ("nops", C.c_uint32), ("nchanges", C.c_uint32),
+                ("max_op", C.c_int64), ("out_off", C.c_uint64), ("out_len", C.c_uint64), ("ws_off", C.c_uint64),
+                ("ws_bytes", C.c_uint64)]
+
+
+class Error(C.Structure):
+    _fields_ = [("code", C.c_uint32), ("is_type_error", C.c_int32), ("message", C.c_char * 480)]
+
+
+P = C.c_void_p
+_sigs = {
+    "am_version": (C.c_char_p, []),
+    "am_engine_create": (P, [C.c_int, C.POINTER(Error)]),
+    "am_engine_destroy": (None, [P]),
+    "am_batch_create": (P, [P]),
+    "am_batch_destroy": (None, [P]),
+    "am_batch_stage": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, C.c_uint32, P, C.c_uint32, C.POINTER(Error)]),
+    "am_batch_run": (C.c_int, [P]),
+    "am_batch_sync": (C.c_int, [P, C.POINTER(Error)]),
+    "am_batch_results": (C.c_int, [P, P]),
+    "am_batch_chunk_results": (C.c_int, [P, P, P, P]),
+    "am_batch_doc_output": (C.c_int, [P, C.c_uint32, P, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "am_batch_doc_heads": (C.c_int, [P, C.c_uint32, P, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "am_batch_stage_times": (C.c_int, [P, C.POINTER(C.c_float)]),
+    "am_batch_workspace_bytes": (C.c_uint64, [P]),
+    "am_doc_init": (P, [P]),
+    "am_doc_load": (P, [P, C.c_char_p, C.c_size_t, C.POINTER(Error)]),
+    "am_doc_clone": (P, [P]),
+    "am_doc_free": (None, [P]),
+    "am_doc_apply_changes": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t, C.POINTER(Error)]),
+    "am_doc_save": (C.c_int, [P, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
+    "am_doc_get_heads": (C.c_size_t, [P, P, C.c_size_t]),
+    "am_doc_pending": (C.c_size_t, [P]),
+    "am_doc_max_op": (C.c_int64, [P]),
+    "am_doc_num_changes": (C.c_size_t, [P]),
+    "am_doc_change": (C.c_int, [P, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), P]),
+    "am_free": (None, [P]),
+    "am_change_hashes": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t, P, C.POINTER(Error)]),
+}
+for _name, (_res, _args) in _sigs.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+EXPORTS = sorted(_sigs)
+
+# status codes (include/automerge_amd.h)
+CHG_DUP, CHG_QUEUED = -3, -2
+
+
+class AutomergeError(Exception):
+    """Error raised by the engine; `kind` is the reference's JS error class."""
+
+    def __init__(self, message, code=0, kind="RangeError"):
+        super().__init__(message)
+        self.code = code
+        self.kind = kind
+
+    @property
+    def unsupported(self):
+        return self.code >= 100
+
+
+def raise_for(err):
+    msg = err.message.decode("utf-8", "replace")
+    raise AutomergeError(msg, err.code, "TypeError" if err.is_type_error else "RangeError")
+
+
+_engines = {}
+
+
+def engine(device=0):
+    """Per-process engine for one HIP device (created on first use)."""
+    if device not in _engines:
+        err = Error()
+        e = lib.am_engine_create(device, C.byref(err))
+        if not e:
+            raise_for(err)
+        _engines[device] = e
+    return _engines[device]
+
+
+def buf_array(bufs):
+    n = len(bufs)
+    arr = (C.c_char_p * max(n, 1))(*[bytes(b) for b in bufs])
+    lens = (C.c_size_t * max(n, 1))(*[len(b) for b in bufs])
+    return arr, lens, n

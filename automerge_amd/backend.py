@@ -1,0 +1,167 @@
+"""Drop-in mirror of the reference Backend module (backend/backend.js, backend/index.js).
+
+Same function names, argument meaning and error behaviour as the reference; every call runs the
+MI355X pipeline of libautomerge_amd.so (there is no CPU path). A backend state is the reference's
+`{state, heads, frozen}` wrapper: after applyChanges / loadChanges the old handle is frozen and
+further use raises the reference's error (backend/util.js:1-10).
+"""
+import ctypes as C
+
+from . import _native as N
+
+_FROZEN_MSG = ("Attempting to use an outdated Automerge document that has already been updated. "
+               "Please use the latest document state, or call Automerge.clone() if you really "
+               "need to use this old document state.")
+
+
+class BackendState:
+    __slots__ = ("state", "heads", "frozen")
+
+    def __init__(self, state, heads):
+        self.state = state
+        self.heads = heads
+        self.frozen = False
+
+
+class _Doc:
+    """Owns an am_doc handle."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def __del__(self):
+        if self.ptr:
+            N.lib.am_doc_free(self.ptr)
+            self.ptr = None
+
+    def heads(self):
+        n = N.lib.am_doc_get_heads(self.ptr, None, 0)
+        buf = (C.c_uint8 * (32 * max(n, 1)))()
+        N.lib.am_doc_get_heads(self.ptr, buf, n)
+        raw = bytes(buf)
+        return [raw[32 * i:32 * i + 32].hex() for i in range(n)]
+
+
+def _backend_state(backend):
+    # backendState() (backend/util.js:1-10)
+    if backend.frozen:
+        raise RuntimeError(_FROZEN_MSG)
+    return backend.state
+
+
+def init(device=0):
+    """Backend.init() (backend/backend.js:8-10)."""
+    d = _Doc(N.lib.am_doc_init(N.engine(device)))
+    return BackendState(d, [])
+
+
+def clone(backend):
+    """Backend.clone() (backend/backend.js:12-14)."""
+    s = _backend_state(backend)
+    return BackendState(_Doc(N.lib.am_doc_clone(s.ptr)), backend.heads)
+
+
+def free(backend):
+    """Backend.free() (backend/backend.js:16-19)."""
+    backend.state = None
+    backend.frozen = True
+
+
+def _apply(backend, changes):
+    s = _backend_state(backend)
+    arr, lens, n = N.buf_array(changes)
+    err = N.Error()
+    if N.lib.am_doc_apply_changes(s.ptr, arr, lens, n, C.byref(err)):
+        N.raise_for(err)
+    backend.frozen = True
+    return BackendState(s, s.heads())
+
+
+def applyChanges(backend, changes):
+    """Backend.applyChanges() (backend/backend.js:27-32). Returns (state, patch); patch
+    generation is not part of this engine yet, so the patch carries only the reference's
+    top-level fields (maxOp, clock-free deps, pendingChanges)."""
+    new = _apply(backend, changes)
+    return new, {"maxOp": maxOp(new), "deps": new.heads, "pendingChanges": pendingChanges(new)}
+
+
+def loadChanges(backend, changes):
+    """Backend.loadChanges() (backend/backend.js:115-120)."""
+    return _apply(backend, changes)
+
+
+def load(data, device=0):
+    """Backend.load() (backend/backend.js:104-107)."""
+    err = N.Error()
+    p = N.lib.am_doc_load(N.engine(device), bytes(data), len(data), C.byref(err))
+    if not p:
+        N.raise_for(err)
+    d = _Doc(p)
+    return BackendState(d, d.heads())
+
+
+def save(backend):
+    """Backend.save() (backend/backend.js:96-98)."""
+    s = _backend_state(backend)
+    out = N.u8p()
+    n = C.c_size_t()
+    err = N.Error()
+    if N.lib.am_doc_save(s.ptr, C.byref(out), C.byref(n), C.byref(err)):
+        N.raise_for(err)
+    data = C.string_at(out, n.value)
+    N.lib.am_free(out)
+    return data
+
+
+def getHeads(backend):
+    """Backend.getHeads() (backend/backend.js:134-136)."""
+    return backend.heads
+
+
+def pendingChanges(backend):
+    return N.lib.am_doc_pending(_backend_state(backend).ptr)
+
+
+def maxOp(backend):
+    return N.lib.am_doc_max_op(_backend_state(backend).ptr)
+
+
+def getAllChanges(backend):
+    """Backend.getAllChanges() for documents built by applyChanges (full hash graph)."""
+    s = _backend_state(backend)
+    out = []
+    i = 0
+    while True:
+        p = N.u8p()
+        n = C.c_size_t()
+        if N.lib.am_doc_change(s.ptr, i, C.byref(p), C.byref(n), None):
+            break
+        out.append(C.string_at(p, n.value))
+        i += 1
+    return out
+
+
+def getChangeByHash(backend, hash_hex):
+    """Backend.getChangeByHash() (backend/backend.js:166-168)."""
+    s = _backend_state(backend)
+    i = 0
+    h = (C.c_uint8 * 32)()
+    while True:
+        p = N.u8p()
+        n = C.c_size_t()
+        if N.lib.am_doc_change(s.ptr, i, C.byref(p), C.byref(n), h):
+            return None
+        if bytes(h).hex() == hash_hex:
+            return C.string_at(p, n.value)
+        i += 1
+
+
+def changeHashes(changes, device=0):
+    """decodeChangeMeta(change, true).hash for each change (columnar.js:783), on the GPU."""
+    arr, lens, n = N.buf_array(changes)
+    out = (C.c_uint8 * (32 * max(n, 1)))()
+    err = N.Error()
+    if N.lib.am_change_hashes(N.engine(device), arr, lens, n, out, C.byref(err)):
+        N.raise_for(err)
+    raw = bytes(out)
+    return [raw[32 * i:32 * i + 32].hex() for i in range(n)]

@@ -1,0 +1,124 @@
+"""Batched load + applyChanges over many documents per launch (am_batch_* in
+include/automerge_amd.h). Each document is (optional base document bytes, list of change
+buffers): Backend.load(base) followed by Backend.applyChanges(state, changes)."""
+import ctypes as C
+
+import numpy as np
+
+from . import _native as N
+
+CHUNK_DT = np.dtype([("off", "<u8"), ("len", "<u4"), ("flags", "<u4")])
+DOC_DT = np.dtype([("base_chunk", "<i8"), ("chg_begin", "<u4"), ("chg_count", "<u4"), ("known_begin", "<u4"),
+                   ("known_count", "<u4"), ("flags", "<u4"), ("pad", "<u4")])
+RESULT_DT = np.dtype([("status", "<u4"), ("err_change", "<u4"), ("arg0", "<i8"), ("arg1", "<i8"),
+                      ("arg_actor_off", "<u8"), ("arg_actor_len", "<u4"), ("napplied", "<u4"), ("nqueued", "<u4"),
+                      ("nheads", "<u4"), ("nops", "<u4"), ("nchanges", "<u4"), ("max_op", "<i8"),
+                      ("out_off", "<u8"), ("out_len", "<u8"), ("ws_off", "<u8"), ("ws_bytes", "<u8")])
+assert CHUNK_DT.itemsize == C.sizeof(N.ChunkDesc)
+assert DOC_DT.itemsize == C.sizeof(N.DocDesc)
+assert RESULT_DT.itemsize == C.sizeof(N.DocResult)
+
+
+def pack(docs):
+    """docs: iterable of (base_bytes | None, [change bytes]) -> (arena, chunks, docdescs)."""
+    parts, chunks, descs = [], [], []
+    off = 0
+    for base, changes in docs:
+        d = np.zeros((), DOC_DT)
+        d["base_chunk"] = -1
+        if base:
+            d["base_chunk"] = len(chunks)
+            chunks.append((off, len(base), 0))
+            parts.append(base)
+            off += len(base)
+        d["chg_begin"] = len(chunks)
+        d["chg_count"] = len(changes)
+        d["flags"] = 0 if base else 1  # fresh documents have the full hash graph
+        for c in changes:
+            chunks.append((off, len(c), 0))
+            parts.append(c)
+            off += len(c)
+        descs.append(d)
+    arena = np.frombuffer(b"".join(parts), dtype=np.uint8) if parts else np.zeros(1, np.uint8)
+    return arena, np.array(chunks, dtype=CHUNK_DT), np.array(descs, dtype=DOC_DT)
+
+
+class Batch:
+    def __init__(self, device=0):
+        self._eng = N.engine(device)
+        self._b = N.lib.am_batch_create(self._eng)
+        self.ndocs = 0
+        self.nchunks = 0
+
+    def __del__(self):
+        if getattr(self, "_b", None):
+            N.lib.am_batch_destroy(self._b)
+            self._b = None
+
+    def stage(self, arena, chunks, docs, known=None):
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        chunks = np.ascontiguousarray(chunks, dtype=CHUNK_DT)
+        docs = np.ascontiguousarray(docs, dtype=DOC_DT)
+        nk = 0 if known is None else len(known)
+        err = N.Error()
+        rc = N.lib.am_batch_stage(self._b, arena.ctypes.data, arena.nbytes, chunks.ctypes.data, len(chunks),
+                                  docs.ctypes.data, len(docs), None if known is None else known.ctypes.data, nk,
+                                  C.byref(err))
+        if rc:
+            N.raise_for(err)
+        self.ndocs = len(docs)
+        self.nchunks = len(chunks)
+        self._keep = (arena, chunks, docs, known)
+
+    def stage_docs(self, docs):
+        self.stage(*pack(docs))
+
+    def run(self):
+        if N.lib.am_batch_run(self._b):
+            raise N.AutomergeError("automerge_amd: kernel launch failed")
+
+    def sync(self):
+        err = N.Error()
+        if N.lib.am_batch_sync(self._b, C.byref(err)):
+            N.raise_for(err)
+
+    def results(self):
+        out = np.zeros(self.ndocs, RESULT_DT)
+        if self.ndocs and N.lib.am_batch_results(self._b, out.ctypes.data):
+            raise N.AutomergeError("automerge_amd: result copy failed")
+        return out
+
+    def chunk_results(self):
+        hashes = np.zeros((self.nchunks, 32), np.uint8)
+        state = np.zeros(self.nchunks, np.int32)
+        status = np.zeros(self.nchunks, np.uint32)
+        if self.nchunks and N.lib.am_batch_chunk_results(self._b, hashes.ctypes.data, state.ctypes.data,
+                                                         status.ctypes.data):
+            raise N.AutomergeError("automerge_amd: result copy failed")
+        return hashes, state, status
+
+    def doc_output(self, i, res=None):
+        n = C.c_uint64()
+        cap = int(res["out_len"]) if res is not None else 1 << 24
+        buf = (C.c_uint8 * max(cap, 1))()
+        rc = N.lib.am_batch_doc_output(self._b, i, buf, cap, C.byref(n))
+        if rc:
+            raise N.AutomergeError("automerge_amd: output copy failed (%d)" % rc)
+        return bytes(buf)[:n.value]
+
+    def doc_heads(self, i, nheads):
+        buf = (C.c_uint8 * (32 * max(nheads, 1)))()
+        n = C.c_uint32()
+        if N.lib.am_batch_doc_heads(self._b, i, buf, nheads, C.byref(n)):
+            raise N.AutomergeError("automerge_amd: heads copy failed")
+        raw = bytes(buf)
+        return [raw[32 * k:32 * k + 32].hex() for k in range(min(n.value, nheads))]
+
+    def stage_times(self):
+        ms = (C.c_float * 4)()
+        if N.lib.am_batch_stage_times(self._b, ms):
+            return None
+        return list(ms)
+
+    def workspace_bytes(self):
+        return N.lib.am_batch_workspace_bytes(self._b)

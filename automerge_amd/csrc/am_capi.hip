@@ -1,0 +1,818 @@
+// am_capi.hip -- host side of libautomerge_amd.so: engine/batch management, the DEFLATE host stage,
+// the per-document backend state (backend/backend.js semantics over the batch path) and error
+// messages. All merge/codec/hash work runs in the kernels of am_kernels.hip; nothing here decodes
+// op columns or merges operations. There is no CPU fallback: without a HIP device the entry points
+// fail with an error.
+#include <hip/hip_runtime.h>
+#include <zlib.h>
+
+#include <array>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "am_launch.h"
+
+namespace {
+
+struct Err {
+  uint32_t code = 0;
+  bool type_error = false;
+  std::string msg;
+};
+
+void to_c(const Err& e, am_error* out) {
+  if (!out) return;
+  out->code = e.code;
+  out->is_type_error = e.type_error ? 1 : 0;
+  std::snprintf(out->message, sizeof(out->message), "%s", e.msg.c_str());
+}
+
+std::string hexs(const uint8_t* p, size_t n) {
+  static const char* H = "0123456789abcdef";
+  std::string s;
+  s.reserve(2 * n);
+  for (size_t i = 0; i < n; i++) { s += H[p[i] >> 4]; s += H[p[i] & 15]; }
+  return s;
+}
+
+std::string fmt(const char* f, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, f);
+  std::vsnprintf(buf, sizeof buf, f, ap);
+  va_end(ap);
+  return buf;
+}
+
+std::string numOrNull(int64_t v, bool is_actor) {
+  if (is_actor ? v < 0 : v == AM_NULL64) return "null";
+  return std::to_string(v);
+}
+
+// Reference error text for a status code (messages of encoding.js / columnar.js / new.js).
+std::string message_for(uint32_t code, int64_t a0, int64_t a1, const std::string& actor) {
+  switch (code) {
+    case AM_E_MAGIC: return "Data does not begin with magic bytes 85 6f 4a 83";
+    case AM_E_CHECKSUM: return "checksum does not match data";
+    case AM_E_SUBARRAY: return "subarray exceeds buffer size";
+    case AM_E_LEB_RANGE: return "number out of range";
+    case AM_E_LEB_INCOMPLETE: return "buffer ended with incomplete number";
+    case AM_E_CHUNK_TYPE: return fmt("Unexpected chunk type: %lld", (long long)a0);
+    case AM_E_CHANGE_TRAILING: return "Encoded change has trailing data";
+    case AM_E_DOC_TRAILING: return "Encoded document has trailing data";
+    case AM_E_COL_ORDER: return "Columns must be in ascending order";
+    case AM_E_CHANGE_DEFLATED_COL: return "change must not contain deflated columns";
+    case AM_E_RLE_SUCC_REP: return "Successive repetitions with the same value are not allowed";
+    case AM_E_RLE_REP1: return "Repetition count of 1 is not allowed, use a literal instead";
+    case AM_E_RLE_SUCC_LIT: return "Successive literals are not allowed";
+    case AM_E_RLE_SUCC_NULL: return "Successive null runs are not allowed";
+    case AM_E_RLE_ZERO_NULL: return "Zero-length null runs are not allowed";
+    case AM_E_RLE_LIT_REP: return "Repetition of values is not allowed in literal";
+    case AM_E_BOOL_ZERO_RUN: return "Zero-length runs are not allowed";
+    case AM_E_REUSE_SEQ: return fmt("Reuse of sequence number %lld for actor %s", (long long)a0, actor.c_str());
+    case AM_E_SKIPPED_SEQ: return fmt("Skipped sequence number %lld for actor %s", (long long)a0, actor.c_str());
+    case AM_E_FIRST_SEQ: return fmt("Seq %lld is the first change for actor %s", (long long)a0, actor.c_str());
+    case AM_E_UNKNOWN_ACTOR: return fmt("actorId %s is not known to document", actor.c_str());
+    case AM_E_NO_ACTOR_INDEX: return fmt("No actor index %lld", (long long)a0);
+    case AM_E_MISMATCH_OBJ:
+      return "Mismatched object reference: (" + numOrNull(a0, false) + ", " + numOrNull(a1, true) + ")";
+    case AM_E_MISMATCH_KEY:
+      return "Mismatched operation key: (" + numOrNull(a0, false) + ", " + numOrNull(a1, true) + ")";
+    case AM_E_PRED_NOT_FOUND: return fmt("no matching operation for pred: %lld@%s", (long long)a0, actor.c_str());
+    case AM_E_REF_NOT_FOUND: return fmt("Reference element not found: %lld@%s", (long long)a0, actor.c_str());
+    case AM_E_ELEM_NOT_FOUND: return fmt("could not find list element with ID: %lld@%s", (long long)a0, actor.c_str());
+    case AM_E_DUP_OPID: return fmt("duplicate operation ID: %lld@%s", (long long)a0, actor.c_str());
+    case AM_E_DOC_SEQ:
+      return "Expected seq " + (a0 == AM_NULL64 ? std::string("NaN") : std::to_string(a0)) + ", got " +
+             std::to_string(a1) + " for actor " + actor;
+    case AM_U_HASH_GRAPH: return "automerge_amd: unsupported: needs the change hash graph of a loaded document";
+    case AM_U_UNKNOWN_COLUMN: return "automerge_amd: unsupported: column id outside the known column set";
+    case AM_U_NONCAUSAL: return "automerge_amd: unsupported: operation ids violate causal (Lamport) order";
+    case AM_U_UTF8: return "automerge_amd: unsupported: invalid UTF-8 in a key or message";
+    case AM_U_DEL_SHAPE: return "automerge_amd: unsupported: del operation without pred or with insert";
+    case AM_U_VALUE: return "automerge_amd: unsupported value shape in the input columns";
+    case AM_U_CAPACITY: return "automerge_amd: workspace capacity exceeded";
+    default: return fmt("automerge_amd: error %u", code);
+  }
+}
+
+#define HIPCHECK(expr)                                                                    \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess) {                                                               \
+      std::fprintf(stderr, "automerge_amd: %s failed: %s\n", #expr, hipGetErrorString(_e)); \
+      return false;                                                                       \
+    }                                                                                     \
+  } while (0)
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t n) {
+    if (n <= cap && p) return true;
+    if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+    size_t bytes = (n ? n : 1) * sizeof(T);
+    if (hipMalloc(&p, bytes) != hipSuccess) { p = nullptr; return false; }
+    cap = n ? n : 1;
+    return true;
+  }
+  ~DevBuf() { if (p) (void)hipFree(p); }
+};
+
+// ---- minimal host-side LEB128 / container handling for the DEFLATE stage ----
+struct HRd {
+  const uint8_t* p;
+  size_t n, off;
+  bool ok = true;
+  uint64_t u() {
+    uint64_t v = 0;
+    int sh = 0;
+    while (off < n) {
+      uint8_t b = p[off++];
+      if (sh < 64) v |= (uint64_t)(b & 0x7f) << sh;
+      sh += 7;
+      if (!(b & 0x80)) return v;
+    }
+    ok = false;
+    return 0;
+  }
+  const uint8_t* raw(size_t k) {
+    if (off + k > n) { ok = false; return p; }
+    const uint8_t* r = p + off;
+    off += k;
+    return r;
+  }
+};
+void put_u(std::vector<uint8_t>& o, uint64_t v) {
+  do { uint8_t b = v & 0x7f; v >>= 7; o.push_back(b | (v ? 0x80 : 0)); } while (v);
+}
+
+bool zinflate(const uint8_t* p, size_t n, std::vector<uint8_t>& out) {
+  size_t cap = n * 4 + 64;
+  for (int attempt = 0; attempt < 16; attempt++) {
+    out.resize(cap);
+    z_stream zs;
+    std::memset(&zs, 0, sizeof zs);
+    if (inflateInit2(&zs, -15) != Z_OK) return false;
+    zs.next_in = const_cast<Bytef*>(p);
+    zs.avail_in = (uInt)n;
+    zs.next_out = out.data();
+    zs.avail_out = (uInt)cap;
+    int r = inflate(&zs, Z_FINISH);
+    size_t got = zs.total_out;
+    inflateEnd(&zs);
+    if (r == Z_STREAM_END) { out.resize(got); return true; }
+    if (r == Z_BUF_ERROR && zs.avail_out == 0) { cap *= 4; continue; }
+    return false;
+  }
+  return false;
+}
+// pako.deflateRaw defaults: level 6, memLevel 8, windowBits 15 (raw), default strategy
+bool zdeflate(const uint8_t* p, size_t n, std::vector<uint8_t>& out) {
+  z_stream zs;
+  std::memset(&zs, 0, sizeof zs);
+  if (deflateInit2(&zs, 6, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+  out.resize(deflateBound(&zs, (uLong)n) + 16);
+  zs.next_in = const_cast<Bytef*>(p);
+  zs.avail_in = (uInt)n;
+  zs.next_out = out.data();
+  zs.avail_out = (uInt)out.size();
+  int r = deflate(&zs, Z_FINISH);
+  size_t got = zs.total_out;
+  deflateEnd(&zs);
+  if (r != Z_STREAM_END) return false;
+  out.resize(got);
+  return true;
+}
+
+struct ColEnt { uint64_t id; std::vector<uint8_t> data; };
+struct DocParts {
+  std::vector<uint8_t> pre;  // actors + heads (verbatim)
+  std::vector<ColEnt> ccols, ocols;
+  std::vector<uint8_t> post; // headsIndexes + extra bytes (verbatim)
+  uint32_t nheads = 0;
+  const uint8_t* heads = nullptr;
+};
+// Splits a document chunk's data (decodeDocumentHeader layout, columnar.js:1006-1038).
+bool split_doc(const uint8_t* data, size_t n, DocParts& d) {
+  HRd r{data, n, 0};
+  uint64_t na = r.u();
+  for (uint64_t i = 0; i < na && r.ok; i++) r.raw(r.u());
+  uint64_t nh = r.u();
+  d.heads = r.raw(32 * nh);
+  d.nheads = (uint32_t)nh;
+  d.pre.assign(data, data + r.off);
+  auto table = [&](std::vector<ColEnt>& cols) {
+    uint64_t nc = r.u();
+    for (uint64_t i = 0; i < nc && r.ok; i++) {
+      ColEnt c;
+      c.id = r.u();
+      c.data.resize(r.u());
+      cols.push_back(std::move(c));
+    }
+  };
+  table(d.ccols);
+  table(d.ocols);
+  for (auto* cols : {&d.ccols, &d.ocols})
+    for (auto& c : *cols) {
+      const uint8_t* p = r.raw(c.data.size());
+      if (!r.ok) return false;
+      if (!c.data.empty()) std::memcpy(c.data.data(), p, c.data.size());
+    }
+  d.post.assign(data + r.off, data + n);
+  return r.ok;
+}
+std::vector<uint8_t> join_doc(const DocParts& d) {
+  std::vector<uint8_t> body(d.pre);
+  for (auto* cols : {&d.ccols, &d.ocols}) {
+    put_u(body, cols->size());
+    for (auto& c : *cols) { put_u(body, c.id); put_u(body, c.data.size()); }
+  }
+  for (auto* cols : {&d.ccols, &d.ocols})
+    for (auto& c : *cols) body.insert(body.end(), c.data.begin(), c.data.end());
+  body.insert(body.end(), d.post.begin(), d.post.end());
+  return body;
+}
+
+struct Container {
+  uint8_t type = 0;
+  size_t data_off = 0, data_len = 0, end = 0;
+};
+bool read_container(const uint8_t* p, size_t n, Container& c) {
+  if (n < 9) return false;
+  HRd r{p, n, 9};
+  c.type = p[8];
+  c.data_len = r.u();
+  c.data_off = r.off;
+  r.raw(c.data_len);
+  c.end = r.off;
+  return r.ok;
+}
+std::vector<uint8_t> make_chunk(const uint8_t checksum[4], uint8_t type, const std::vector<uint8_t>& data) {
+  std::vector<uint8_t> o = {0x85, 0x6f, 0x4a, 0x83, checksum[0], checksum[1], checksum[2], checksum[3], type};
+  put_u(o, data.size());
+  o.insert(o.end(), data.begin(), data.end());
+  return o;
+}
+
+}  // namespace
+
+// =============================================================================================
+// engine / batch
+// =============================================================================================
+struct am_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[5] = {};
+  am_batch* scratch = nullptr;  // batch reused by the per-document API
+};
+
+struct am_batch {
+  am_engine* eng = nullptr;
+  DevBuf<uint8_t> arena;
+  DevBuf<am_chunk_desc> chunks;
+  DevBuf<am_doc_desc> docs;
+  DevBuf<am_known_hash> known;
+  DevBuf<ChunkInfo> info;
+  DevBuf<DocBounds> bounds;
+  DevBuf<uint64_t> ws_bytes, ws_off, scan_tmp, ws_total;
+  DevBuf<uint8_t> ws;
+  DevBuf<am_doc_result> results;
+  DevBuf<int32_t> chg_state;
+  uint32_t nchunks = 0, ndocs = 0;
+  uint64_t ws_need = 0;
+  bool timed = false;
+
+  BatchDev dev() {
+    BatchDev b;
+    b.arena = arena.p; b.chunks = chunks.p; b.docs = docs.p; b.known = known.p; b.info = info.p; b.bounds = bounds.p;
+    b.ws_bytes = ws_bytes.p; b.ws_off = ws_off.p; b.scan_tmp = scan_tmp.p; b.ws_total = ws_total.p; b.ws = ws.p;
+    b.ws_cap = ws.cap; b.results = results.p; b.chg_state = chg_state.p; b.nchunks = nchunks; b.ndocs = ndocs;
+    return b;
+  }
+};
+
+static bool set_device(am_engine* e) { return hipSetDevice(e->device) == hipSuccess; }
+
+extern "C" const char* am_version(void) { return "automerge_amd 0.1 (gfx950)"; }
+
+extern "C" am_engine* am_engine_create(int device, am_error* err) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) {
+    Err e{AM_U_CAPACITY, false, "automerge_amd: no HIP device available (MI355X required; no CPU fallback)"};
+    to_c(e, err);
+    return nullptr;
+  }
+  am_engine* eng = new am_engine();
+  eng->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&eng->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete eng;
+    Err e{AM_U_CAPACITY, false, "automerge_amd: cannot create a HIP stream"};
+    to_c(e, err);
+    return nullptr;
+  }
+  for (auto& ev : eng->ev) (void)hipEventCreate(&ev);
+  if (err) err->code = 0;
+  return eng;
+}
+
+extern "C" void am_batch_destroy(am_batch* b) {
+  if (!b) return;
+  set_device(b->eng);
+  delete b;
+}
+
+extern "C" void am_engine_destroy(am_engine* eng) {
+  if (!eng) return;
+  set_device(eng);
+  am_batch_destroy(eng->scratch);
+  for (auto& ev : eng->ev) (void)hipEventDestroy(ev);
+  (void)hipStreamDestroy(eng->stream);
+  delete eng;
+}
+
+extern "C" am_batch* am_batch_create(am_engine* eng) {
+  am_batch* b = new am_batch();
+  b->eng = eng;
+  return b;
+}
+
+static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, const am_chunk_desc* chunks, uint32_t nchunks,
+                       const am_doc_desc* docs, uint32_t ndocs, const am_known_hash* known, uint32_t nknown) {
+  am_engine* e = b->eng;
+  if (!set_device(e)) return false;
+  hipStream_t s = e->stream;
+  if (!b->arena.ensure(arena_len) || !b->chunks.ensure(nchunks) || !b->docs.ensure(ndocs) || !b->known.ensure(nknown) ||
+      !b->info.ensure(nchunks) || !b->bounds.ensure(ndocs) || !b->ws_bytes.ensure(ndocs) || !b->ws_off.ensure(ndocs) ||
+      !b->scan_tmp.ensure(am_scan_tmp_elems(ndocs)) || !b->ws_total.ensure(1) || !b->results.ensure(ndocs) ||
+      !b->chg_state.ensure(nchunks))
+    return false;
+  if (arena_len) HIPCHECK(hipMemcpyAsync(b->arena.p, arena, arena_len, hipMemcpyHostToDevice, s));
+  if (nchunks) HIPCHECK(hipMemcpyAsync(b->chunks.p, chunks, sizeof(am_chunk_desc) * nchunks, hipMemcpyHostToDevice, s));
+  if (ndocs) HIPCHECK(hipMemcpyAsync(b->docs.p, docs, sizeof(am_doc_desc) * ndocs, hipMemcpyHostToDevice, s));
+  if (nknown) HIPCHECK(hipMemcpyAsync(b->known.p, known, sizeof(am_known_hash) * nknown, hipMemcpyHostToDevice, s));
+  b->nchunks = nchunks;
+  b->ndocs = ndocs;
+  // sizing pass: chunk counts -> per-document workspace bounds -> total
+  BatchDev d = b->dev();
+  am_launch_chunks(d, s);
+  am_launch_bounds(d, s);
+  uint64_t total = 0;
+  if (ndocs) HIPCHECK(hipMemcpyAsync(&total, b->ws_total.p, sizeof total, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  HIPCHECK(hipGetLastError());
+  b->ws_need = total;
+  if (!b->ws.ensure(total + 16)) return false;
+  return true;
+}
+
+extern "C" int am_batch_stage(am_batch* b, const uint8_t* arena, uint64_t arena_len, const am_chunk_desc* chunks,
+                              uint32_t nchunks, const am_doc_desc* docs, uint32_t ndocs, const am_known_hash* known,
+                              uint32_t nknown, am_error* err) {
+  if (!stage_impl(b, arena, arena_len, chunks, nchunks, docs, ndocs, known, nknown)) {
+    to_c(Err{AM_U_CAPACITY, false, "automerge_amd: device allocation or copy failed"}, err);
+    return 1;
+  }
+  if (err) err->code = 0;
+  return 0;
+}
+
+extern "C" int am_batch_run(am_batch* b) {
+  am_engine* e = b->eng;
+  if (!set_device(e)) return 1;
+  hipStream_t s = e->stream;
+  BatchDev d = b->dev();
+  (void)hipEventRecord(e->ev[0], s);
+  am_launch_chunks(d, s);
+  (void)hipEventRecord(e->ev[1], s);
+  am_launch_bounds(d, s);
+  (void)hipEventRecord(e->ev[2], s);
+  am_launch_doc(d, s);
+  (void)hipEventRecord(e->ev[3], s);
+  am_launch_out_hash(d, s);
+  (void)hipEventRecord(e->ev[4], s);
+  b->timed = true;
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+extern "C" int am_batch_sync(am_batch* b, am_error* err) {
+  if (!set_device(b->eng)) return 1;
+  hipError_t r = hipStreamSynchronize(b->eng->stream);
+  if (r != hipSuccess) {
+    to_c(Err{AM_U_CAPACITY, false, std::string("automerge_amd: HIP error: ") + hipGetErrorString(r)}, err);
+    return 1;
+  }
+  if (err) err->code = 0;
+  return 0;
+}
+
+extern "C" int am_batch_results(am_batch* b, am_doc_result* out) {
+  if (!set_device(b->eng) || !b->ndocs) return b->ndocs ? 1 : 0;
+  return hipMemcpy(out, b->results.p, sizeof(am_doc_result) * b->ndocs, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+
+extern "C" int am_batch_chunk_results(am_batch* b, uint8_t* hashes32, int32_t* chg_state, uint32_t* status) {
+  if (!set_device(b->eng)) return 1;
+  if (!b->nchunks) return 0;
+  std::vector<ChunkInfo> info(b->nchunks);
+  if (hipMemcpy(info.data(), b->info.p, sizeof(ChunkInfo) * b->nchunks, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  if (chg_state && hipMemcpy(chg_state, b->chg_state.p, sizeof(int32_t) * b->nchunks, hipMemcpyDeviceToHost) != hipSuccess)
+    return 1;
+  for (uint32_t i = 0; i < b->nchunks; i++) {
+    if (hashes32) std::memcpy(hashes32 + 32 * i, info[i].hash, 32);
+    if (status) status[i] = info[i].status;
+  }
+  return 0;
+}
+
+extern "C" int am_batch_doc_output(am_batch* b, uint32_t doc, uint8_t* dst, uint64_t cap, uint64_t* len) {
+  if (!set_device(b->eng) || doc >= b->ndocs) return 1;
+  am_doc_result r;
+  if (hipMemcpy(&r, b->results.p + doc, sizeof r, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  *len = r.out_len;
+  if (!r.out_len) return 0;
+  if (cap < r.out_len) return 2;
+  return hipMemcpy(dst, b->ws.p + r.out_off, r.out_len, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+
+extern "C" int am_batch_doc_heads(am_batch* b, uint32_t doc, uint8_t* dst32, uint32_t cap, uint32_t* n) {
+  if (!set_device(b->eng) || doc >= b->ndocs) return 1;
+  am_doc_result r;
+  DocBounds bd;
+  if (hipMemcpy(&r, b->results.p + doc, sizeof r, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  if (hipMemcpy(&bd, b->bounds.p + doc, sizeof bd, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  *n = r.nheads;
+  if (!r.nheads || r.status) return 0;
+  WsLayout L = ws_layout(bd);
+  uint32_t k = r.nheads < cap ? r.nheads : cap;
+  return hipMemcpy(dst32, b->ws.p + r.ws_off + L.heads, 32ull * k, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+
+extern "C" int am_batch_stage_times(am_batch* b, float* ms4) {
+  if (!b->timed) return 1;
+  for (int i = 0; i < 4; i++) {
+    if (hipEventElapsedTime(&ms4[i], b->eng->ev[i], b->eng->ev[i + 1]) != hipSuccess) return 1;
+  }
+  return 0;
+}
+
+extern "C" uint64_t am_batch_workspace_bytes(am_batch* b) { return b->ws_need; }
+
+// =============================================================================================
+// per-document backend state (backend/backend.js + BackendDoc over the batch path, n = 1)
+// =============================================================================================
+struct am_doc {
+  am_engine* eng = nullptr;
+  std::vector<uint8_t> state;   // merged document chunk, uncompressed columns (empty = Backend.init())
+  std::vector<uint8_t> binary;  // save() cache: the loaded buffer until the first applyChanges (new.js:1712,1859)
+  bool has_binary = false;
+  bool have_hash_graph = true;  // new.js:1697,1752
+  std::vector<std::vector<uint8_t>> changes;           // applied change buffers (this.changes)
+  std::vector<std::array<uint8_t, 32>> hashes;         // their hashes
+  std::vector<std::vector<uint8_t>> queue;             // enqueued change buffers (this.queue)
+  std::vector<std::array<uint8_t, 32>> heads;
+  int64_t max_op = 0;
+  size_t nchanges = 0;
+};
+
+namespace {
+
+am_batch* scratch_batch(am_engine* e) {
+  if (!e->scratch) e->scratch = am_batch_create(e);
+  return e->scratch;
+}
+
+// Host stage for one change buffer: DEFLATE-compressed changes (chunk type 2) are inflated into
+// an uncompressed type-1 chunk that keeps the original checksum (inflateChange, columnar.js:813).
+bool stage_change(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, Err& err) {
+  if (in.size() > 8 && in[8] == 2) {
+    if (in.size() < 4 || std::memcmp(in.data(), "\x85\x6f\x4a\x83", 4) != 0) {
+      err = {AM_E_MAGIC, false, message_for(AM_E_MAGIC, 0, 0, "")};
+      return false;
+    }
+    Container c;
+    if (!read_container(in.data(), in.size(), c)) {
+      err = {AM_E_SUBARRAY, false, message_for(AM_E_SUBARRAY, 0, 0, "")};
+      return false;
+    }
+    std::vector<uint8_t> dec;
+    if (!zinflate(in.data() + c.data_off, c.data_len, dec)) {
+      err = {AM_E_SUBARRAY, false, "invalid deflate data"};
+      return false;
+    }
+    out = make_chunk(in.data() + 4, 1, dec);
+    return true;
+  }
+  out = in;
+  return true;
+}
+
+struct OneResult {
+  am_doc_result r;
+  std::vector<uint8_t> out;
+  std::vector<int32_t> chg_state;
+  std::vector<std::array<uint8_t, 32>> hashes;
+  std::vector<std::array<uint8_t, 32>> heads;
+};
+
+// Runs one document (optional base chunk + change list) through the GPU pipeline.
+bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified, const std::vector<std::vector<uint8_t>>& chg,
+             const std::vector<am_known_hash>& known, bool have_graph, OneResult& res, std::vector<uint8_t>& arena, Err& err) {
+  arena.clear();
+  std::vector<am_chunk_desc> cds;
+  am_doc_desc dd{};
+  dd.base_chunk = -1;
+  if (base && !base->empty()) {
+    cds.push_back({arena.size(), (uint32_t)base->size(), base_verified ? 1u : 0u});
+    arena.insert(arena.end(), base->begin(), base->end());
+    dd.base_chunk = 0;
+  }
+  dd.chg_begin = (uint32_t)cds.size();
+  dd.chg_count = (uint32_t)chg.size();
+  for (auto& c : chg) {
+    cds.push_back({arena.size(), (uint32_t)c.size(), 0});
+    arena.insert(arena.end(), c.begin(), c.end());
+  }
+  dd.known_begin = 0;
+  dd.known_count = (uint32_t)known.size();
+  dd.flags = have_graph ? 1 : 0;
+  am_batch* b = scratch_batch(e);
+  am_error ce;
+  if (am_batch_stage(b, arena.data(), arena.size(), cds.data(), (uint32_t)cds.size(), &dd, 1, known.data(),
+                     (uint32_t)known.size(), &ce) ||
+      am_batch_run(b) || am_batch_sync(b, &ce) || am_batch_results(b, &res.r)) {
+    err = {AM_U_CAPACITY, false, std::string("automerge_amd: GPU pipeline failed: ") + ce.message};
+    return false;
+  }
+  res.chg_state.assign(cds.size(), 0);
+  std::vector<uint8_t> hs(32 * cds.size());
+  std::vector<uint32_t> st(cds.size());
+  if (!cds.empty() && am_batch_chunk_results(b, hs.data(), res.chg_state.data(), st.data())) {
+    err = {AM_U_CAPACITY, false, "automerge_amd: result copy failed"};
+    return false;
+  }
+  res.hashes.resize(cds.size());
+  for (size_t i = 0; i < cds.size(); i++) std::memcpy(res.hashes[i].data(), hs.data() + 32 * i, 32);
+  if (res.r.status) {
+    std::string actor;
+    if (res.r.arg_actor_len && res.r.arg_actor_off + res.r.arg_actor_len <= arena.size())
+      actor = hexs(arena.data() + res.r.arg_actor_off, res.r.arg_actor_len);
+    err = {res.r.status, false, message_for(res.r.status, res.r.arg0, res.r.arg1, actor)};
+    return false;
+  }
+  res.out.resize(res.r.out_len);
+  uint64_t len = 0;
+  if (am_batch_doc_output(b, 0, res.out.data(), res.out.size(), &len)) {
+    err = {AM_U_CAPACITY, false, "automerge_amd: output copy failed"};
+    return false;
+  }
+  std::vector<uint8_t> hb(32 * (res.r.nheads + 1));
+  uint32_t nh = 0;
+  am_batch_doc_heads(b, 0, hb.data(), res.r.nheads, &nh);
+  res.heads.resize(nh);
+  for (uint32_t i = 0; i < nh; i++) std::memcpy(res.heads[i].data(), hb.data() + 32 * i, 32);
+  return true;
+}
+
+bool gpu_sha256(am_engine* e, const std::vector<const std::vector<uint8_t>*>& msgs, size_t skip,
+                std::vector<std::array<uint8_t, 32>>& out) {
+  std::vector<uint8_t> arena;
+  std::vector<am_chunk_desc> d;
+  for (auto* m : msgs) {
+    size_t n = m->size() > skip ? m->size() - skip : 0;
+    d.push_back({arena.size(), (uint32_t)n, 0});
+    arena.insert(arena.end(), m->begin() + (m->size() > skip ? skip : m->size()), m->end());
+  }
+  if (!set_device(e)) return false;
+  DevBuf<uint8_t> da;
+  DevBuf<am_chunk_desc> dd;
+  DevBuf<uint8_t> dout;
+  if (!da.ensure(arena.size()) || !dd.ensure(d.size()) || !dout.ensure(32 * d.size())) return false;
+  hipStream_t s = e->stream;
+  if (!arena.empty()) HIPCHECK(hipMemcpyAsync(da.p, arena.data(), arena.size(), hipMemcpyHostToDevice, s));
+  HIPCHECK(hipMemcpyAsync(dd.p, d.data(), sizeof(am_chunk_desc) * d.size(), hipMemcpyHostToDevice, s));
+  am_launch_sha256(da.p, dd.p, (uint32_t)d.size(), dout.p, s);
+  std::vector<uint8_t> h(32 * d.size());
+  HIPCHECK(hipMemcpyAsync(h.data(), dout.p, h.size(), hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  out.resize(d.size());
+  for (size_t i = 0; i < d.size(); i++) std::memcpy(out[i].data(), h.data() + 32 * i, 32);
+  return true;
+}
+
+// Host stage of Backend.load for documents with DEFLATE-compressed columns: the checksum of the
+// original chunk is verified on the GPU, then the columns are inflated (inflateColumn,
+// columnar.js:1062) into an uncompressed chunk marked as verified.
+bool stage_doc(am_engine* e, const std::vector<uint8_t>& in, std::vector<uint8_t>& out, bool& verified, Err& err) {
+  verified = false;
+  Container c;
+  if (in.size() < 4 || std::memcmp(in.data(), "\x85\x6f\x4a\x83", 4) != 0 || !read_container(in.data(), in.size(), c) ||
+      c.type != 0) {
+    out = in;  // let the GPU report the exact error
+    return true;
+  }
+  DocParts parts;
+  if (!split_doc(in.data() + c.data_off, c.data_len, parts)) { out = in; return true; }
+  bool any = false;
+  for (auto* cols : {&parts.ccols, &parts.ocols})
+    for (auto& col : *cols) any |= (col.id & COL_DEFLATE) != 0;
+  if (!any) { out = in; return true; }
+  std::vector<std::array<uint8_t, 32>> h;
+  if (!gpu_sha256(e, {&in}, 8, h)) { err = {AM_U_CAPACITY, false, "automerge_amd: GPU hash failed"}; return false; }
+  std::vector<uint8_t> whole(in.begin() + 8, in.begin() + c.end);
+  std::vector<std::array<uint8_t, 32>> hh;
+  if (!gpu_sha256(e, {&whole}, 0, hh)) { err = {AM_U_CAPACITY, false, "automerge_amd: GPU hash failed"}; return false; }
+  if (std::memcmp(hh[0].data(), in.data() + 4, 4) != 0) {
+    err = {AM_E_CHECKSUM, false, message_for(AM_E_CHECKSUM, 0, 0, "")};
+    return false;
+  }
+  for (auto* cols : {&parts.ccols, &parts.ocols})
+    for (auto& col : *cols)
+      if (col.id & COL_DEFLATE) {
+        std::vector<uint8_t> dec;
+        if (!zinflate(col.data.data(), col.data.size(), dec)) { err = {AM_E_SUBARRAY, false, "invalid deflate data"}; return false; }
+        col.data = std::move(dec);
+        col.id ^= COL_DEFLATE;
+      }
+  out = make_chunk(in.data() + 4, 0, join_doc(parts));
+  verified = true;
+  return true;
+}
+
+}  // namespace
+
+extern "C" am_doc* am_doc_init(am_engine* eng) {
+  am_doc* d = new am_doc();
+  d->eng = eng;
+  return d;
+}
+
+extern "C" am_doc* am_doc_clone(const am_doc* s) { return new am_doc(*s); }
+extern "C" void am_doc_free(am_doc* d) { delete d; }
+extern "C" void am_free(void* p) { std::free(p); }
+
+// Backend.load (backend/backend.js:104-107 -> new BackendDoc(buffer), new.js:1709-1750)
+extern "C" am_doc* am_doc_load(am_engine* eng, const uint8_t* data, size_t len, am_error* err) {
+  Err e;
+  std::vector<uint8_t> in(data, data + len), staged, arena;
+  bool verified = false;
+  if (!stage_doc(eng, in, staged, verified, e)) { to_c(e, err); return nullptr; }
+  OneResult res;
+  if (!run_one(eng, &staged, verified, {}, {}, false, res, arena, e)) { to_c(e, err); return nullptr; }
+  am_doc* d = new am_doc();
+  d->eng = eng;
+  d->state = std::move(res.out);
+  d->binary = in;
+  d->has_binary = true;
+  d->have_hash_graph = false;
+  d->heads = res.heads;
+  d->nchanges = res.r.nchanges;
+  d->max_op = 0;
+  // maxOp of a loaded document: the largest op counter in ids and succs (documentPatch, new.js:1627-1630)
+  d->max_op = res.r.max_op;
+  if (err) err->code = 0;
+  return d;
+}
+
+// Backend.applyChanges (backend/backend.js:27-32 -> BackendDoc.applyChanges, new.js:1796-1871)
+extern "C" int am_doc_apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* lens, size_t n, am_error* err) {
+  Err e;
+  // decoded changes first, then the existing queue (new.js:1814)
+  std::vector<std::vector<uint8_t>> orig, staged;
+  for (size_t i = 0; i < n; i++) orig.emplace_back(bufs[i], bufs[i] + lens[i]);
+  for (auto& q : d->queue) orig.push_back(q);
+  for (auto& o : orig) {
+    std::vector<uint8_t> s;
+    if (!stage_change(o, s, e)) { to_c(e, err); return 1; }
+    staged.push_back(std::move(s));
+  }
+  std::vector<am_known_hash> known;
+  if (d->have_hash_graph) {
+    for (size_t i = 0; i < d->hashes.size(); i++) {
+      am_known_hash k;
+      std::memcpy(k.hash, d->hashes[i].data(), 32);
+      k.index = (int64_t)i;
+      known.push_back(k);
+    }
+  }
+  OneResult res;
+  std::vector<uint8_t> arena;
+  if (!run_one(d->eng, d->state.empty() ? nullptr : &d->state, false, staged, known, d->have_hash_graph, res, arena, e)) {
+    to_c(e, err);
+    return 1;
+  }
+  // commit (new.js:1838-1860)
+  const size_t base = d->state.empty() ? 0 : 1;
+  std::vector<size_t> applied(res.r.napplied);
+  std::vector<std::vector<uint8_t>> newq;
+  for (size_t i = 0; i < orig.size(); i++) {
+    int32_t st = res.chg_state[base + i];
+    if (st >= 0) applied[(size_t)st] = i;
+    else if (st == CHG_QUEUED) newq.push_back(orig[i]);
+  }
+  for (size_t k = 0; k < applied.size(); k++) {
+    d->changes.push_back(orig[applied[k]]);
+    d->hashes.push_back(res.hashes[base + applied[k]]);
+  }
+  d->queue = std::move(newq);
+  d->state = std::move(res.out);
+  d->heads = res.heads;
+  d->has_binary = false;
+  d->binary.clear();
+  d->nchanges = res.r.nchanges;
+  if (res.r.max_op > d->max_op) d->max_op = res.r.max_op;
+  if (err) err->code = 0;
+  return 0;
+}
+
+// Backend.save (new.js:2025-2047): DEFLATE of columns >= 256 bytes is the host stage; the
+// container checksum of the compressed form is computed on the GPU.
+extern "C" int am_doc_save(am_doc* d, uint8_t** out, size_t* len, am_error* err) {
+  std::vector<uint8_t> bytes;
+  if (d->has_binary) {
+    bytes = d->binary;
+  } else if (d->state.empty()) {
+    // Backend.init() saved: produce through the pipeline (no base, no changes)
+    OneResult res;
+    std::vector<uint8_t> arena;
+    Err e;
+    if (!run_one(d->eng, nullptr, false, {}, {}, true, res, arena, e)) { to_c(e, err); return 1; }
+    bytes = res.out;
+  } else {
+    Container c;
+    DocParts parts;
+    if (!read_container(d->state.data(), d->state.size(), c) || !split_doc(d->state.data() + c.data_off, c.data_len, parts)) {
+      to_c(Err{AM_U_VALUE, false, "automerge_amd: corrupt internal state"}, err);
+      return 1;
+    }
+    bool any = false;
+    for (auto* cols : {&parts.ccols, &parts.ocols})
+      for (auto& col : *cols)
+        if (col.data.size() >= 256) {  // DEFLATE_MIN_SIZE (columnar.js:32)
+          std::vector<uint8_t> z;
+          if (!zdeflate(col.data.data(), col.data.size(), z)) { to_c(Err{AM_U_VALUE, false, "deflate failed"}, err); return 1; }
+          col.data = std::move(z);
+          col.id |= COL_DEFLATE;
+          any = true;
+        }
+    if (!any) {
+      bytes = d->state;
+    } else {
+      std::vector<uint8_t> body = join_doc(parts);
+      uint8_t zero[4] = {0, 0, 0, 0};
+      bytes = make_chunk(zero, 0, body);
+      std::vector<std::array<uint8_t, 32>> h;
+      if (!gpu_sha256(d->eng, {&bytes}, 8, h)) { to_c(Err{AM_U_CAPACITY, false, "automerge_amd: GPU hash failed"}, err); return 1; }
+      std::memcpy(bytes.data() + 4, h[0].data(), 4);
+    }
+    d->binary = bytes;
+    d->has_binary = true;
+  }
+  *out = (uint8_t*)std::malloc(bytes.size() ? bytes.size() : 1);
+  if (!bytes.empty()) std::memcpy(*out, bytes.data(), bytes.size());
+  *len = bytes.size();
+  if (err) err->code = 0;
+  return 0;
+}
+
+extern "C" size_t am_doc_get_heads(const am_doc* d, uint8_t* out32, size_t cap) {
+  for (size_t i = 0; i < d->heads.size() && i < cap; i++) std::memcpy(out32 + 32 * i, d->heads[i].data(), 32);
+  return d->heads.size();
+}
+extern "C" size_t am_doc_pending(const am_doc* d) { return d->queue.size(); }
+extern "C" int64_t am_doc_max_op(const am_doc* d) { return d->max_op; }
+extern "C" size_t am_doc_num_changes(const am_doc* d) { return d->nchanges; }
+extern "C" int am_doc_change(const am_doc* d, size_t i, const uint8_t** data, size_t* len, uint8_t* hash32) {
+  if (i >= d->changes.size()) return 1;
+  *data = d->changes[i].data();
+  *len = d->changes[i].size();
+  if (hash32) std::memcpy(hash32, d->hashes[i].data(), 32);
+  return 0;
+}
+
+extern "C" int am_change_hashes(am_engine* eng, const uint8_t* const* bufs, const size_t* lens, size_t n, uint8_t* out32,
+                                am_error* err) {
+  std::vector<std::vector<uint8_t>> staged(n);
+  std::vector<const std::vector<uint8_t>*> ptrs;
+  for (size_t i = 0; i < n; i++) {
+    Err e;
+    std::vector<uint8_t> in(bufs[i], bufs[i] + lens[i]);
+    if (!stage_change(in, staged[i], e)) { to_c(e, err); return 1; }
+    Container c;
+    if (!read_container(staged[i].data(), staged[i].size(), c)) {
+      to_c(Err{AM_E_SUBARRAY, false, message_for(AM_E_SUBARRAY, 0, 0, "")}, err);
+      return 1;
+    }
+    staged[i].resize(c.end);
+    ptrs.push_back(&staged[i]);
+  }
+  std::vector<std::array<uint8_t, 32>> h;
+  if (!gpu_sha256(eng, ptrs, 8, h)) { to_c(Err{AM_U_CAPACITY, false, "automerge_amd: GPU hash failed"}, err); return 1; }
+  for (size_t i = 0; i < n; i++) std::memcpy(out32 + 32 * i, h[i].data(), 32);
+  if (err) err->code = 0;
+  return 0;
+}

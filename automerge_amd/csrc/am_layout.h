@@ -1,0 +1,119 @@
+// am_layout.h -- per-document workspace layout (host + device). Every region is bounded from
+// the per-chunk counts of k_chunks, so one exclusive scan sizes the whole batch.
+#pragma once
+#include <stdint.h>
+
+#include "am_common.h"
+
+#ifndef __HIPCC__
+#define AM_HD
+#else
+#define AM_HD __host__ __device__
+#endif
+
+struct DocBounds {
+  uint32_t R;   // op rows (base + every change in the list)
+  uint32_t E;   // pred/succ entries
+  uint32_t C;   // document change rows
+  uint32_t D;   // depsIndex entries
+  uint32_t A;   // actor table
+  uint32_t H;   // heads
+  uint32_t N;   // changes in the list
+  uint32_t K;   // changeIndexByHash entries
+  uint32_t AM;  // actor-map entries (sum of change actor lists)
+  uint32_t overflow;
+  uint64_t S;   // key + message string bytes over all rows
+  uint64_t B;   // input bytes (base + changes)
+};
+
+struct WsLayout {
+  uint64_t rows, ents, idk, elemk, sortrec, newent, elem_of, parent, first_child, next_sib, tour_nxt, tour_w, scan,
+      succ_cnt, outent, chg, deps, actors, clock, heads, hidx, htab, chghdr, order, rowbase, entbase, ambase, amap,
+      queue, enq, scratch, scratch_stride, out, out_cap, total;
+  uint64_t colbuf[OC_NCOLS + DC_NCOLS];
+};
+
+AM_HD inline uint32_t am_pow2(uint32_t n) {
+  uint32_t p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+// sizes of the device structs (kept in sync by static_asserts in am_kernels.hip)
+#define AM_SZ_ROW 96
+#define AM_SZ_ENT 16
+#define AM_SZ_IDKEY 16
+#define AM_SZ_ELEMKEY 32
+#define AM_SZ_SORTREC 56
+#define AM_SZ_NEWENT 24
+#define AM_SZ_CHGROW 80
+#define AM_SZ_ACTORREF 16
+#define AM_SZ_HENT 40
+#define AM_SZ_CHGHDR 288
+
+AM_HD inline WsLayout ws_layout(const DocBounds& b) {
+  WsLayout L;
+  uint64_t o = 0;
+  auto take = [&](uint64_t bytes) { uint64_t at = o; o += (bytes + 15) & ~(uint64_t)15; return at; };
+  const uint64_t R = b.R, E = b.E, C = b.C, D = b.D;
+  const uint64_t PR = am_pow2(b.R ? b.R : 1), PE = am_pow2(b.E ? b.E : 1);
+  L.rows = take(R * AM_SZ_ROW);
+  L.ents = take(E * AM_SZ_ENT);
+  L.idk = take(PR * AM_SZ_IDKEY);
+  L.elemk = take(PR * AM_SZ_ELEMKEY);
+  L.sortrec = take(PR * AM_SZ_SORTREC);
+  L.newent = take(PE * AM_SZ_NEWENT);
+  L.elem_of = take(R * 4);
+  L.parent = take(R * 4);
+  L.first_child = take(R * 4);
+  L.next_sib = take(R * 4);
+  L.tour_nxt = take(4 * R * 4);
+  L.tour_w = take(4 * R * 4);
+  L.scan = take(R * 4);
+  L.succ_cnt = take(R * 4);
+  L.outent = take(E * AM_SZ_ENT);
+  L.chg = take(C * AM_SZ_CHGROW);
+  L.deps = take(D * 8);
+  L.actors = take((uint64_t)b.A * AM_SZ_ACTORREF);
+  L.clock = take((uint64_t)b.A * 8);
+  L.heads = take((uint64_t)b.H * 32);
+  L.hidx = take((uint64_t)b.H * 8);
+  L.htab = take((uint64_t)b.K * AM_SZ_HENT);
+  L.chghdr = take((uint64_t)b.N * AM_SZ_CHGHDR);
+  L.order = take((uint64_t)b.N * 4);
+  L.rowbase = take((uint64_t)b.N * 4);
+  L.entbase = take((uint64_t)b.N * 4);
+  L.ambase = take((uint64_t)b.N * 4);
+  L.amap = take((uint64_t)b.AM * 4);
+  L.queue = take((uint64_t)b.N * 4);
+  L.enq = take((uint64_t)b.N * 4);
+  uint64_t stride = R;
+  if (E > stride) stride = E;
+  if (C > stride) stride = C;
+  if (D > stride) stride = D;
+  L.scratch_stride = stride;
+  L.scratch = take(8 * stride * 8);
+  // column buffers: a value costs at most 8 LEB bytes plus 2 bytes of RLE headers
+  uint64_t cap = 0;
+  for (int c = 0; c < OC_NCOLS + DC_NCOLS; c++) {
+    uint64_t bound;
+    if (c == OC_KEY_STR) bound = 10 * R + b.S;
+    else if (c == OC_VAL_RAW) bound = b.B;
+    else if (c == OC_INSERT) bound = 10 * (R + 1);
+    else if (c == OC_GRP_ACTOR || c == OC_GRP_CTR) bound = 10 * E;
+    else if (c < OC_NCOLS) bound = 10 * R;
+    else if (c == OC_NCOLS + DC_MESSAGE) bound = 10 * C + b.S;
+    else if (c == OC_NCOLS + DC_DEPS_INDEX) bound = 10 * D;
+    else if (c == OC_NCOLS + DC_EXTRA_RAW) bound = b.B;
+    else bound = 10 * C;
+    bound += 16;
+    L.colbuf[c] = take(bound);
+    cap += bound;
+  }
+  // document: header + actor ids + heads + column table + data + headsIndexes + extra bytes
+  cap += 64 + 10 * (uint64_t)b.A + b.B + 42 * (uint64_t)b.H + 25 * 20 + b.B;
+  L.out_cap = cap;
+  L.out = take(cap);
+  L.total = o;
+  return L;
+}

