@@ -74,6 +74,10 @@ _sigs = {
     "am_doc_change": (C.c_int, [P, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), P]),
     "am_free": (None, [P]),
     "am_change_hashes": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t, P, C.POINTER(Error)]),
+    "am_stage_change": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
+    "am_stage_document": (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t),
+                                    C.POINTER(C.c_int), C.POINTER(Error)]),
+    "am_workload_c4": (C.c_uint64, [C.c_uint64, C.c_uint32, P, C.c_uint64, P, P, C.POINTER(C.c_uint64), C.c_int]),
 }
 for _name, (_res, _args) in _sigs.items():
     _f = getattr(lib, _name)
@@ -123,3 +127,26 @@ def buf_array(bufs):
     arr = (C.c_char_p * max(n, 1))(*[bytes(b) for b in bufs])
     lens = (C.c_size_t * max(n, 1))(*[len(b) for b in bufs])
     return arr, lens, n
+
+
+def stage_change(data):
+    """Host DEFLATE stage for one change (inflates chunk type 2)."""
+    if len(data) <= 8 or data[8] != 2:
+        return bytes(data)
+    out, n, err = u8p(), C.c_size_t(), Error()
+    if lib.am_stage_change(bytes(data), len(data), C.byref(out), C.byref(n), C.byref(err)):
+        raise_for(err)
+    b = C.string_at(out, n.value)
+    lib.am_free(out)
+    return b
+
+
+def stage_document(data, device=0):
+    """Host DEFLATE stage for a document: returns (bytes, checksum_already_verified)."""
+    out, n, v, err = u8p(), C.c_size_t(), C.c_int(), Error()
+    if lib.am_stage_document(engine(device), bytes(data), len(data), C.byref(out), C.byref(n), C.byref(v),
+                             C.byref(err)):
+        raise_for(err)
+    b = C.string_at(out, n.value)
+    lib.am_free(out)
+    return b, bool(v.value)

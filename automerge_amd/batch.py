@@ -19,16 +19,19 @@ assert DOC_DT.itemsize == C.sizeof(N.DocDesc)
 assert RESULT_DT.itemsize == C.sizeof(N.DocResult)
 
 
-def pack(docs):
-    """docs: iterable of (base_bytes | None, [change bytes]) -> (arena, chunks, docdescs)."""
+def pack(docs, device=0):
+    """docs: iterable of (base_bytes | None, [change bytes]) -> (arena, chunks, docdescs).
+    Compressed inputs go through the host DEFLATE stage (am_stage_change / am_stage_document)."""
     parts, chunks, descs = [], [], []
     off = 0
     for base, changes in docs:
         d = np.zeros((), DOC_DT)
         d["base_chunk"] = -1
+        changes = [N.stage_change(c) for c in changes]
         if base:
+            base, verified = N.stage_document(base, device)
             d["base_chunk"] = len(chunks)
-            chunks.append((off, len(base), 0))
+            chunks.append((off, len(base), 1 if verified else 0))
             parts.append(base)
             off += len(base)
         d["chg_begin"] = len(chunks)

@@ -816,3 +816,29 @@ extern "C" int am_change_hashes(am_engine* eng, const uint8_t* const* bufs, cons
   if (err) err->code = 0;
   return 0;
 }
+
+// ---- host stage exposed for batch callers ----
+extern "C" int am_stage_change(const uint8_t* in, size_t len, uint8_t** out, size_t* outlen, am_error* err) {
+  Err e;
+  std::vector<uint8_t> src(in, in + len), dst;
+  if (!stage_change(src, dst, e)) { to_c(e, err); return 1; }
+  *out = (uint8_t*)std::malloc(dst.size() ? dst.size() : 1);
+  if (!dst.empty()) std::memcpy(*out, dst.data(), dst.size());
+  *outlen = dst.size();
+  if (err) err->code = 0;
+  return 0;
+}
+
+extern "C" int am_stage_document(am_engine* eng, const uint8_t* in, size_t len, uint8_t** out, size_t* outlen,
+                                 int* verified, am_error* err) {
+  Err e;
+  std::vector<uint8_t> src(in, in + len), dst;
+  bool v = false;
+  if (!stage_doc(eng, src, dst, v, e)) { to_c(e, err); return 1; }
+  *out = (uint8_t*)std::malloc(dst.size() ? dst.size() : 1);
+  if (!dst.empty()) std::memcpy(*out, dst.data(), dst.size());
+  *outlen = dst.size();
+  *verified = v ? 1 : 0;
+  if (err) err->code = 0;
+  return 0;
+}

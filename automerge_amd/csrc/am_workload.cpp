@@ -1,0 +1,377 @@
+// am_workload.cpp -- synthetic workloads of SURVEY.md §8(d) for bench.py (host-side data
+// preparation, runs before any timed region). Documents are generated from a seeded LCG
+// (s = s*1664525 + 1013904223 mod 2^32, seed = document index) and encoded in the Automerge
+// binary change format (columnar.js encodeChange/encodeContainer). The bytes are pinned by the
+// SHA-256 digests in tests/golden/workload.json, which the reference's own encoder produced for
+// the same specification (tests/golden/gen/make_fixtures.js: c4Doc, c2Doc).
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/automerge_amd.h"
+
+namespace {
+
+// ---------------- SHA-256 (change hashes are part of the generated change headers) -------------
+struct Sha {
+  static uint32_t ror(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+  static void block(uint32_t h[8], const uint8_t* p) {
+    static const uint32_t K[64] = {
+        0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5, 0xd807aa98,
+        0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786,
+        0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8,
+        0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13,
+        0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819,
+        0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a,
+        0x5b9cca4f, 0x682e6ff3, 0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
+        0xc67178f2};
+    uint32_t w[64];
+    for (int i = 0; i < 16; i++) w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
+    for (int i = 16; i < 64; i++)
+      w[i] = w[i - 16] + (ror(w[i - 15], 7) ^ ror(w[i - 15], 18) ^ (w[i - 15] >> 3)) + w[i - 7] +
+             (ror(w[i - 2], 17) ^ ror(w[i - 2], 19) ^ (w[i - 2] >> 10));
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+    for (int i = 0; i < 64; i++) {
+      uint32_t t1 = hh + (ror(e, 6) ^ ror(e, 11) ^ ror(e, 25)) + ((e & f) ^ (~e & g)) + K[i] + w[i];
+      uint32_t t2 = (ror(a, 2) ^ ror(a, 13) ^ ror(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+  }
+  static void hash(const uint8_t* data, size_t len, uint8_t out[32]) {
+    uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    size_t i = 0;
+    for (; i + 64 <= len; i += 64) block(h, data + i);
+    uint8_t t[128] = {0};
+    size_t rem = len - i;
+    memcpy(t, data + i, rem);
+    t[rem] = 0x80;
+    size_t tl = rem + 9 <= 64 ? 64 : 128;
+    uint64_t bits = (uint64_t)len * 8;
+    for (int k = 0; k < 8; k++) t[tl - 1 - k] = (uint8_t)(bits >> (8 * k));
+    block(h, t);
+    if (tl == 128) block(h, t + 64);
+    for (int k = 0; k < 8; k++) { out[4 * k] = h[k] >> 24; out[4 * k + 1] = h[k] >> 16; out[4 * k + 2] = h[k] >> 8; out[4 * k + 3] = h[k]; }
+  }
+};
+
+using Bytes = std::vector<uint8_t>;
+void pu(Bytes& o, uint64_t v) { do { uint8_t b = v & 0x7f; v >>= 7; o.push_back(b | (v ? 0x80 : 0)); } while (v); }
+void ps(Bytes& o, int64_t v) {
+  for (;;) {
+    uint8_t b = v & 0x7f;
+    v >>= 7;
+    if ((v == 0 && !(b & 0x40)) || (v == -1 && (b & 0x40))) { o.push_back(b); return; }
+    o.push_back(b | 0x80);
+  }
+}
+
+// nullable value for the column encoders
+struct V { bool null; int64_t i; std::string s; };
+V N0() { return {true, 0, {}}; }
+V I(int64_t x) { return {false, x, {}}; }
+V S(const std::string& x) { return {false, 0, x}; }
+bool eqv(const V& a, const V& b, bool str) { return a.null == b.null && (a.null || (str ? a.s == b.s : a.i == b.i)); }
+
+// canonical RLE (RLEEncoder, encoding.js:558-783)
+Bytes rle(const std::vector<V>& v, int type /*0 uint 1 int 2 utf8*/) {
+  Bytes o;
+  bool any = false;
+  for (auto& x : v) any |= !x.null;
+  if (!any) return o;
+  auto put = [&](const V& x) {
+    if (type == 2) { pu(o, x.s.size()); o.insert(o.end(), x.s.begin(), x.s.end()); }
+    else if (type == 1) ps(o, x.i);
+    else pu(o, (uint64_t)x.i);
+  };
+  size_t n = v.size(), i = 0;
+  while (i < n) {
+    size_t j = i + 1;
+    while (j < n && eqv(v[j], v[i], type == 2)) j++;
+    if (v[i].null) { ps(o, 0); pu(o, j - i); i = j; continue; }
+    if (j - i >= 2) { ps(o, (int64_t)(j - i)); put(v[i]); i = j; continue; }
+    size_t k = i;
+    while (k < n && !v[k].null && (k + 1 >= n || !eqv(v[k + 1], v[k], type == 2))) k++;
+    ps(o, -(int64_t)(k - i));
+    for (size_t t = i; t < k; t++) put(v[t]);
+    i = k;
+  }
+  return o;
+}
+Bytes delta(const std::vector<V>& v) {
+  std::vector<V> d;
+  int64_t abs = 0;
+  for (auto& x : v) {
+    if (x.null) d.push_back(N0());
+    else { d.push_back(I(x.i - abs)); abs = x.i; }
+  }
+  return rle(d, 1);
+}
+Bytes boolean(const std::vector<bool>& v) {
+  Bytes o;
+  bool last = false;
+  uint64_t c = 0;
+  for (bool x : v) { if (x == last) c++; else { pu(o, c); last = x; c = 1; } }
+  if (c) pu(o, c);
+  return o;
+}
+
+Bytes container(uint8_t type, const Bytes& body, uint8_t hash_out[32]) {
+  Bytes hb;
+  hb.push_back(type);
+  pu(hb, body.size());
+  hb.insert(hb.end(), body.begin(), body.end());
+  uint8_t h[32];
+  Sha::hash(hb.data(), hb.size(), h);
+  if (hash_out) memcpy(hash_out, h, 32);
+  Bytes o = {0x85, 0x6f, 0x4a, 0x83, h[0], h[1], h[2], h[3]};
+  o.insert(o.end(), hb.begin(), hb.end());
+  return o;
+}
+
+struct Actor { uint8_t b[16]; };
+bool operator<(const Actor& a, const Actor& b) { return memcmp(a.b, b.b, 16) < 0; }
+bool operator==(const Actor& a, const Actor& b) { return memcmp(a.b, b.b, 16) == 0; }
+
+// one op of a generated change (only the shapes the workloads need)
+struct Op {
+  int obj;            // -1 root, else actor index (in `actors` of the document) with ctr obj_ctr
+  int64_t obj_ctr;
+  std::string key;    // map key (empty -> list op)
+  int elem_actor;     // list: -1 = _head
+  int64_t elem_ctr;
+  bool insert;
+  int action;         // 0 makeMap 1 set 2 makeList 5 inc ...
+  int vtype;          // 0 null, 4 int, 6 utf8, 8 counter
+  int64_t ival;
+  std::string sval;
+  std::vector<std::pair<int64_t, int>> pred;  // (ctr, doc actor index)
+};
+
+// encodeChange (columnar.js:710-739) for a change whose ops reference `doc_actors` indexes
+Bytes encode_change(const std::vector<Actor>& doc_actors, int author, int64_t seq, int64_t start_op,
+                    const std::vector<std::vector<uint8_t>>& deps_sorted, const std::vector<Op>& ops, uint8_t hash[32]) {
+  // parseAllOpIds(single): author first, then the other referenced actors sorted
+  std::vector<int> others;
+  auto add = [&](int a) {
+    if (a >= 0 && a != author && std::find(others.begin(), others.end(), a) == others.end()) others.push_back(a);
+  };
+  for (auto& op : ops) {
+    if (op.obj >= 0) add(op.obj);
+    if (op.elem_actor >= 0) add(op.elem_actor);
+    for (auto& p : op.pred) add(p.second);
+  }
+  std::sort(others.begin(), others.end(), [&](int a, int b) { return doc_actors[a] < doc_actors[b]; });
+  auto num = [&](int a) -> int64_t {
+    if (a == author) return 0;
+    return 1 + (std::find(others.begin(), others.end(), a) - others.begin());
+  };
+  std::vector<V> objA, objC, keyA, keyC, keyS, act, vlen, predN, predA, predC;
+  std::vector<bool> ins;
+  Bytes vraw;
+  for (auto& op : ops) {
+    if (op.obj < 0) { objA.push_back(N0()); objC.push_back(N0()); }
+    else { objA.push_back(I(num(op.obj))); objC.push_back(I(op.obj_ctr)); }
+    if (!op.key.empty()) { keyA.push_back(N0()); keyC.push_back(N0()); keyS.push_back(S(op.key)); }
+    else if (op.elem_actor < 0) { keyA.push_back(N0()); keyC.push_back(I(0)); keyS.push_back(N0()); }
+    else { keyA.push_back(I(num(op.elem_actor))); keyC.push_back(I(op.elem_ctr)); keyS.push_back(N0()); }
+    ins.push_back(op.insert);
+    act.push_back(I(op.action));
+    if (op.vtype == 6) {
+      vraw.insert(vraw.end(), op.sval.begin(), op.sval.end());
+      vlen.push_back(I((int64_t)(op.sval.size() << 4) | 6));
+    } else if (op.vtype == 4 || op.vtype == 8) {
+      Bytes t;
+      ps(t, op.ival);
+      vraw.insert(vraw.end(), t.begin(), t.end());
+      vlen.push_back(I((int64_t)(t.size() << 4) | op.vtype));
+    } else {
+      vlen.push_back(I(0));
+    }
+    auto pr = op.pred;
+    std::sort(pr.begin(), pr.end(), [&](const std::pair<int64_t, int>& a, const std::pair<int64_t, int>& b) {
+      if (a.first != b.first) return a.first < b.first;
+      return doc_actors[a.second] < doc_actors[b.second];
+    });
+    predN.push_back(I((int64_t)pr.size()));
+    for (auto& p : pr) { predA.push_back(I(num(p.second))); predC.push_back(I(p.first)); }
+  }
+  std::vector<V> chA(ops.size(), N0()), chC(ops.size(), N0());
+  struct Col { int id; Bytes b; };
+  std::vector<Col> cols = {{0x01, rle(objA, 0)}, {0x02, rle(objC, 0)}, {0x11, rle(keyA, 0)}, {0x13, delta(keyC)},
+                           {0x15, rle(keyS, 2)}, {0x34, boolean(ins)}, {0x42, rle(act, 0)}, {0x56, rle(vlen, 0)},
+                           {0x57, vraw},       {0x61, rle(chA, 0)}, {0x63, delta(chC)}, {0x70, rle(predN, 0)},
+                           {0x71, rle(predA, 0)}, {0x73, delta(predC)}};
+  Bytes body;
+  pu(body, deps_sorted.size());
+  for (auto& d : deps_sorted) body.insert(body.end(), d.begin(), d.end());
+  pu(body, 16);
+  body.insert(body.end(), doc_actors[author].b, doc_actors[author].b + 16);
+  pu(body, (uint64_t)seq);
+  pu(body, (uint64_t)start_op);
+  ps(body, 0);   // time
+  pu(body, 0);   // message ''
+  pu(body, others.size());
+  for (int a : others) { pu(body, 16); body.insert(body.end(), doc_actors[a].b, doc_actors[a].b + 16); }
+  size_t ne = 0;
+  for (auto& c : cols) ne += !c.b.empty();
+  pu(body, ne);
+  for (auto& c : cols) if (!c.b.empty()) { pu(body, c.id); pu(body, c.b.size()); }
+  for (auto& c : cols) body.insert(body.end(), c.b.begin(), c.b.end());
+  return container(1, body, hash);
+}
+
+uint32_t lcg(uint32_t& s) { s = s * 1664525u + 1013904223u; return s; }
+
+void make_actors(uint32_t& s, int n, std::vector<Actor>& out) {
+  while ((int)out.size() < n) {
+    Actor a;
+    for (int i = 0; i < 4; i++) {
+      uint32_t x = lcg(s);
+      a.b[4 * i] = x >> 24; a.b[4 * i + 1] = x >> 16; a.b[4 * i + 2] = x >> 8; a.b[4 * i + 3] = x;
+    }
+    if (std::find(out.begin(), out.end(), a) == out.end()) out.push_back(a);
+  }
+}
+
+// Base document = save(loadChanges(init, [change0])) for the C4 first change: root 'items'
+// (makeList, 1@a0) and 'title' = 'untitled' (2@a0). Encoded as BackendDoc.save() does.
+Bytes c4_base_doc(const Actor& a0, const uint8_t h0[32], const Bytes& change0) {
+  // change columns (DOCUMENT_COLUMNS): one row
+  struct Col { int id; Bytes b; };
+  std::vector<Col> cc = {{0x01, rle({I(0)}, 0)}, {0x03, delta({I(1)})}, {0x13, delta({I(2)})}, {0x23, delta({I(0)})},
+                         {0x35, rle({S("")}, 2)}, {0x40, rle({I(0)}, 0)}, {0x43, {}}, {0x56, rle({I(7)}, 0)},
+                         {0x57, {}}};
+  std::vector<Col> oc = {{0x01, {}}, {0x02, {}}, {0x11, {}}, {0x13, {}},
+                         {0x15, rle({S("items"), S("title")}, 2)}, {0x21, rle({I(0), I(0)}, 0)},
+                         {0x23, delta({I(1), I(2)})}, {0x34, boolean({false, false})}, {0x42, rle({I(2), I(1)}, 0)},
+                         {0x56, rle({I(0), I((8 << 4) | 6)}, 0)}, {0x57, Bytes{'u', 'n', 't', 'i', 't', 'l', 'e', 'd'}},
+                         {0x61, {}}, {0x63, {}}, {0x80, rle({I(0), I(0)}, 0)}, {0x81, {}}, {0x83, {}}};
+  Bytes body;
+  pu(body, 1);
+  pu(body, 16);
+  body.insert(body.end(), a0.b, a0.b + 16);
+  pu(body, 1);
+  body.insert(body.end(), h0, h0 + 32);
+  for (auto* cols : {&cc, &oc}) {
+    size_t ne = 0;
+    for (auto& c : *cols) ne += !c.b.empty();
+    pu(body, ne);
+    for (auto& c : *cols) if (!c.b.empty()) { pu(body, c.id); pu(body, c.b.size()); }
+  }
+  for (auto* cols : {&cc, &oc})
+    for (auto& c : *cols) body.insert(body.end(), c.b.begin(), c.b.end());
+  pu(body, 0);  // headsIndexes
+  (void)change0;
+  return container(0, body, nullptr);
+}
+
+struct DocOut {
+  Bytes base;
+  std::vector<Bytes> changes;
+  uint64_t ops = 0;
+};
+
+// C4: 4 actors x 3 concurrent changes of 4 list inserts + 1 conflicting title set.
+void gen_c4(uint32_t doc_index, DocOut& out) {
+  uint32_t s = doc_index;
+  std::vector<Actor> actors;
+  make_actors(s, 4, actors);
+  const int A0 = 0;
+  std::vector<Op> ops0 = {
+      {-1, 0, "items", -1, 0, false, 2, 0, 0, "", {}},
+      {-1, 0, "title", -1, 0, false, 1, 6, 0, "untitled", {}},
+  };
+  uint8_t h0[32];
+  Bytes change0 = encode_change(actors, A0, 1, 1, {}, ops0, h0);
+  out.base = c4_base_doc(actors[0], h0, change0);
+  std::vector<std::vector<Bytes>> ch(4);
+  for (int i = 0; i < 4; i++) {
+    std::vector<uint8_t> last(h0, h0 + 32);
+    int64_t last_title_ctr = 2;
+    int last_title_actor = A0;
+    std::vector<int64_t> own;
+    int64_t seq_base = i == 0 ? 2 : 1;
+    for (int j = 0; j < 3; j++) {
+      int64_t start = 3 + 5 * j;
+      std::vector<Op> ops;
+      int ref_actor = -1;
+      int64_t ref_ctr = 0;
+      if (!own.empty()) {  // JS: (own.length === 0 || r() % 4 === 0) ? '_head' : own[r() % own.length]
+        if (lcg(s) % 4 != 0) { ref_ctr = own[lcg(s) % own.size()]; ref_actor = i; }
+      }
+      for (int k = 0; k < 4; k++) {
+        char c = (char)(97 + lcg(s) % 26);
+        ops.push_back({A0, 1, "", ref_actor, ref_ctr, true, 1, 6, 0, std::string(1, c), {}});
+        own.push_back(start + k);
+        ref_actor = i;
+        ref_ctr = start + k;
+      }
+      std::string title = "t" + std::to_string(i) + "." + std::to_string(j) + "." + std::to_string(lcg(s) % 1000);
+      ops.push_back({-1, 0, "title", -1, 0, false, 1, 6, 0, title, {{last_title_ctr, last_title_actor}}});
+      last_title_ctr = start + 4;
+      last_title_actor = i;
+      uint8_t h[32];
+      Bytes b = encode_change(actors, i, seq_base + j, start, {last}, ops, h);
+      last.assign(h, h + 32);
+      ch[i].push_back(std::move(b));
+    }
+  }
+  for (int j = 0; j < 3; j++)
+    for (int i = 0; i < 4; i++) out.changes.push_back(ch[i][j]);
+  out.ops = 60;
+}
+
+}  // namespace
+
+extern "C" {
+
+/* Generates C4 documents [first, first + n): each = base document (change 0 saved) + 12 change
+ * chunks. Returns the number of bytes needed; fills the outputs when `arena` is non-NULL and
+ * cap suffices. chunks: n * 13 entries; docs: n entries. ops_out: total ops in the changes. */
+uint64_t am_workload_c4(uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks, am_doc_desc* docs,
+                        uint64_t* ops_out, int nthreads) {
+  std::vector<DocOut> outs(n);
+  if (nthreads < 1) nthreads = 1;
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; t++)
+    th.emplace_back([&, t]() {
+      for (uint32_t d = t; d < n; d += nthreads) gen_c4((uint32_t)(first + d), outs[d]);
+    });
+  for (auto& x : th) x.join();
+  uint64_t total = 0, ops = 0;
+  for (auto& o : outs) {
+    total += o.base.size();
+    for (auto& c : o.changes) total += c.size();
+    ops += o.ops;
+  }
+  if (ops_out) *ops_out = ops;
+  if (!arena || cap < total) return total;
+  uint64_t off = 0;
+  uint32_t ci = 0;
+  for (uint32_t d = 0; d < n; d++) {
+    DocOut& o = outs[d];
+    docs[d].base_chunk = ci;
+    chunks[ci++] = {off, (uint32_t)o.base.size(), 0};
+    memcpy(arena + off, o.base.data(), o.base.size());
+    off += o.base.size();
+    docs[d].chg_begin = ci;
+    docs[d].chg_count = (uint32_t)o.changes.size();
+    docs[d].known_begin = 0;
+    docs[d].known_count = 0;
+    docs[d].flags = 0;
+    docs[d].pad = 0;
+    for (auto& c : o.changes) {
+      chunks[ci++] = {off, (uint32_t)c.size(), 0};
+      memcpy(arena + off, c.data(), c.size());
+      off += c.size();
+    }
+  }
+  return total;
+}
+
+}  // extern "C"

@@ -166,10 +166,27 @@ size_t am_doc_num_changes(const am_doc *doc);
 int am_doc_change(const am_doc *doc, size_t i, const uint8_t **data, size_t *len, uint8_t *hash32);
 void am_free(void *p);
 
+/* ---- host stage for batch callers (DEFLATE, columnar.js:798-823, 1052-1067) ----
+ * am_stage_change: a DEFLATE-compressed change (chunk type 2) becomes an uncompressed type-1 chunk
+ *   keeping its checksum (which covers the uncompressed form); other chunks are copied.
+ * am_stage_document: a document with DEFLATE-compressed columns has its checksum verified on the
+ *   GPU and its columns inflated; *verified = 1 means the result must be staged with
+ *   am_chunk_desc.flags bit0 set (checksum already checked). Outputs are malloc'd (am_free). */
+int am_stage_change(const uint8_t *in, size_t len, uint8_t **out, size_t *outlen, am_error *err);
+int am_stage_document(am_engine *eng, const uint8_t *in, size_t len, uint8_t **out, size_t *outlen, int *verified,
+                      am_error *err);
+
 /* ---- utilities ---- */
 /* Change hash (SHA-256 of the uncompressed chunk) of each change, computed on the GPU. */
 int am_change_hashes(am_engine *eng, const uint8_t *const *bufs, const size_t *lens, size_t n, uint8_t *out32,
                      am_error *err);
+
+/* ---- synthetic workloads (bench.py input preparation, host side) ----
+ * C4: document i = base document (change 0 saved) + 12 concurrent changes (4 actors x 3), seeded
+ * by i. Returns the arena bytes needed; fills arena/chunks (13 per doc)/docs when arena != NULL
+ * and cap suffices. ops_out receives the number of ops in the 12 changes of all documents. */
+uint64_t am_workload_c4(uint64_t first_doc, uint32_t ndocs, uint8_t *arena, uint64_t cap, am_chunk_desc *chunks,
+                        am_doc_desc *docs, uint64_t *ops_out, int nthreads);
 
 #ifdef __cplusplus
 }
