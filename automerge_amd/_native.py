@@ -7,7 +7,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libautomerge_amd.so")
+LIB_PATH = os.environ.get("AM_LIB_PATH") or os.path.join(_HERE, "libautomerge_amd.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

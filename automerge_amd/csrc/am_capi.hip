@@ -279,7 +279,8 @@ struct am_batch {
   DevBuf<am_known_hash> known;
   DevBuf<ChunkInfo> info;
   DevBuf<DocBounds> bounds;
-  DevBuf<uint64_t> ws_bytes, ws_off, scan_tmp, ws_total;
+  DevBuf<uint64_t> ws_bytes, ws_off, scan_tmp, ws_total, max_hot;
+  uint32_t lds_bytes = 0;
   DevBuf<uint8_t> ws;
   DevBuf<am_doc_result> results;
   DevBuf<int32_t> chg_state;
@@ -290,7 +291,7 @@ struct am_batch {
   BatchDev dev() {
     BatchDev b;
     b.arena = arena.p; b.chunks = chunks.p; b.docs = docs.p; b.known = known.p; b.info = info.p; b.bounds = bounds.p;
-    b.ws_bytes = ws_bytes.p; b.ws_off = ws_off.p; b.scan_tmp = scan_tmp.p; b.ws_total = ws_total.p; b.ws = ws.p;
+    b.ws_bytes = ws_bytes.p; b.ws_off = ws_off.p; b.scan_tmp = scan_tmp.p; b.ws_total = ws_total.p; b.max_hot = max_hot.p; b.lds_bytes = lds_bytes; b.ws = ws.p;
     b.ws_cap = ws.cap; b.results = results.p; b.chg_state = chg_state.p; b.nchunks = nchunks; b.ndocs = ndocs;
     return b;
   }
@@ -348,7 +349,7 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   hipStream_t s = e->stream;
   if (!b->arena.ensure(arena_len) || !b->chunks.ensure(nchunks) || !b->docs.ensure(ndocs) || !b->known.ensure(nknown) ||
       !b->info.ensure(nchunks) || !b->bounds.ensure(ndocs) || !b->ws_bytes.ensure(ndocs) || !b->ws_off.ensure(ndocs) ||
-      !b->scan_tmp.ensure(am_scan_tmp_elems(ndocs)) || !b->ws_total.ensure(1) || !b->results.ensure(ndocs) ||
+      !b->scan_tmp.ensure(am_scan_tmp_elems(ndocs)) || !b->ws_total.ensure(1) || !b->max_hot.ensure(1) || !b->results.ensure(ndocs) ||
       !b->chg_state.ensure(nchunks))
     return false;
   if (arena_len) HIPCHECK(hipMemcpyAsync(b->arena.p, arena, arena_len, hipMemcpyHostToDevice, s));
@@ -361,11 +362,16 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   BatchDev d = b->dev();
   am_launch_chunks(d, s);
   am_launch_bounds(d, s);
-  uint64_t total = 0;
+  uint64_t total = 0, max_hot = 0;
   if (ndocs) HIPCHECK(hipMemcpyAsync(&total, b->ws_total.p, sizeof total, hipMemcpyDeviceToHost, s));
+  if (ndocs) HIPCHECK(hipMemcpyAsync(&max_hot, b->max_hot.p, sizeof max_hot, hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
   HIPCHECK(hipGetLastError());
   b->ws_need = total;
+  // dynamic LDS of the document workgroups: the largest hot working set, capped by the budget
+  uint64_t lds = (max_hot + 15) & ~(uint64_t)15;
+  if (lds > AM_LDS_BUDGET) lds = AM_LDS_BUDGET;
+  b->lds_bytes = (uint32_t)lds;
   if (!b->ws.ensure(total + 16)) return false;
   return true;
 }

@@ -503,3 +503,37 @@ __host__ __device__ inline uint32_t pow2_ceil(uint32_t n) {
   while (p < n) p <<= 1;
   return p;
 }
+
+// ------------------------------------------------------------------------------------------
+// Wave64 scans (the document workgroup is exactly one wave: blockDim.x == 64)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t x = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v += x;
+  }
+  return v;
+}
+__device__ __forceinline__ int32_t wave_incl_max(int32_t v) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int32_t x = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d && x > v) v = x;
+  }
+  return v;
+}
+// exclusive add-scan of a[0..n) in place (one wave); returns the total
+__device__ static uint32_t wave_excl_scan_arr(uint32_t* a, uint32_t n) {
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < n; base += 64) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t v = i < n ? a[i] : 0;
+    const uint32_t inc = wave_incl_add(v);
+    if (i < n) a[i] = carry + inc - v;
+    carry += __shfl(inc, 63, 64);
+  }
+  return carry;
+}

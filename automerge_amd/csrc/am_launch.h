@@ -16,6 +16,8 @@ struct BatchDev {
   uint64_t* ws_off;        // per doc (exclusive scan)
   uint64_t* scan_tmp;      // block sums
   uint64_t* ws_total;      // 1 value
+  uint64_t* max_hot;       // 1 value: largest hot working set of the batch
+  uint32_t lds_bytes;      // dynamic LDS per document workgroup
   uint8_t* ws;
   uint64_t ws_cap;
   am_doc_result* results;

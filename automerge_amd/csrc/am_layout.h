@@ -1,5 +1,11 @@
 // am_layout.h -- per-document workspace layout (host + device). Every region is bounded from
 // the per-chunk counts of k_chunks, so one exclusive scan sizes the whole batch.
+//
+// Two parts:
+//   hot  -- everything the merge touches repeatedly (rows, sort keys, Euler tour, plan tables,
+//           the document's input bytes). Placed in LDS when it fits the per-workgroup budget
+//           (the common case for small documents), else in the global workspace.
+//   cold -- streaming buffers written once (encoded columns, delta scratch, merged document).
 #pragma once
 #include <stdint.h>
 
@@ -11,6 +17,9 @@
 #define AM_HD __host__ __device__
 #endif
 
+// LDS budget of one document workgroup (bytes of dynamic shared memory)
+#define AM_LDS_BUDGET (40 * 1024)
+
 struct DocBounds {
   uint32_t R;   // op rows (base + every change in the list)
   uint32_t E;   // pred/succ entries
@@ -21,15 +30,19 @@ struct DocBounds {
   uint32_t N;   // changes in the list
   uint32_t K;   // changeIndexByHash entries
   uint32_t AM;  // actor-map entries (sum of change actor lists)
-  uint32_t overflow;
+  uint32_t ND;  // sum of change deps (plan)
   uint64_t S;   // key + message string bytes over all rows
   uint64_t B;   // input bytes (base + changes)
+  uint64_t span_lo, span_hi;  // arena byte span covering the document's chunks
 };
 
 struct WsLayout {
+  // hot (offsets relative to the hot base)
   uint64_t rows, ents, idk, elemk, sortrec, newent, elem_of, parent, first_child, next_sib, tour_nxt, tour_w, scan,
-      succ_cnt, outent, chg, deps, actors, clock, heads, hidx, htab, chghdr, order, rowbase, entbase, ambase, amap,
-      queue, enq, scratch, scratch_stride, out, out_cap, total;
+      succ_cnt, outent, chg, deps, actors, clock, heads, hidx, chghdr, order, rowbase, entbase, ambase, amap, queue,
+      enq, applied, amb_out, hashes, dup_of, self_idx, aut, can, dbase, dref, dref_idx, docpos, head_ref, input, hot_total;
+  // cold (offsets relative to the document's global workspace, after the hot mirror)
+  uint64_t scratch, scratch_stride, out, out_cap, total;
   uint64_t colbuf[OC_NCOLS + DC_NCOLS];
 };
 
@@ -48,14 +61,13 @@ AM_HD inline uint32_t am_pow2(uint32_t n) {
 #define AM_SZ_NEWENT 24
 #define AM_SZ_CHGROW 80
 #define AM_SZ_ACTORREF 16
-#define AM_SZ_HENT 40
-#define AM_SZ_CHGHDR 288
+#define AM_SZ_CHGHDR 224
 
 AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   WsLayout L;
   uint64_t o = 0;
   auto take = [&](uint64_t bytes) { uint64_t at = o; o += (bytes + 15) & ~(uint64_t)15; return at; };
-  const uint64_t R = b.R, E = b.E, C = b.C, D = b.D;
+  const uint64_t R = b.R, E = b.E, C = b.C, D = b.D, N = b.N;
   const uint64_t PR = am_pow2(b.R ? b.R : 1), PE = am_pow2(b.E ? b.E : 1);
   L.rows = take(R * AM_SZ_ROW);
   L.ents = take(E * AM_SZ_ENT);
@@ -75,18 +87,31 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   L.chg = take(C * AM_SZ_CHGROW);
   L.deps = take(D * 8);
   L.actors = take((uint64_t)b.A * AM_SZ_ACTORREF);
-  L.clock = take((uint64_t)b.A * 8);
+  L.clock = take((uint64_t)(b.A + N) * 8);
   L.heads = take((uint64_t)b.H * 32);
   L.hidx = take((uint64_t)b.H * 8);
-  L.htab = take((uint64_t)b.K * AM_SZ_HENT);
-  L.chghdr = take((uint64_t)b.N * AM_SZ_CHGHDR);
-  L.order = take((uint64_t)b.N * 4);
-  L.rowbase = take((uint64_t)b.N * 4);
-  L.entbase = take((uint64_t)b.N * 4);
-  L.ambase = take((uint64_t)b.N * 4);
+  L.chghdr = take(N * AM_SZ_CHGHDR);
+  L.order = take(N * 4);
+  L.rowbase = take(N * 4);
+  L.entbase = take(N * 4);
+  L.ambase = take(N * 4);
   L.amap = take((uint64_t)b.AM * 4);
-  L.queue = take((uint64_t)b.N * 4);
-  L.enq = take((uint64_t)b.N * 4);
+  L.queue = take(N * 4);
+  L.enq = take(N * 4);
+  L.applied = take(N * 4);
+  L.amb_out = take(N * 4);
+  L.hashes = take(N * 32);
+  L.dup_of = take(N * 4);
+  L.self_idx = take(N * 8);
+  L.aut = take(N * 4);
+  L.can = take((uint64_t)b.AM * 4);
+  L.dbase = take(N * 4);
+  L.dref = take((uint64_t)b.ND * 4);
+  L.dref_idx = take((uint64_t)b.ND * 8);
+  L.docpos = take((uint64_t)(b.A + N) * 4);
+  L.head_ref = take((uint64_t)b.H * 4);
+  L.input = take(b.span_hi - b.span_lo);
+  L.hot_total = o;
   uint64_t stride = R;
   if (E > stride) stride = E;
   if (C > stride) stride = C;
