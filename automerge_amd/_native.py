@@ -72,6 +72,7 @@ _sigs = {
     "am_doc_max_op": (C.c_int64, [P]),
     "am_doc_num_changes": (C.c_size_t, [P]),
     "am_doc_change": (C.c_int, [P, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), P]),
+    "am_doc_queued": (C.c_int, [P, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]),
     "am_free": (None, [P]),
     "am_change_hashes": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t, P, C.POINTER(Error)]),
     "am_stage_change": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),

@@ -281,6 +281,7 @@ struct am_batch {
   DevBuf<DocBounds> bounds;
   DevBuf<uint64_t> ws_bytes, ws_off, scan_tmp, ws_total, max_hot;
   uint32_t lds_bytes = 0;
+  uint64_t max_hot_v = 0;
   DevBuf<uint8_t> ws;
   DevBuf<am_doc_result> results;
   DevBuf<int32_t> chg_state;
@@ -291,7 +292,7 @@ struct am_batch {
   BatchDev dev() {
     BatchDev b;
     b.arena = arena.p; b.chunks = chunks.p; b.docs = docs.p; b.known = known.p; b.info = info.p; b.bounds = bounds.p;
-    b.ws_bytes = ws_bytes.p; b.ws_off = ws_off.p; b.scan_tmp = scan_tmp.p; b.ws_total = ws_total.p; b.max_hot = max_hot.p; b.lds_bytes = lds_bytes; b.ws = ws.p;
+    b.ws_bytes = ws_bytes.p; b.ws_off = ws_off.p; b.scan_tmp = scan_tmp.p; b.ws_total = ws_total.p; b.max_hot = max_hot.p; b.lds_bytes = lds_bytes; b.max_hot_host = max_hot_v; b.ws = ws.p;
     b.ws_cap = ws.cap; b.results = results.p; b.chg_state = chg_state.p; b.nchunks = nchunks; b.ndocs = ndocs;
     return b;
   }
@@ -372,6 +373,7 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   uint64_t lds = (max_hot + 15) & ~(uint64_t)15;
   if (lds > AM_LDS_BUDGET) lds = AM_LDS_BUDGET;
   b->lds_bytes = (uint32_t)lds;
+  b->max_hot_v = max_hot;
   if (!b->ws.ensure(total + 16)) return false;
   return true;
 }
@@ -797,6 +799,13 @@ extern "C" int am_doc_change(const am_doc* d, size_t i, const uint8_t** data, si
   *data = d->changes[i].data();
   *len = d->changes[i].size();
   if (hash32) std::memcpy(hash32, d->hashes[i].data(), 32);
+  return 0;
+}
+
+extern "C" int am_doc_queued(const am_doc* d, size_t i, const uint8_t** data, size_t* len) {
+  if (i >= d->queue.size()) return 1;
+  *data = d->queue[i].data();
+  *len = d->queue[i].size();
   return 0;
 }
 

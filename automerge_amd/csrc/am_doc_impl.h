@@ -1,0 +1,1331 @@
+// am_doc_impl.h -- the per-document merge kernel (k_doc) and its phases. Included twice by
+// am_kernels.hip: namespace lds_mode (kHotLds = true: the hot working set and the document's
+// input bytes live in LDS and every access compiles to ds_* instructions) and namespace glb_mode
+// (kHotLds = false: documents whose working set exceeds the LDS budget run from the global
+// workspace). Keeping the address space a compile-time fact matters on CDNA: generic (flat)
+// accesses to LDS go through the vector-memory path and wait on outstanding global stores.
+
+template <typename T>
+__device__ __forceinline__ T* hp(DocShared& s, uint64_t off) {
+  if constexpr (kHotLds) return reinterpret_cast<T*>(am_lds + off);
+  else return reinterpret_cast<T*>(s.hot + off);
+}
+// View of the arena: AV(s) + arena_offset -> byte of the document's input. In LDS mode the base
+// is the staged copy of [span_lo, span_hi); offsets are rebased before forming a pointer, so
+// every pointer handed out stays inside the LDS allocation (no wrapped 32-bit arithmetic).
+struct APtr {
+  const uint8_t* base;
+  uint64_t lo;
+  __device__ __forceinline__ const uint8_t* operator+(uint64_t off) const { return base + (off - lo); }
+  __device__ __forceinline__ uint8_t operator[](uint64_t off) const { return base[off - lo]; }
+};
+__device__ __forceinline__ APtr AV(DocShared& s) {
+  if constexpr (kHotLds) return APtr{am_lds + s.L.input, s.b.span_lo};
+  else return APtr{s.A, 0};
+}
+
+__device__ static int64_t base_head_index(DocShared& s, uint32_t h) {
+  if (s.dh.has_hidx) {
+    Rd r{AV(s) + s.dh.base + s.dh.hidx_off, (uint64_t)1 << 40, 0};
+    int64_t v = -1;
+    for (uint32_t i = 0; i <= h; i++) rd_u53(r, v);
+    return v;
+  }
+  return s.dh.nheads == 1 ? (int64_t)s.nbc - 1 : -1;
+}
+
+// ---- P2a: lane-parallel lookups -- hashes, duplicates, canonical actors, dependency refs ----
+// Canonical actor ids: base actors 0..NB-1, the author of change j (first occurrence) NB + j.
+// Dependency refs: >= 0 change index (first occurrence of that hash in the list),
+// <= -10: base head (-10 - h), -2: host-known hash, -1: missing.
+__device__ static void plan_lookups(DocShared& s, const am_doc_desc& dd, const ChunkInfo* info, const am_known_hash* known) {
+  const WsLayout& L = s.L;
+  const uint32_t N = dd.chg_count, t = threadIdx.x, T = blockDim.x;
+  const ChgHdr* ch = hp<ChgHdr>(s, L.chghdr);
+  uint8_t* hashes = hp<uint8_t>(s, L.hashes);
+  const APtr A = AV(s);
+  const uint32_t NB = s.has_base ? s.dh.nactors : 0;
+  for (uint32_t c = t; c < N; c += T) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(info[dd.chg_begin + c].hash);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(hashes + 32 * c);
+    for (int k = 0; k < 8; k++) dst[k] = src[k];
+  }
+  __syncthreads();
+  uint32_t* dup_of = hp<uint32_t>(s, L.dup_of);
+  int64_t* self_idx = hp<int64_t>(s, L.self_idx);
+  int32_t* aut = hp<int32_t>(s, L.aut);
+  int32_t* can = hp<int32_t>(s, L.can);
+  int32_t* dref = hp<int32_t>(s, L.dref);
+  int64_t* dref_idx = hp<int64_t>(s, L.dref_idx);
+  const uint32_t* ambase = hp<uint32_t>(s, L.ambase);
+  const uint32_t* dbase = hp<uint32_t>(s, L.dbase);
+  auto base_actor = [&](uint64_t off, uint32_t len) -> int32_t {
+    if (!s.has_base) return -1;
+    Rd r{A + s.dh.base + s.dh.actors_off, (uint64_t)1 << 40, 0};
+    for (uint32_t i = 0; i < s.dh.nactors; i++) {
+      int64_t l;
+      rd_u53(r, l);
+      if ((uint32_t)l == len && bytes_eq(r.p + r.off, A + off, len)) return (int32_t)i;
+      r.off += (uint64_t)l;
+    }
+    return -1;
+  };
+  auto author_canon = [&](uint64_t off, uint32_t len, uint32_t upto) -> int32_t {
+    int32_t a = base_actor(off, len);
+    if (a >= 0) return a;
+    for (uint32_t j = 0; j < upto; j++) {
+      const ChgHdr& hj = ch[j];
+      if (hj.actor_len == len && bytes_eq(A + hj.base + hj.actor_off, A + off, len)) return (int32_t)(NB + j);
+    }
+    return -1;
+  };
+  auto match_base = [&](const uint8_t* h, int32_t& ref, int64_t& idx) -> bool {
+    if (s.has_base)
+      for (uint32_t k = 0; k < s.dh.nheads; k++)
+        if (hash_eq(A + s.dh.base + s.dh.heads_off + 32 * k, h)) { ref = -10 - (int32_t)k; idx = base_head_index(s, k); return true; }
+    for (uint32_t k = 0; k < dd.known_count; k++)
+      if (hash_eq(known[dd.known_begin + k].hash, h)) { ref = -2; idx = known[dd.known_begin + k].index; return true; }
+    return false;
+  };
+  for (uint32_t c = t; c < N; c += T) {
+    const ChgHdr& h = ch[c];
+    const uint8_t* hc = hashes + 32 * c;
+    uint32_t d = c;
+    for (uint32_t j = 0; j < c; j++) if (hash_eq(hashes + 32 * j, hc)) { d = j; break; }
+    dup_of[c] = d;
+    int32_t ref;
+    int64_t idx;
+    self_idx[c] = match_base(hc, ref, idx) ? idx : (int64_t)-2;
+    aut[c] = author_canon(h.base + h.actor_off, h.actor_len, c + 1);
+    uint32_t am = ambase[c];
+    can[am] = aut[c];
+    Rd ar{A + h.base + h.actors_off, (uint64_t)1 << 40, 0};
+    for (uint32_t k = 1; k < h.nactors; k++) {
+      int64_t l;
+      rd_u53(ar, l);
+      can[am + k] = author_canon(h.base + h.actors_off + ar.off, (uint32_t)l, N);
+      ar.off += (uint64_t)l;
+    }
+    for (uint32_t di = 0; di < h.ndeps; di++) {
+      const uint8_t* dep = A + h.base + h.deps_off + 32 * di;
+      int32_t r = -1;
+      int64_t x = 0;
+      if (!match_base(dep, r, x)) {
+        for (uint32_t j = 0; j < N; j++) if (hash_eq(hashes + 32 * j, dep)) { r = (int32_t)j; break; }
+      }
+      dref[dbase[c] + di] = r;
+      dref_idx[dbase[c] + di] = x;
+    }
+  }
+}
+
+// ---- P2b: causal queue, clock, actor table, heads (one lane; integer work only) ----
+__device__ static void plan_doc(DocShared& s, const am_doc_desc& dd, const ChunkInfo* info, int32_t* chg_state) {
+  const WsLayout& L = s.L;
+  const APtr A = AV(s);
+  ActorRef* actors = hp<ActorRef>(s, L.actors);
+  int64_t* clock = hp<int64_t>(s, L.clock);
+  int32_t* docpos = hp<int32_t>(s, L.docpos);
+  uint8_t* heads = hp<uint8_t>(s, L.heads);
+  int32_t* head_ref = hp<int32_t>(s, L.head_ref);
+  ChgRow* chg = hp<ChgRow>(s, L.chg);
+  int64_t* deps = hp<int64_t>(s, L.deps);
+  const ChgHdr* ch = hp<ChgHdr>(s, L.chghdr);
+  uint32_t* order = hp<uint32_t>(s, L.order);
+  uint32_t* rowbase = hp<uint32_t>(s, L.rowbase);
+  uint32_t* entbase = hp<uint32_t>(s, L.entbase);
+  uint32_t* ambase_out = hp<uint32_t>(s, L.amb_out);  // per applied change, its amap base
+  uint32_t* amap = hp<uint32_t>(s, L.amap);
+  uint32_t* queue = hp<uint32_t>(s, L.queue);
+  const uint8_t* hashes = hp<uint8_t>(s, L.hashes);
+  const uint32_t* dup_of = hp<uint32_t>(s, L.dup_of);
+  const int64_t* self_idx = hp<int64_t>(s, L.self_idx);
+  const int32_t* aut = hp<int32_t>(s, L.aut);
+  const int32_t* can = hp<int32_t>(s, L.can);
+  const int32_t* dref = hp<int32_t>(s, L.dref);
+  const int64_t* dref_idx = hp<int64_t>(s, L.dref_idx);
+  const uint32_t* ambase = hp<uint32_t>(s, L.ambase);
+  const uint32_t* dbase = hp<uint32_t>(s, L.dbase);
+  int32_t* applied = hp<int32_t>(s, L.applied);  // applied index per change (first occurrence of its hash)
+  const uint32_t N = dd.chg_count;
+  const uint32_t NB = s.has_base ? s.dh.nactors : 0;
+
+  // base actors + clock (readDocumentChanges, new.js:1645-1675)
+  uint32_t na = 0;
+  if (s.has_base) {
+    Rd r{A + s.dh.base + s.dh.actors_off, (uint64_t)1 << 40, 0};
+    for (uint32_t i = 0; i < NB; i++) {
+      int64_t l;
+      rd_u53(r, l);
+      actors[na].off = s.dh.base + s.dh.actors_off + r.off;
+      actors[na].len = (uint32_t)l;
+      r.off += (uint64_t)l;
+      docpos[na] = (int32_t)na;
+      na++;
+    }
+  }
+  for (uint32_t i = 0; i < NB + N; i++) clock[i] = 0;
+  for (uint32_t j = 0; j < N; j++) { docpos[NB + j] = -1; applied[j] = -1; }
+  for (uint32_t i = 0; i < s.nbc; i++) {
+    int64_t a = chg[i].actor, seq = chg[i].seq;
+    if (a == AM_NULL64 || a < 0 || a >= (int64_t)NB || seq == AM_NULL64) { set_err(s, AM_U_VALUE); return; }
+    if (seq != 1 && seq != clock[a] + 1) {
+      set_err(s, AM_E_DOC_SEQ, clock[a] == 0 ? AM_NULL64 : clock[a] + 1, seq, actors[a].off, actors[a].len);
+      return;
+    }
+    clock[a] = seq;
+  }
+  uint32_t nheads = 0;
+  if (s.has_base)
+    for (uint32_t h = 0; h < s.dh.nheads; h++) head_ref[nheads++] = -10 - (int32_t)h;
+
+  const bool have_graph = (dd.flags & 1) != 0;
+  uint32_t nq = N;
+  for (uint32_t i = 0; i < nq; i++) { queue[i] = i; chg_state[dd.chg_begin + i] = CHG_UNSEEN; }
+  uint32_t nall = 0, nrow = s.nb, nent = s.nbe, nam = 0, ndep = s.nbd;
+  int64_t max_op = 0;
+  for (;;) {
+    // one pass of applyChanges() (new.js:1550-1597)
+    uint32_t ne = 0, na_pass = 0;
+    for (uint32_t qi = 0; qi < nq; qi++) {
+      const uint32_t c = queue[qi];
+      const ChunkInfo& ci = info[dd.chg_begin + c];
+      const ChgHdr& h = ch[c];
+      const uint32_t j0 = dup_of[c];
+      if (self_idx[c] != -2 || applied[j0] >= 0) { chg_state[dd.chg_begin + c] = CHG_DUP; continue; }
+      bool ready = true;
+      for (uint32_t di = 0; di < h.ndeps && ready; di++) {
+        int32_t r = dref[dbase[c] + di];
+        if (r >= 0) ready = applied[r] >= 0;
+        else if (r == -1) ready = false;
+        else ready = dref_idx[dbase[c] + di] != -1;
+      }
+      if (!ready) { queue[ne++] = c; continue; }
+      const int32_t a = aut[c];
+      const int64_t expected = clock[a] + 1;
+      if (h.seq < expected) {
+        if (have_graph) { set_err(s, AM_E_REUSE_SEQ, h.seq, 0, h.base + h.actor_off, h.actor_len, c); return; }
+        set_err(s, AM_U_HASH_GRAPH);
+        return;
+      }
+      if (h.seq > expected) { set_err(s, AM_E_SKIPPED_SEQ, expected, 0, h.base + h.actor_off, h.actor_len, c); return; }
+      clock[a] = h.seq;
+      if (docpos[a] < 0) {  // getActorTable appends a new author (new.js:1435-1441)
+        docpos[a] = (int32_t)na;
+        actors[na].off = h.base + h.actor_off;
+        actors[na].len = h.actor_len;
+        na++;
+      }
+      // actor table of the change's columns (getActorTable, new.js:1442-1450)
+      ambase_out[nall] = nam;
+      Rd ar{A + h.base + h.actors_off, (uint64_t)1 << 40, 0};
+      for (uint32_t k = 0; k < h.nactors; k++) {
+        int32_t x = can[ambase[c] + k];
+        uint64_t aoff = h.base + h.actor_off;
+        uint32_t alen = h.actor_len;
+        if (k > 0) {
+          int64_t l;
+          rd_u53(ar, l);
+          aoff = h.base + h.actors_off + ar.off;
+          alen = (uint32_t)l;
+          ar.off += (uint64_t)l;
+        }
+        if (x < 0 || docpos[x] < 0) { set_err(s, AM_E_UNKNOWN_ACTOR, 0, 0, aoff, alen, c); return; }
+        amap[nam++] = (uint32_t)docpos[x];
+      }
+      // heads: drop the dependencies, add this change (new.js:1581-1583)
+      for (uint32_t di = 0; di < h.ndeps; di++) {
+        int32_t r = dref[dbase[c] + di];
+        for (uint32_t q = 0; q < nheads; q++)
+          if (head_ref[q] == r && r != -1 && r != -2) { head_ref[q] = head_ref[--nheads]; break; }
+      }
+      bool present = false;
+      for (uint32_t q = 0; q < nheads; q++) present |= head_ref[q] == (int32_t)j0;
+      if (!present) head_ref[nheads++] = (int32_t)j0;
+      applied[j0] = (int32_t)nall;
+      order[nall] = c;
+      rowbase[nall] = nrow;
+      entbase[nall] = nent;
+      nrow += ci.nops;
+      nent += ci.nents;
+      // appendChange row (new.js:1680-1692)
+      ChgRow& cr = chg[s.nbc + nall];
+      cr.actor = docpos[a];
+      cr.seq = h.seq;
+      cr.max_op = h.start_op + (int64_t)ci.nops - 1;
+      cr.time = h.time;
+      cr.msg_off = h.base + h.msg_off;
+      cr.msg_len = h.msg_len;
+      cr.ndeps = h.ndeps;
+      cr.deps_off = ndep;
+      ndep += h.ndeps;
+      cr.extra_len = h.has_extra ? (int64_t)(((uint64_t)h.extra_len << 4) | 7) : 7;
+      cr.extra_off = h.base + h.extra_off;
+      cr.extra_raw_len = h.has_extra ? h.extra_len : 0;
+      if (ci.nops > 0 && cr.max_op > max_op) max_op = cr.max_op;
+      chg_state[dd.chg_begin + c] = (int32_t)nall;
+      nall++;
+      na_pass++;
+    }
+    nq = ne;
+    if (nq == 0) break;
+    if (na_pass == 0) {
+      if (have_graph) break;
+      set_err(s, AM_U_HASH_GRAPH);  // BackendDoc.applyChanges would computeHashGraph() (new.js:1830)
+      return;
+    }
+  }
+  for (uint32_t i = 0; i < nq; i++) chg_state[dd.chg_begin + queue[i]] = CHG_QUEUED;
+  // deps indexes of the appended change rows: changeIndexByHash[dep]
+  for (uint32_t k = 0; k < nall; k++) {
+    const uint32_t c = order[k];
+    const ChgHdr& h = ch[c];
+    ChgRow& cr = chg[s.nbc + k];
+    for (uint32_t di = 0; di < h.ndeps; di++) {
+      int32_t r = dref[dbase[c] + di];
+      deps[cr.deps_off + di] = r >= 0 ? (int64_t)(s.nbc + applied[r]) : dref_idx[dbase[c] + di];
+    }
+  }
+  // heads (sorted, new.js:1593) with their headsIndexes
+  int64_t* hidx = hp<int64_t>(s, L.hidx);
+  for (uint32_t q = 0; q < nheads; q++) {
+    int32_t r = head_ref[q];
+    const uint8_t* src = r >= 0 ? hashes + 32 * r : A + s.dh.base + s.dh.heads_off + 32 * (uint32_t)(-10 - r);
+    for (int k = 0; k < 32; k++) heads[32 * q + k] = src[k];
+    hidx[q] = r >= 0 ? (int64_t)(s.nbc + applied[r]) : base_head_index(s, (uint32_t)(-10 - r));
+  }
+  for (uint32_t a2 = 1; a2 < nheads; a2++)
+    for (uint32_t b2 = a2; b2 > 0 && hash_cmp(heads + 32 * (b2 - 1), heads + 32 * b2) > 0; b2--) {
+      for (int k = 0; k < 32; k++) { uint8_t tt = heads[32 * b2 + k]; heads[32 * b2 + k] = heads[32 * (b2 - 1) + k]; heads[32 * (b2 - 1) + k] = tt; }
+      int64_t ti = hidx[b2]; hidx[b2] = hidx[b2 - 1]; hidx[b2 - 1] = ti;
+    }
+  if (nall > 0 || nq > 0)
+    for (uint32_t q = 0; q < nheads; q++)
+      if (hidx[q] < 0) { set_err(s, AM_U_HASH_GRAPH); return; }
+  s.napplied = nall;
+  s.nqueued = nq;
+  s.nactors = na;
+  s.nheads = nheads;
+  s.nrows = nrow;
+  s.nents = nent;
+  s.nchg = s.nbc + nall;
+  s.ndeps = ndep;
+  s.max_op = max_op;
+}
+
+// ---- P4: column decode. Every lane runs the same stream decoder over one (source, column)
+// stream into a dense cell array; a lane-per-row gather then assembles the rows, and two scans
+// place the raw values and the pred/succ groups (readOperation new.js:557-611, 700-724). ----
+// value type of each op column as decoded: 0 uint RLE, 3 delta, 2 utf8, 4 boolean
+__device__ __constant__ static const uint8_t kOpColDec[OC_NCOLS] = {
+    DT_UINT, DT_UINT, DT_UINT, DT_DELTA, DT_UTF8, DT_UINT, DT_DELTA, DT_BOOL,
+    DT_UINT, DT_UINT, DT_UINT, DT_UINT, DT_DELTA, DT_UINT, DT_UINT, DT_DELTA};
+#define DEC_STREAMS 15  // op columns without valRaw
+#define DEC_ROWCOLS 13  // per-row cells: streams 0..12; entry cells: 13 (actor), 14 (ctr)
+
+struct SrcInfo {
+  uint64_t base;            // arena offset of the chunk data the column offsets are relative to
+  const uint32_t* coff;
+  const uint32_t* clen;
+  const uint32_t* map;      // change: actor index map (amap slice)
+  int64_t start_op;
+  uint32_t row0, nr, ent0, ne, chg, nmap, self, is_change;
+};
+
+__device__ static SrcInfo src_info(DocShared& s, uint32_t src) {
+  const WsLayout& L = s.L;
+  SrcInfo si;
+  if (s.has_base && src == 0) {
+    si.base = s.dh.base; si.coff = s.dh.ocol_off; si.clen = s.dh.ocol_len;
+    si.row0 = 0; si.nr = s.nb; si.ent0 = 0; si.ne = s.nbe;
+    si.chg = 0xffffffffu; si.map = nullptr; si.nmap = 0; si.self = 0; si.start_op = 0; si.is_change = 0;
+  } else {
+    const uint32_t k = src - (s.has_base ? 1 : 0);
+    const uint32_t c = hp<uint32_t>(s, L.order)[k];
+    const ChgHdr& h = hp<ChgHdr>(s, L.chghdr)[c];
+    si.base = h.base; si.coff = h.col_off; si.clen = h.col_len;
+    si.row0 = hp<uint32_t>(s, L.rowbase)[k];
+    si.ent0 = hp<uint32_t>(s, L.entbase)[k];
+    si.nr = ((k + 1 < s.napplied) ? hp<uint32_t>(s, L.rowbase)[k + 1] : s.nrows) - si.row0;
+    si.ne = ((k + 1 < s.napplied) ? hp<uint32_t>(s, L.entbase)[k + 1] : s.nents) - si.ent0;
+    si.map = hp<uint32_t>(s, L.amap) + hp<uint32_t>(s, L.amb_out)[k];
+    si.nmap = h.nactors; si.self = si.map[0]; si.start_op = h.start_op; si.chg = c; si.is_change = 1;
+  }
+  return si;
+}
+
+// largest source whose first row (entry) is <= i; empty sources share the next source's start
+__device__ static uint32_t src_of(DocShared& s, uint32_t i, bool ents) {
+  const uint32_t nsrc = (s.has_base ? 1 : 0) + s.napplied;
+  const uint32_t* base = hp<uint32_t>(s, ents ? s.L.entbase : s.L.rowbase);
+  uint32_t lo = 0, hi = nsrc;  // first source with start > i
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    const uint32_t st = (s.has_base && m == 0) ? 0 : base[m - (s.has_base ? 1 : 0)];
+    if (st <= i) lo = m + 1; else hi = m;
+  }
+  return lo - 1;
+}
+
+// one stream: decodes n values into cells (utf8: (offset - span_lo) << 32 | length; boolean 0/1)
+__device__ static void decode_stream(DocShared& s, uint32_t item, int64_t* cells) {
+  const uint32_t src = item / DEC_STREAMS, j = item % DEC_STREAMS;
+  const uint32_t col = j < OC_VAL_RAW ? j : j + 1;
+  const SrcInfo si = src_info(s, src);
+  if (si.is_change && (col == OC_ID_ACTOR || col == OC_ID_CTR)) return;  // ids from the header (new.js:708-709)
+  const uint32_t n = j < DEC_ROWCOLS ? si.nr : si.ne;
+  int64_t* dst = cells + (uint64_t)DEC_ROWCOLS * si.row0 + 2ull * si.ent0 +
+                 (j < DEC_ROWCOLS ? (uint64_t)j * si.nr : (uint64_t)DEC_ROWCOLS * si.nr + (uint64_t)(j - DEC_ROWCOLS) * si.ne);
+  const uint8_t type = kOpColDec[col];
+  const uint64_t off = si.base + si.coff[col];
+  ColDec d;
+  cd_init(d, type, AV(s) + off, si.clen[col]);
+  const int64_t sbase = (int64_t)(off - s.b.span_lo);
+  for (uint32_t i = 0; i < n; i++) {
+    int64_t v;
+    uint32_t e;
+    if (type == DT_BOOL) {
+      bool bv;
+      e = cd_next_bool(d, bv);
+      v = bv;
+    } else {
+      bool isnull;
+      uint32_t l;
+      int64_t x;
+      e = cd_next(d, x, isnull, l);
+      if (isnull) v = AM_NULL64;
+      else if (type == DT_UTF8) v = ((sbase + x) << 32) | (int64_t)l;
+      else if (type == DT_DELTA) v = (d.absolute += x);
+      else v = x;
+    }
+    if (e) { set_err(s, e, 0, 0, 0, 0, si.chg); return; }
+    dst[i] = v;
+  }
+}
+
+// row i from the cells (lane per row)
+__device__ static void gather_row(DocShared& s, uint32_t i, const int64_t* cells, uint32_t* vsum, uint32_t* psum) {
+  const uint32_t src = src_of(s, i, false);
+  const SrcInfo si = src_info(s, src);
+  const uint32_t q = i - si.row0, nr = si.nr;
+  const int64_t* c = cells + (uint64_t)DEC_ROWCOLS * si.row0 + 2ull * si.ent0 + q;
+  bool bad = false;
+  auto mapact = [&](int64_t v) -> int32_t {
+    if (v == AM_NULL64) return -1;
+    if (si.is_change) {
+      if (v < 0 || v >= (int64_t)si.nmap) { set_err(s, AM_E_NO_ACTOR_INDEX, v, 0, 0, 0, si.chg); bad = true; return -1; }
+      return (int32_t)si.map[v];
+    }
+    if (v < 0 || v >= (int64_t)s.nactors) { set_err(s, AM_U_VALUE); bad = true; return -1; }
+    return (int32_t)v;
+  };
+  Row r;
+  r.obj_actor = mapact(c[0]);
+  r.obj_ctr = c[(uint64_t)1 * nr];
+  r.key_actor = mapact(c[(uint64_t)2 * nr]);
+  r.key_ctr = c[(uint64_t)3 * nr];
+  const int64_t ks = c[(uint64_t)4 * nr];
+  if (ks == AM_NULL64) { r.key_len = AM_NOSTR; r.key_off = 0; }
+  else {
+    r.key_len = (uint32_t)(ks & 0xffffffff);
+    r.key_off = s.b.span_lo + (uint64_t)(ks >> 32);
+    if (!utf8_valid_dev(AV(s) + r.key_off, r.key_len)) { set_err(s, AM_U_UTF8); bad = true; }
+  }
+  if (si.is_change) { r.id_actor = (int32_t)si.self; r.id_ctr = si.start_op + q; }
+  else { r.id_actor = mapact(c[(uint64_t)5 * nr]); r.id_ctr = c[(uint64_t)6 * nr]; }
+  r.insert = c[(uint64_t)7 * nr] != 0;
+  r.action = c[(uint64_t)8 * nr];
+  r.val_len = c[(uint64_t)9 * nr];
+  r.chld_actor = mapact(c[(uint64_t)10 * nr]);
+  r.chld_ctr = c[(uint64_t)11 * nr];
+  const int64_t pc = c[(uint64_t)12 * nr];
+  r.ps_cnt = pc == AM_NULL64 ? 0 : (uint32_t)pc;
+  r.src_change = (uint8_t)si.is_change;
+  r.is_del = si.is_change && r.action == 3;
+  r.flags = 0;
+  r.val_off = 0;
+  r.ps_off = 0;
+  (void)bad;
+  hp<Row>(s, s.L.rows)[i] = r;
+  vsum[i] = r.val_len == AM_NULL64 ? 0u : (uint32_t)((uint64_t)r.val_len >> 4);
+  psum[i] = r.ps_cnt;
+}
+
+__device__ static void gather_ent(DocShared& s, uint32_t j, const int64_t* cells) {
+  const uint32_t src = src_of(s, j, true);
+  const SrcInfo si = src_info(s, src);
+  const uint32_t q = j - si.ent0;
+  const int64_t* c = cells + (uint64_t)DEC_ROWCOLS * si.row0 + 2ull * si.ent0 + (uint64_t)DEC_ROWCOLS * si.nr + q;
+  const int64_t a = c[0], ctr = c[si.ne];
+  Ent e;
+  e.row = -1;
+  e.ctr = ctr;
+  e.actor = -1;
+  if (a == AM_NULL64 || ctr == AM_NULL64) { set_err(s, AM_U_VALUE); }
+  else if (si.is_change) {
+    if (a < 0 || a >= (int64_t)si.nmap) set_err(s, AM_E_NO_ACTOR_INDEX, a, 0, 0, 0, si.chg);
+    else e.actor = (int32_t)si.map[a];
+  } else {
+    if (a < 0 || a >= (int64_t)s.nactors) set_err(s, AM_U_VALUE);
+    else e.actor = (int32_t)a;
+  }
+  hp<Ent>(s, s.L.ents)[j] = e;
+}
+
+// after the scans: raw value offsets and group offsets of each row; per-source totals checked
+__device__ static void place_row(DocShared& s, uint32_t i, const uint32_t* vsum, const uint32_t* psum) {
+  const uint32_t src = src_of(s, i, false);
+  const SrcInfo si = src_info(s, src);
+  Row& r = hp<Row>(s, s.L.rows)[i];
+  r.val_off = si.base + si.coff[OC_VAL_RAW] + (vsum[i] - vsum[si.row0]);
+  r.ps_off = psum[i];
+  if (i + 1 == si.row0 + si.nr) {  // last row of its source
+    const uint64_t vend = (uint64_t)(vsum[i] - vsum[si.row0]) + (r.val_len == AM_NULL64 ? 0 : ((uint64_t)r.val_len >> 4));
+    if (vend > si.clen[OC_VAL_RAW]) set_err(s, AM_E_SUBARRAY, 0, 0, 0, 0, si.chg);
+    if (psum[i] + r.ps_cnt - psum[si.row0] != si.ne) set_err(s, AM_U_VALUE);
+  }
+}
+
+// base document change rows (DOCUMENT_COLUMNS), one column per lane
+__device__ static void decode_base_chg_col(DocShared& s, uint32_t col) {
+  ChgRow* chg = hp<ChgRow>(s, s.L.chg);
+  int64_t* deps = hp<int64_t>(s, s.L.deps);
+  const APtr A = AV(s);
+  const uint64_t off = s.dh.base + s.dh.ccol_off[col];
+  const uint32_t len = s.dh.ccol_len[col];
+  const uint32_t n = s.nbc;
+  ColDec d;
+  uint32_t e = AM_OK;
+  switch (col) {
+    case DC_ACTOR: case DC_SEQ: case DC_MAXOP: case DC_TIME: case DC_EXTRA_LEN: {
+      cd_init(d, (col == DC_ACTOR || col == DC_EXTRA_LEN) ? DT_UINT : DT_INT, A + off, len);
+      uint64_t acc = 0;
+      for (uint32_t i = 0; i < n; i++) {
+        int64_t v;
+        if ((e = (col == DC_ACTOR || col == DC_EXTRA_LEN) ? cd_next_int(d, v) : cd_next_delta(d, v))) break;
+        ChgRow& r = chg[i];
+        if (col == DC_ACTOR) r.actor = v;
+        else if (col == DC_SEQ) r.seq = v;
+        else if (col == DC_MAXOP) r.max_op = v;
+        else if (col == DC_TIME) r.time = v;
+        else {
+          r.extra_len = v;
+          uint64_t nb = (v == AM_NULL64) ? 0 : ((uint64_t)v >> 4);
+          if (acc + nb > s.dh.ccol_len[DC_EXTRA_RAW]) { e = AM_E_SUBARRAY; break; }
+          r.extra_off = s.dh.base + s.dh.ccol_off[DC_EXTRA_RAW] + acc;
+          r.extra_raw_len = (uint32_t)nb;
+          acc += nb;
+        }
+      }
+      break;
+    }
+    case DC_MESSAGE: {
+      cd_init(d, DT_UTF8, A + off, len);
+      for (uint32_t i = 0; i < n; i++) {
+        uint64_t so;
+        uint32_t sl;
+        if ((e = cd_next_str(d, so, sl))) break;
+        chg[i].msg_len = sl;
+        chg[i].msg_off = sl == AM_NOSTR ? 0 : off + so;
+        if (sl != AM_NOSTR && !utf8_valid_dev(A + off + so, sl)) { set_err(s, AM_U_UTF8); return; }
+      }
+      break;
+    }
+    case DC_DEPS_NUM: {
+      cd_init(d, DT_UINT, A + off, len);
+      uint32_t acc = 0;
+      for (uint32_t i = 0; i < n; i++) {
+        int64_t v;
+        if ((e = cd_next_int(d, v))) break;
+        uint32_t c = v == AM_NULL64 ? 0 : (uint32_t)v;
+        chg[i].ndeps = c;
+        chg[i].deps_off = acc;
+        acc += c;
+      }
+      break;
+    }
+    case DC_DEPS_INDEX: {
+      cd_init(d, DT_INT, A + off, len);
+      for (uint32_t j = 0; j < s.nbd; j++) {
+        int64_t v;
+        if ((e = cd_next_delta(d, v))) break;
+        deps[j] = v;
+      }
+      break;
+    }
+    default: break;
+  }
+  if (e) set_err(s, e);
+}
+
+// ---- P6: canonical column encoders, one column at a time by the whole wave
+// (RLEEncoder / DeltaEncoder / BooleanEncoder, encoding.js:558-1135). A column's values are
+// gathered into V; delta columns are differenced into W (nulls keep the running value); then
+//   run starts (value != previous) -> maximal runs (scan + scatter of the start positions),
+//   runs >= 2 -> repetition records, null runs -> null records, adjacent single values -> one
+//   literal record (groups found with a scan over the runs, sized with LDS atomics),
+//   record bytes -> exclusive scan -> every run writes its record at its own offset.
+// An all-null RLE column encodes to nothing. ----
+enum : uint8_t { EK_U = 0, EK_D = 1, EK_S = 2, EK_B = 3, EK_W = 4 };
+// output columns: DOC_OPS_COLUMNS (0..15) then DOCUMENT_COLUMNS (16..24)
+__device__ __constant__ static const uint8_t kEncKind[OC_NCOLS + DC_NCOLS] = {
+    EK_U, EK_U, EK_U, EK_D, EK_S, EK_U, EK_D, EK_B, EK_U, EK_U, EK_W, EK_U, EK_D, EK_U, EK_U, EK_D,
+    EK_U, EK_D, EK_D, EK_D, EK_S, EK_U, EK_D, EK_U, EK_W};
+
+struct EncCtx {
+  int64_t* V;
+  int64_t* W;
+  uint32_t *S, *RS, *RB, *RG;
+  const uint8_t* As;  // input bytes at span_lo
+};
+
+__device__ __forceinline__ bool enc_eq(uint8_t kind, int64_t a, int64_t b, const uint8_t* As) {
+  if (kind != EK_S || a == AM_NULL64 || b == AM_NULL64) return a == b;
+  const uint32_t la = (uint32_t)(a & 0xffffffff), lb = (uint32_t)(b & 0xffffffff);
+  return la == lb && bytes_eq(As + (a >> 32), As + (b >> 32), la);
+}
+__device__ __forceinline__ uint32_t enc_vsize(uint8_t kind, int64_t v) {
+  if (kind == EK_U) return uleb_len((uint64_t)v);
+  if (kind == EK_D) return sleb_len(v);
+  const uint32_t l = (uint32_t)(v & 0xffffffff);
+  return uleb_len(l) + l;
+}
+__device__ __forceinline__ uint8_t* enc_put(uint8_t kind, uint8_t* o, int64_t v, const uint8_t* As) {
+  if (kind == EK_U) return put_uleb(o, (uint64_t)v);
+  if (kind == EK_D) return put_sleb(o, v);
+  const uint32_t l = (uint32_t)(v & 0xffffffff);
+  o = put_uleb(o, l);
+  const uint8_t* p = As + (v >> 32);
+  for (uint32_t q = 0; q < l; q++) o[q] = p[q];
+  return o + l;
+}
+
+// Encodes the n values of column c (V already filled) into out; returns the byte length.
+__device__ static uint32_t encode_column(uint8_t kind, uint32_t n, uint8_t* out, EncCtx& x, uint32_t* s_flag) {
+  const uint32_t t = threadIdx.x;
+  if (n == 0) return 0;
+  int64_t* X = x.V;
+  if (kind == EK_D) {  // differences against the previous non-null value
+    int32_t carry = -1;
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t i = base + t;
+      const int64_t v = i < n ? x.V[i] : AM_NULL64;
+      const int32_t inc = wave_incl_max(v != AM_NULL64 ? (int32_t)i : -1);
+      int32_t prev = __shfl_up(inc, 1, 64);
+      if (t == 0) prev = -1;
+      if (carry > prev) prev = carry;
+      if (i < n) x.W[i] = v == AM_NULL64 ? AM_NULL64 : v - (prev >= 0 ? x.V[prev] : 0);
+      const int32_t top = __shfl(inc, 63, 64);
+      if (top > carry) carry = top;
+    }
+    X = x.W;
+    __syncthreads();
+  }
+  // maximal runs: start positions compacted into RS
+  uint32_t nr = 0;
+  for (uint32_t base = 0; base < n; base += 64) {
+    const uint32_t i = base + t;
+    const uint32_t f = (i < n && (kind == EK_W || i == 0 || !enc_eq(kind, X[i], X[i - 1], x.As))) ? 1u : 0u;
+    const uint32_t inc = wave_incl_add(f);
+    if (f) x.RS[nr + inc - 1] = i;
+    nr += __shfl(inc, 63, 64);
+  }
+  const bool rle = kind <= EK_S;
+  for (uint32_t r = t; r < nr; r += 64) x.S[r] = 0;
+  __syncthreads();
+  // classify runs; literal groups (consecutive single-value runs) get ids and sizes
+  bool any = false;
+  if (rle) {
+    uint32_t gcarry = 0, prev_single = 0;
+    for (uint32_t base = 0; base < nr; base += 64) {
+      const uint32_t r = base + t;
+      uint32_t single = 0;
+      if (r < nr) {
+        const uint32_t i0 = x.RS[r], i1 = r + 1 < nr ? x.RS[r + 1] : n;
+        const bool isnull = X[i0] == AM_NULL64;
+        single = (!isnull && i1 - i0 == 1) ? 1u : 0u;
+        any |= !isnull;
+      }
+      uint32_t ps = __shfl_up(single, 1, 64);
+      if (t == 0) ps = prev_single;
+      const uint32_t gs = (single && !ps) ? 1u : 0u;
+      const uint32_t ginc = wave_incl_add(gs);
+      if (r < nr) {
+        const uint32_t gid = gcarry + ginc - 1;
+        x.RG[r] = single ? (gid | (gs << 31)) : 0xffffffffu;
+        if (single) atomicAdd(&x.S[gid], 1u);
+      }
+      prev_single = __shfl(single, 63, 64);
+      gcarry += __shfl(ginc, 63, 64);
+    }
+    any = __any(any);
+    if (!any) return 0;  // all-null column (wave-uniform)
+    __syncthreads();
+  }
+  // record bytes -> offsets
+  uint32_t total = 0;
+  for (uint32_t base = 0; base < nr; base += 64) {
+    const uint32_t r = base + t;
+    uint32_t bytes = 0;
+    if (r < nr) {
+      const uint32_t i0 = x.RS[r], i1 = r + 1 < nr ? x.RS[r + 1] : n, len = i1 - i0;
+      const int64_t v = X[i0];
+      if (kind == EK_B) bytes = uleb_len(len) + ((r == 0 && v) ? 1u : 0u);
+      else if (kind == EK_W) bytes = (uint32_t)(v & 0xffffffff);
+      else if (v == AM_NULL64) bytes = 1 + uleb_len(len);
+      else if (len >= 2) bytes = sleb_len((int64_t)len) + enc_vsize(kind, v);
+      else {
+        const uint32_t g = x.RG[r];
+        bytes = enc_vsize(kind, v) + ((g >> 31) ? sleb_len(-(int64_t)x.S[g & 0x7fffffff]) : 0u);
+      }
+    }
+    const uint32_t inc = wave_incl_add(bytes);
+    if (r < nr) x.RB[r] = total + inc - bytes;
+    total += __shfl(inc, 63, 64);
+  }
+  // write records
+  for (uint32_t r = t; r < nr; r += 64) {
+    const uint32_t i0 = x.RS[r], i1 = r + 1 < nr ? x.RS[r + 1] : n, len = i1 - i0;
+    const int64_t v = X[i0];
+    uint8_t* o = out + x.RB[r];
+    if (kind == EK_B) {
+      if (r == 0 && v) *o++ = 0;
+      put_uleb(o, len);
+    } else if (kind == EK_W) {
+      const uint32_t l = (uint32_t)(v & 0xffffffff);
+      const uint8_t* p = x.As + (v >> 32);
+      for (uint32_t q = 0; q < l; q++) o[q] = p[q];
+    } else if (v == AM_NULL64) {
+      *o++ = 0;
+      put_uleb(o, len);
+    } else if (len >= 2) {
+      o = put_sleb(o, (int64_t)len);
+      enc_put(kind, o, v, x.As);
+    } else {
+      const uint32_t g = x.RG[r];
+      if (g >> 31) o = put_sleb(o, -(int64_t)x.S[g & 0x7fffffff]);
+      enc_put(kind, o, v, x.As);
+    }
+  }
+  (void)s_flag;
+  __syncthreads();
+  return total;
+}
+
+__device__ __forceinline__ bool same_obj(const Row& a, const Row& b) {
+  return a.obj_ctr == b.obj_ctr && a.obj_actor == b.obj_actor;
+}
+
+// binary search of (ctr, actor) in the id index; returns row or -1
+__device__ static int32_t id_lookup(const IdKey* idk, uint32_t n, int64_t ctr, int32_t actor) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1;
+    const IdKey& k = idk[mid];
+    if (k.ctr < ctr || (k.ctr == ctr && k.actor < actor)) lo = mid + 1; else hi = mid;
+  }
+  if (lo < n && idk[lo].ctr == ctr && idk[lo].actor == actor) return idk[lo].row;
+  return -1;
+}
+
+
+__global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
+                                               const am_doc_desc* __restrict__ docs, const am_known_hash* __restrict__ known,
+                                               const ChunkInfo* __restrict__ info, const DocBounds* __restrict__ bounds,
+                                               const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base,
+                                               uint64_t ws_cap, uint32_t lds_bytes, am_doc_result* __restrict__ results,
+                                               int32_t* __restrict__ chg_state) {
+  __shared__ DocShared s;
+  const uint32_t doc = blockIdx.x, t = threadIdx.x, T = blockDim.x;
+  const am_doc_desc dd = docs[doc];
+  uint8_t* const wsg = ws_base + ws_off[doc];  // global (derived from the kernel argument)
+  if (t == 0) {
+    s.b = bounds[doc];
+    s.ws = ws_base + ws_off[doc];
+    s.L = ws_layout(s.b);
+    // hot working set in LDS when it fits (this namespace's mode decides who runs the document)
+    s.hot = kHotLds ? am_lds : s.ws;
+    s.A = arena;
+    s.status = AM_OK; s.errchg = 0xffffffffu; s.arg0 = s.arg1 = 0; s.arg_actor_off = 0; s.arg_actor_len = 0;
+    s.has_base = dd.base_chunk >= 0;
+    s.nb = s.nbe = s.nbc = s.nbd = 0;
+    s.napplied = s.nqueued = s.nactors = s.nheads = 0;
+    s.nrows = s.nents = s.nchg = s.ndeps = s.nout = s.nnew = 0;
+    s.max_op = 0;
+    s.out_len = 0;
+    s.ph_last = clock64();
+    if (ws_off[doc] + s.L.total > ws_cap) set_err(s, AM_U_CAPACITY);
+    // chunk-level errors: the base document first (load), then changes in order (new.js:1798)
+    if (s.has_base) {
+      const ChunkInfo& ci = info[dd.base_chunk];
+      if (ci.status) set_err(s, ci.status, ci.arg0);
+      else if (ci.type != 0) set_err(s, AM_E_CHUNK_TYPE, ci.type);
+      else { s.nb = ci.nops; s.nbe = ci.nents; s.nbc = ci.nchg; s.nbd = ci.ndeps; }
+    }
+    for (uint32_t k = 0; k < dd.chg_count && s.status == AM_OK; k++) {
+      const ChunkInfo& ci = info[dd.chg_begin + k];
+      if (ci.status) set_err(s, ci.status, ci.arg0, 0, 0, 0, k);
+      else if (ci.type != 1) set_err(s, AM_E_CHUNK_TYPE, ci.type, 0, 0, 0, k);
+    }
+    if (s.b.R == 0 && s.b.N == 0 && !s.has_base && dd.chg_count) set_err(s, AM_U_CAPACITY);
+  }
+  __syncthreads();
+  if ((s.L.hot_total <= lds_bytes) != kHotLds) return;  // the other mode's document
+  const WsLayout& L = s.L;
+  if (s.status) goto done;
+  // P0: stage the document's input bytes (base + changes, adjacent in the arena) into the hot
+  // region with 16-byte coalesced loads; every later parse/decode reads them from there.
+  if constexpr (kHotLds) {
+    const uint64_t lo = s.b.span_lo, n = s.b.span_hi - s.b.span_lo;
+    uint8_t* dst = am_lds + L.input;
+    if (n) {
+      const uint64_t head = (16 - (lo & 15)) & 15;  // bytes before the first 16-aligned source address
+      for (uint64_t q = t; q < head && q < n; q += T) dst[q] = arena[lo + q];
+      if (n > head) {
+        const uint64_t nv = (n - head) / 16;
+        for (uint64_t v = t; v < nv; v += T) {
+          const uint4 x = *reinterpret_cast<const uint4*>(arena + lo + head + 16 * v);
+          uint8_t* o = dst + head + 16 * v;
+          const uint8_t* xb = reinterpret_cast<const uint8_t*>(&x);
+#pragma unroll
+          for (int k = 0; k < 16; k++) o[k] = xb[k];
+        }
+        for (uint64_t q = head + 16 * nv + t; q < n; q += T) dst[q] = arena[lo + q];
+      }
+    }
+  }
+  __syncthreads();
+  PH(0);
+  // P1: base document header, change headers (lane per change), base change rows (lane per column)
+  if (t == 0 && s.has_base) {
+    const ChunkInfo& ci = info[dd.base_chunk];
+    const am_chunk_desc cd = chunks[dd.base_chunk];
+    parse_doc_hdr(AV(s) + cd.off + ci.data_off, ci.data_len, cd.off + ci.data_off, s.dh);
+  }
+  if (t == 0 && !s.has_base) { s.dh.nactors = 0; s.dh.nheads = 0; s.dh.has_hidx = 0; s.dh.extra_len = 0; s.dh.base = 0; }
+  for (uint32_t k = t; k < dd.chg_count; k += T) {
+    const ChunkInfo& ci = info[dd.chg_begin + k];
+    const am_chunk_desc cd = chunks[dd.chg_begin + k];
+    ChgHdr& h = hp<ChgHdr>(s, L.chghdr)[k];
+    parse_change_hdr(AV(s) + cd.off + ci.data_off, ci.data_len, cd.off + ci.data_off, h);
+  }
+  if (t == 0) {  // prefix offsets of the change actor lists and deps
+    uint32_t am = 0, db = 0;
+    for (uint32_t k = 0; k < dd.chg_count; k++) {
+      hp<uint32_t>(s, L.ambase)[k] = am;
+      hp<uint32_t>(s, L.dbase)[k] = db;
+      am += info[dd.chg_begin + k].nactors;
+      db += info[dd.chg_begin + k].ndeps;
+    }
+  }
+  __syncthreads();
+  if (s.has_base)
+    for (uint32_t c = t; c < DC_NCOLS; c += T) decode_base_chg_col(s, c);
+#if defined(AM_STOP_PHASE) && AM_STOP_PHASE == 1
+  goto done;
+#endif
+  PH(1);
+  // P2: plan -- lane-parallel lookups, then the sequential causal queue on integers
+  plan_lookups(s, dd, info, known);
+  __syncthreads();
+  if (s.status) goto done;
+  PH(2);
+  if (t == 0) plan_doc(s, dd, info, chg_state);
+  __syncthreads();
+  if (s.status) goto done;
+  {
+    const APtr A = AV(s);
+    Row* rows = hp<Row>(s, L.rows);
+    Ent* ents = hp<Ent>(s, L.ents);
+    ActorRef* actors = hp<ActorRef>(s, L.actors);
+    const uint32_t R = s.nrows;
+    PH(3);
+    // P4: decode every (source, column) stream into cells, then gather rows and entries
+    int64_t* cells = hp<int64_t>(s, L.cells);
+    uint32_t* vsum = hp<uint32_t>(s, L.scan);
+    uint32_t* psum = hp<uint32_t>(s, L.succ_cnt);
+    const uint32_t nsrc = (s.has_base ? 1 : 0) + s.napplied;
+#if defined(AM_STOP_PHASE) && AM_STOP_PHASE == 2
+    goto done;
+#endif
+    for (uint32_t it = t; it < nsrc * DEC_STREAMS; it += T) decode_stream(s, it, cells);
+    for (uint32_t src = t; src < nsrc; src += T) {
+      const SrcInfo si = src_info(s, src);
+      if (si.nr == 0 && si.ne != 0) set_err(s, AM_U_VALUE);  // group entries without ops
+    }
+    // actor ranks (lexicographic order of the hex ids)
+    for (uint32_t i = t; i < s.nactors; i += T) {
+      uint32_t rank = 0;
+      for (uint32_t j = 0; j < s.nactors; j++)
+        if (actor_cmp_dev(A + actors[j].off, actors[j].len, A + actors[i].off, actors[i].len) < 0) rank++;
+      actors[i].rank = rank;
+    }
+    __syncthreads();
+    if (s.status) goto done;
+    PH(4);
+    for (uint32_t i = t; i < R; i += T) gather_row(s, i, cells, vsum, psum);
+    for (uint32_t j = t; j < s.nents; j += T) gather_ent(s, j, cells);
+    __syncthreads();
+    if (s.status) goto done;
+    wave_excl_scan_arr(vsum, R);
+    wave_excl_scan_arr(psum, R);
+    __syncthreads();
+    for (uint32_t i = t; i < R; i += T) place_row(s, i, vsum, psum);
+    __syncthreads();
+    if (s.status) goto done;
+#if defined(AM_STOP_PHASE) && AM_STOP_PHASE == 3
+    goto done;
+#endif
+
+    PH(5);
+    // P5a: per-op checks of change rows (readNextChangeOp new.js:715-723; mergeDocChangeOps shapes)
+    for (uint32_t i = t; i < R; i += T) {
+      const Row& r = rows[i];
+      if (r.id_ctr == AM_NULL64 || r.id_actor < 0) { set_err(s, AM_U_VALUE); continue; }
+      if (!r.src_change) continue;
+      if ((r.obj_ctr == AM_NULL64) != (r.obj_actor < 0)) { set_err(s, AM_E_MISMATCH_OBJ, r.obj_ctr, r.obj_actor); continue; }
+      if ((r.key_ctr == AM_NULL64 && r.key_actor >= 0) || (r.key_ctr == 0 && r.key_actor >= 0) ||
+          (r.key_ctr != AM_NULL64 && r.key_ctr > 0 && r.key_actor < 0)) {
+        set_err(s, AM_E_MISMATCH_KEY, r.key_ctr, r.key_actor);
+        continue;
+      }
+      if (r.action == AM_NULL64) { set_err(s, AM_U_VALUE); continue; }
+      if (r.is_del && (r.insert || r.ps_cnt == 0)) { set_err(s, AM_U_DEL_SHAPE); continue; }
+      if (r.insert && r.ps_cnt > 0) {
+        const Ent& p = ents[r.ps_off];
+        set_err(s, AM_E_PRED_NOT_FOUND, p.ctr, 0, actors[p.actor].off, actors[p.actor].len);
+        continue;
+      }
+      if (r.key_len == AM_NOSTR && !r.insert && r.key_ctr == AM_NULL64) { set_err(s, AM_U_VALUE); continue; }
+    }
+    // P5c: id index sorted by (ctr, actor index)
+    const uint32_t PR = pow2_ceil(R > 0 ? R : 1);
+    IdKey* idk = hp<IdKey>(s, L.idk);
+    for (uint32_t i = t; i < PR; i += T) {
+      IdKey k;
+      if (i < R) { k.ctr = rows[i].id_ctr; k.actor = rows[i].id_actor; k.row = (int32_t)i; }
+      else { k.ctr = INT64_MAX; k.actor = INT32_MAX; k.row = INT32_MAX; }
+      idk[i] = k;
+    }
+    __syncthreads();
+    if (s.status) goto done;
+    block_bitonic_sort(idk, PR, [](const IdKey& a, const IdKey& b) {
+      if (a.ctr != b.ctr) return a.ctr < b.ctr;
+      if (a.actor != b.actor) return a.actor < b.actor;
+      return a.row < b.row;
+    });
+    for (uint32_t i = t + 1; i < R; i += T)
+      if (idk[i].ctr == idk[i - 1].ctr && idk[i].actor == idk[i - 1].actor)
+        set_err(s, AM_E_DUP_OPID, idk[i].ctr, 0, actors[idk[i].actor].off, actors[idk[i].actor].len);
+    __syncthreads();
+    if (s.status) goto done;
+
+    PH(6);
+    auto id_less = [&](int64_t c1, int32_t a1, int64_t c2, int32_t a2) {
+      if (c1 != c2) return c1 < c2;
+      return actors[a1].rank < actors[a2].rank;
+    };
+    // P5d: resolve preds -> targets (new.js:1173-1188, 1254-1258)
+    int32_t* elem_of = hp<int32_t>(s, L.elem_of);
+    int32_t* parent = hp<int32_t>(s, L.parent);
+    for (uint32_t i = t; i < R; i += T) {
+      const Row& r = rows[i];
+      elem_of[i] = -1;
+      parent[i] = -1;
+      if (!r.src_change || r.insert) continue;
+      for (uint32_t q = 0; q < r.ps_cnt; q++) {
+        Ent& p = ents[r.ps_off + q];
+        int32_t tr = id_lookup(idk, R, p.ctr, p.actor);
+        bool ok = tr >= 0 && (uint32_t)tr < i && !rows[tr].is_del;
+        if (ok) {
+          const Row& x = rows[tr];
+          ok = same_obj(x, r) && id_less(x.id_ctr, x.id_actor, r.id_ctr, r.id_actor);
+          if (ok) {
+            if (r.key_len != AM_NOSTR) {
+              ok = x.key_len == r.key_len && bytes_eq(A + x.key_off, A + r.key_off, r.key_len);
+            } else {
+              int64_t ec = x.insert ? x.id_ctr : x.key_ctr;
+              int32_t ea = x.insert ? x.id_actor : x.key_actor;
+              ok = x.key_len == AM_NOSTR && ec == r.key_ctr && ea == r.key_actor;
+            }
+          }
+        }
+        if (!ok) { set_err(s, AM_E_PRED_NOT_FOUND, p.ctr, 0, actors[p.actor].off, actors[p.actor].len); break; }
+        p.row = tr;
+      }
+    }
+    __syncthreads();
+    if (s.status) goto done;
+    // P5e: list elements: reference elements of inserts, target elements of updates
+    for (uint32_t i = t; i < R; i += T) {
+      const Row& r = rows[i];
+      if (r.key_len != AM_NOSTR || r.is_del) continue;
+      if (r.insert) {
+        elem_of[i] = (int32_t)i;
+        if (r.key_ctr == AM_NULL64 || r.key_ctr == 0 || r.key_actor < 0) { parent[i] = -1; continue; }
+        int32_t p = id_lookup(idk, R, r.key_ctr, r.key_actor);
+        bool ok = p >= 0 && rows[p].insert && !rows[p].is_del && same_obj(rows[p], r) && rows[p].key_len == AM_NOSTR &&
+                  (!r.src_change || (uint32_t)p < i);
+        if (!ok) {
+          if (r.src_change) set_err(s, AM_E_REF_NOT_FOUND, r.key_ctr, 0, actors[r.key_actor].off, actors[r.key_actor].len);
+          else set_err(s, AM_U_VALUE);
+          continue;
+        }
+        if (!(rows[p].id_ctr < r.id_ctr)) { set_err(s, AM_U_NONCAUSAL); continue; }
+        parent[i] = p;
+      } else {
+        int32_t e = (r.key_actor >= 0) ? id_lookup(idk, R, r.key_ctr, r.key_actor) : -1;
+        bool ok = e >= 0 && rows[e].insert && !rows[e].is_del && same_obj(rows[e], r) && rows[e].key_len == AM_NOSTR &&
+                  (!r.src_change || (uint32_t)e < i);
+        if (!ok) {
+          if (r.src_change) set_err(s, AM_E_ELEM_NOT_FOUND, r.key_ctr, 0, r.key_actor >= 0 ? actors[r.key_actor].off : 0,
+                                    r.key_actor >= 0 ? actors[r.key_actor].len : 0);
+          else set_err(s, AM_U_VALUE);
+          continue;
+        }
+        if (!id_less(rows[e].id_ctr, rows[e].id_actor, r.id_ctr, r.id_actor)) { set_err(s, AM_U_NONCAUSAL); continue; }
+        elem_of[i] = e;
+      }
+    }
+    __syncthreads();
+    if (s.status) goto done;
+
+    PH(7);
+    // P5f: RGA order = preorder of the reference-element tree with children in descending opId
+    // order (new.js:145-163). Euler tour + Wyllie list ranking (pointer jumping).
+    uint32_t* scan = hp<uint32_t>(s, L.scan);
+    for (uint32_t i = t; i < R; i += T) scan[i] = (elem_of[i] == (int32_t)i) ? 1u : 0u;
+    __syncthreads();
+    const uint32_t M = block_excl_scan(scan, R, s.tmp);
+    const uint32_t PM = pow2_ceil(M > 0 ? M : 1);
+    ElemKey* ek = hp<ElemKey>(s, L.elemk);
+    for (uint32_t i = t; i < R; i += T)
+      if (elem_of[i] == (int32_t)i) {
+        const Row& r = rows[i];
+        ElemKey k;
+        k.obj_ctr = r.obj_ctr == AM_NULL64 ? -1 : r.obj_ctr;
+        k.obj_rank = r.obj_actor < 0 ? -1 : (int32_t)actors[r.obj_actor].rank;
+        k.parent = parent[i];
+        k.id_ctr = r.id_ctr;
+        k.id_rank = (int32_t)actors[r.id_actor].rank;
+        k.row = (int32_t)i;
+        ek[scan[i]] = k;
+      }
+    for (uint32_t i = M + t; i < PM; i += T) { ElemKey k; k.obj_ctr = INT64_MAX; k.row = -1; k.obj_rank = 0; k.parent = 0; k.id_ctr = 0; k.id_rank = 0; ek[i] = k; }
+    __syncthreads();
+    block_bitonic_sort(ek, PM, [](const ElemKey& a, const ElemKey& b) {
+      if (a.obj_ctr != b.obj_ctr) return a.obj_ctr < b.obj_ctr;
+      if (a.obj_rank != b.obj_rank) return a.obj_rank < b.obj_rank;
+      if (a.parent != b.parent) return a.parent < b.parent;
+      if (a.id_ctr != b.id_ctr) return a.id_ctr > b.id_ctr;  // children: descending opId
+      return a.id_rank > b.id_rank;
+    });
+    int32_t* first_child = hp<int32_t>(s, L.first_child);
+    int32_t* next_sib = hp<int32_t>(s, L.next_sib);
+    for (uint32_t i = t; i < R; i += T) { first_child[i] = -1; next_sib[i] = -1; }
+    __syncthreads();
+    auto same_group = [&](const ElemKey& a, const ElemKey& b) {
+      return a.obj_ctr == b.obj_ctr && a.obj_rank == b.obj_rank && a.parent == b.parent;
+    };
+    for (uint32_t i = t; i < M; i += T) {
+      const ElemKey& k = ek[i];
+      if (i + 1 < M && same_group(k, ek[i + 1])) next_sib[k.row] = ek[i + 1].row;
+      if ((i == 0 || !same_group(ek[i - 1], k)) && k.parent >= 0) first_child[k.parent] = k.row;
+    }
+    __syncthreads();
+    int32_t* nxtA = hp<int32_t>(s, L.tour_nxt);
+    int32_t* nxtB = nxtA + 2 * R;
+    int32_t* wA = hp<int32_t>(s, L.tour_w);
+    int32_t* wB = wA + 2 * R;
+    const int32_t END = -1;
+    for (uint32_t i = t; i < R; i += T) {
+      bool el = elem_of[i] == (int32_t)i;
+      nxtA[2 * i] = el ? (first_child[i] >= 0 ? 2 * first_child[i] : (int32_t)(2 * i + 1)) : END;
+      wA[2 * i] = el ? 1 : 0;
+      nxtA[2 * i + 1] = el ? (next_sib[i] >= 0 ? 2 * next_sib[i] : (parent[i] >= 0 ? 2 * parent[i] + 1 : END)) : END;
+      wA[2 * i + 1] = 0;
+    }
+    __syncthreads();
+    for (uint32_t span = 1; span < 2 * R; span <<= 1) {
+      for (uint32_t x = t; x < 2 * R; x += T) {
+        int32_t nx = nxtA[x];
+        if (nx != END) { wB[x] = wA[x] + wA[nx]; nxtB[x] = nxtA[nx]; }
+        else { wB[x] = wA[x]; nxtB[x] = END; }
+      }
+      __syncthreads();
+      int32_t* tp = nxtA; nxtA = nxtB; nxtB = tp;
+      tp = wA; wA = wB; wB = tp;
+    }
+    // wA[2v] = number of elements from v to the end of its object's list (suffix count)
+#if defined(AM_STOP_PHASE) && AM_STOP_PHASE == 4
+    goto done;
+#endif
+
+    PH(8);
+    // P5g: document order: object, then key (UTF-16) | element position, then opId
+    SortRec* sr = hp<SortRec>(s, L.sortrec);
+    for (uint32_t i = t; i < R; i += T) scan[i] = rows[i].is_del ? 0u : 1u;
+    __syncthreads();
+    const uint32_t NOUT = block_excl_scan(scan, R, s.tmp);
+    const uint32_t PO = pow2_ceil(NOUT > 0 ? NOUT : 1);
+    for (uint32_t i = t; i < R; i += T) {
+      const Row& r = rows[i];
+      if (r.is_del) continue;
+      SortRec k;
+      k.obj_ctr = r.obj_ctr == AM_NULL64 ? -1 : r.obj_ctr;
+      k.obj_rank = r.obj_actor < 0 ? -1 : (int32_t)actors[r.obj_actor].rank;
+      k.kind = r.key_len != AM_NOSTR ? 0 : 1;
+      k.k1 = k.kind ? -(int64_t)wA[2 * elem_of[i]] : 0;
+      k.key_off = r.key_off;
+      k.key_len = r.key_len;
+      k.id_ctr = r.id_ctr;
+      k.id_rank = (int32_t)actors[r.id_actor].rank;
+      k.row = (int32_t)i;
+      k.pad = 0;
+      sr[scan[i]] = k;
+    }
+    for (uint32_t i = NOUT + t; i < PO; i += T) { SortRec k; k.row = -1; k.obj_ctr = INT64_MAX; k.obj_rank = 0; k.kind = 0; k.k1 = 0; k.key_off = 0; k.key_len = 0; k.id_ctr = 0; k.id_rank = 0; k.pad = 0; sr[i] = k; }
+    __syncthreads();
+    block_bitonic_sort(sr, PO, [A](const SortRec& a, const SortRec& b) {
+      if ((a.row < 0) != (b.row < 0)) return b.row < 0;
+      if (a.row < 0) return false;
+      if (a.obj_ctr != b.obj_ctr) return a.obj_ctr < b.obj_ctr;
+      if (a.obj_rank != b.obj_rank) return a.obj_rank < b.obj_rank;
+      if (a.kind != b.kind) return a.kind < b.kind;
+      if (a.kind == 0) {
+        int c = utf16_cmp_dev(A + a.key_off, a.key_len, A + b.key_off, b.key_len);
+        if (c) return c < 0;
+      } else if (a.k1 != b.k1) {
+        return a.k1 < b.k1;
+      }
+      if (a.id_ctr != b.id_ctr) return a.id_ctr < b.id_ctr;
+      return a.id_rank < b.id_rank;
+    });
+
+    PH(9);
+    // P5h: succ lists = existing succ (base rows) merged with new succs from preds
+    NewEnt* ne = hp<NewEnt>(s, L.newent);
+    const uint32_t NNEW = s.nents - s.nbe;
+    const uint32_t PN = pow2_ceil(NNEW > 0 ? NNEW : 1);
+    for (uint32_t j = t; j < PN; j += T) {
+      NewEnt x;
+      x.target = j < NNEW ? ents[s.nbe + j].row : INT32_MAX;
+      x.ctr = 0; x.actor = 0; x.rank = 0; x.pad = 0;
+      ne[j] = x;
+    }
+    __syncthreads();
+    // owning op id of each pred entry
+    for (uint32_t i = t; i < R; i += T) {
+      const Row& r = rows[i];
+      if (!r.src_change) continue;
+      for (uint32_t q = 0; q < r.ps_cnt; q++) {
+        NewEnt& x = ne[r.ps_off + q - s.nbe];
+        x.ctr = r.id_ctr;
+        x.actor = r.id_actor;
+        x.rank = (int32_t)actors[r.id_actor].rank;
+      }
+    }
+    __syncthreads();
+    block_bitonic_sort(ne, PN, [](const NewEnt& a, const NewEnt& b) {
+      if (a.target != b.target) return a.target < b.target;
+      if (a.ctr != b.ctr) return a.ctr < b.ctr;
+      return a.rank < b.rank;
+    });
+    uint32_t* succ_cnt = hp<uint32_t>(s, L.succ_cnt);
+    auto new_range = [&](int32_t row, uint32_t& lo_out) -> uint32_t {
+      uint32_t lo = 0, hi = NNEW;
+      while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (ne[m].target < row) lo = m + 1; else hi = m; }
+      uint32_t a = lo;
+      hi = NNEW;
+      while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (ne[m].target <= row) lo = m + 1; else hi = m; }
+      lo_out = a;
+      return lo - a;
+    };
+    for (uint32_t i = t; i < NOUT; i += T) {
+      const Row& r = rows[sr[i].row];
+      uint32_t lo;
+      succ_cnt[i] = (r.src_change ? 0 : r.ps_cnt) + new_range(sr[i].row, lo);
+    }
+    __syncthreads();
+    const uint32_t NSUCC = block_excl_scan(succ_cnt, NOUT, s.tmp);
+    Ent* outent = hp<Ent>(s, L.outent);
+    for (uint32_t i = t; i < NOUT; i += T) {
+      const int32_t ri = sr[i].row;
+      const Row& r = rows[ri];
+      uint32_t lo;
+      uint32_t nn = new_range(ri, lo);
+      uint32_t no = r.src_change ? 0 : r.ps_cnt;
+      uint32_t a = 0, b2 = 0, w = succ_cnt[i];
+      while (a < no || b2 < nn) {
+        bool take_old;
+        if (a >= no) take_old = false;
+        else if (b2 >= nn) take_old = true;
+        else {
+          const Ent& eo = ents[r.ps_off + a];
+          const NewEnt& en = ne[lo + b2];
+          // insertion point: first existing succ that is not smaller (new.js:1178-1182)
+          take_old = eo.ctr < en.ctr || (eo.ctr == en.ctr && (eo.actor >= 0 && (int32_t)actors[eo.actor].rank < en.rank));
+        }
+        Ent o;
+        if (take_old) { o = ents[r.ps_off + a]; a++; }
+        else { o.ctr = ne[lo + b2].ctr; o.actor = ne[lo + b2].actor; b2++; }
+        o.row = ri;
+        outent[w++] = o;
+      }
+    }
+    if (t == 0) { s.nout = NOUT; s.nnew = NSUCC; }
+    __syncthreads();
+#if defined(AM_STOP_PHASE) && AM_STOP_PHASE == 5
+    goto done;
+#endif
+
+    PH(10);
+    // P6: canonical re-encode, one column at a time (DOC_OPS_COLUMNS then DOCUMENT_COLUMNS)
+    const ChgRow* chg = hp<ChgRow>(s, L.chg);
+    const int64_t* depsv = hp<int64_t>(s, L.deps);
+    const uint32_t NC = s.nchg;
+    EncCtx ex;
+    ex.V = hp<int64_t>(s, L.enc);
+    ex.W = ex.V + L.enc_n;
+    ex.S = reinterpret_cast<uint32_t*>(ex.W + L.enc_n);
+    ex.RS = ex.S + L.enc_n;
+    ex.RB = ex.RS + L.enc_n;
+    ex.RG = ex.RB + L.enc_n;
+    ex.As = A + s.b.span_lo;
+    const uint64_t lo = s.b.span_lo;
+    auto pk = [lo](uint64_t off, uint32_t len) -> int64_t { return (int64_t)((off - lo) << 32) | (int64_t)len; };
+    auto act = [](int32_t a) -> int64_t { return a < 0 ? AM_NULL64 : (int64_t)a; };
+    for (int c = 0; c < OC_NCOLS + DC_NCOLS; c++) {
+      const uint32_t n = c < OC_GRP_ACTOR ? NOUT : c < OC_NCOLS ? NSUCC : c == OC_NCOLS + DC_DEPS_INDEX ? s.ndeps : NC;
+      for (uint32_t i = t; i < n; i += T) {
+        int64_t v = 0;
+        if (c < OC_GRP_NUM) {
+          const Row& r = rows[sr[i].row];
+          switch (c) {
+            case OC_OBJ_ACTOR: v = act(r.obj_actor); break;
+            case OC_OBJ_CTR: v = r.obj_ctr; break;
+            case OC_KEY_ACTOR: v = act(r.key_actor); break;
+            case OC_KEY_CTR: v = r.key_ctr; break;
+            case OC_KEY_STR: v = r.key_len == AM_NOSTR ? AM_NULL64 : pk(r.key_off, r.key_len); break;
+            case OC_ID_ACTOR: v = act(r.id_actor); break;
+            case OC_ID_CTR: v = r.id_ctr; break;
+            case OC_INSERT: v = r.insert; break;
+            case OC_ACTION: v = r.action; break;
+            case OC_VAL_LEN: v = r.val_len; break;
+            case OC_VAL_RAW: v = pk(r.val_off, r.val_len == AM_NULL64 ? 0u : (uint32_t)((uint64_t)r.val_len >> 4)); break;
+            case OC_CHLD_ACTOR: v = act(r.chld_actor); break;
+            default: v = r.chld_ctr; break;
+          }
+        } else if (c == OC_GRP_NUM) {
+          v = (int64_t)(i + 1 < NOUT ? succ_cnt[i + 1] : NSUCC) - succ_cnt[i];
+        } else if (c == OC_GRP_ACTOR) {
+          v = act(outent[i].actor);
+        } else if (c == OC_GRP_CTR) {
+          v = outent[i].ctr;
+        } else {
+          const ChgRow& g = chg[i < NC ? i : 0];
+          switch (c - OC_NCOLS) {
+            case DC_ACTOR: v = g.actor; break;
+            case DC_SEQ: v = g.seq; break;
+            case DC_MAXOP: v = g.max_op; break;
+            case DC_TIME: v = g.time; break;
+            case DC_MESSAGE: v = g.msg_len == AM_NOSTR ? AM_NULL64 : pk(g.msg_off, g.msg_len); break;
+            case DC_DEPS_NUM: v = (int64_t)g.ndeps; break;
+            case DC_DEPS_INDEX: v = depsv[i]; break;
+            case DC_EXTRA_LEN: v = g.extra_len; break;
+            default: v = pk(g.extra_off, g.extra_raw_len); break;
+          }
+        }
+        ex.V[i] = v;
+      }
+      __syncthreads();
+      const uint32_t len = encode_column(kEncKind[c], n, wsg + L.colbuf[c], ex, nullptr);
+      if (t == 0) s.col_len[c] = len;
+    }
+    __syncthreads();
+    PH(11);
+    // header + body assembly (encodeDocumentHeader, columnar.js:983-1004)
+    uint8_t* out = wsg + L.out;
+    const uint8_t* heads = hp<uint8_t>(s, L.heads);
+    const int64_t* hidx = hp<int64_t>(s, L.hidx);
+    if (t == 0) {
+      uint64_t body = uleb_len(s.nactors);
+      for (uint32_t i = 0; i < s.nactors; i++) body += uleb_len(actors[i].len) + actors[i].len;
+      body += uleb_len(s.nheads) + 32ull * s.nheads;
+      uint32_t nce = 0, noe = 0;
+      for (int c = 0; c < DC_NCOLS; c++) if (s.col_len[16 + c]) { nce++; body += uleb_len(kDocChgColIds[c]) + uleb_len(s.col_len[16 + c]) + s.col_len[16 + c]; }
+      for (int c = 0; c < OC_NCOLS; c++) if (s.col_len[c]) { noe++; body += uleb_len(kDocOpColIds[c]) + uleb_len(s.col_len[c]) + s.col_len[c]; }
+      body += uleb_len(nce) + uleb_len(noe);
+      // headsIndexes only when every head index is known (loaded documents may lack them)
+      bool write_hidx = true;
+      for (uint32_t i = 0; i < s.nheads; i++) if (hidx[i] < 0) write_hidx = false;
+      if (write_hidx)
+        for (uint32_t i = 0; i < s.nheads; i++) body += uleb_len((uint64_t)hidx[i]);
+      const uint32_t extra_len = s.has_base ? s.dh.extra_len : 0;
+      body += extra_len;
+      if (9 + 10 + body > L.out_cap) {
+        set_err(s, AM_U_CAPACITY);
+      } else {
+        uint8_t* o = out;
+        for (int k = 0; k < 4; k++) *o++ = kMagic[k];
+        for (int k = 0; k < 4; k++) *o++ = 0;  // checksum, filled by k_out_hash_ws
+        *o++ = 0;  // CHUNK_TYPE_DOCUMENT
+        o = put_uleb(o, body);
+        o = put_uleb(o, s.nactors);
+        for (uint32_t i = 0; i < s.nactors; i++) {
+          o = put_uleb(o, actors[i].len);
+          for (uint32_t q = 0; q < actors[i].len; q++) *o++ = A[actors[i].off + q];
+        }
+        o = put_uleb(o, s.nheads);
+        for (uint32_t i = 0; i < 32 * s.nheads; i++) *o++ = heads[i];
+        o = put_uleb(o, nce);
+        for (int c = 0; c < DC_NCOLS; c++) if (s.col_len[16 + c]) { o = put_uleb(o, kDocChgColIds[c]); o = put_uleb(o, s.col_len[16 + c]); }
+        o = put_uleb(o, noe);
+        for (int c = 0; c < OC_NCOLS; c++) if (s.col_len[c]) { o = put_uleb(o, kDocOpColIds[c]); o = put_uleb(o, s.col_len[c]); }
+        uint64_t pos = (uint64_t)(o - out);
+        // column data positions, in DOCUMENT_COLUMNS then DOC_OPS_COLUMNS order
+        for (int c = 0; c < DC_NCOLS; c++) { s.col_pos[16 + c] = (uint32_t)pos; pos += s.col_len[16 + c]; }
+        for (int c = 0; c < OC_NCOLS; c++) { s.col_pos[c] = (uint32_t)pos; pos += s.col_len[c]; }
+        o = out + pos;
+        if (write_hidx)
+          for (uint32_t i = 0; i < s.nheads; i++) o = put_uleb(o, (uint64_t)hidx[i]);
+        for (uint32_t q = 0; q < extra_len; q++) *o++ = A[s.dh.base + s.dh.extra_off + q];
+        s.out_len = (uint64_t)(o - out);
+      }
+    }
+    __syncthreads();
+    if (s.status) goto done;
+    for (int c = 0; c < OC_NCOLS + DC_NCOLS; c++) {
+      const uint8_t* src = wsg + L.colbuf[c];
+      uint8_t* dst = out + s.col_pos[c];
+      for (uint32_t q = t; q < s.col_len[c]; q += T) dst[q] = src[q];
+    }
+    // heads for the host (hot region may be LDS): mirror into the global workspace
+    if (kHotLds)
+      for (uint32_t q = t; q < 32 * s.nheads; q += T) wsg[L.heads + q] = heads[q];
+  }
+    PH(12);
+done:
+  __syncthreads();
+  if (t == 0) {
+    am_doc_result r;
+    r.status = s.status;
+    r.err_change = s.errchg;
+    r.arg0 = s.arg0;
+    r.arg1 = s.arg1;
+    r.arg_actor_off = s.arg_actor_off;
+    r.arg_actor_len = s.arg_actor_len;
+    r.napplied = s.napplied;
+    r.nqueued = s.nqueued;
+    r.nheads = s.nheads;
+    r.nops = s.nout;
+    r.nchanges = s.nchg;
+    r.max_op = s.max_op;
+    r.out_off = 0;
+    r.out_len = s.status ? 0 : s.out_len;
+    r.ws_off = ws_off[doc];
+    r.ws_bytes = s.L.total;
+    results[doc] = r;
+  }
+}
+

@@ -18,6 +18,7 @@ struct BatchDev {
   uint64_t* ws_total;      // 1 value
   uint64_t* max_hot;       // 1 value: largest hot working set of the batch
   uint32_t lds_bytes;      // dynamic LDS per document workgroup
+  uint64_t max_hot_host;   // host copy of *max_hot
   uint8_t* ws;
   uint64_t ws_cap;
   am_doc_result* results;

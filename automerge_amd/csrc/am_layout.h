@@ -37,12 +37,18 @@ struct DocBounds {
 };
 
 struct WsLayout {
-  // hot (offsets relative to the hot base)
-  uint64_t rows, ents, idk, elemk, sortrec, newent, elem_of, parent, first_child, next_sib, tour_nxt, tour_w, scan,
-      succ_cnt, outent, chg, deps, actors, clock, heads, hidx, chghdr, order, rowbase, entbase, ambase, amap, queue,
-      enq, applied, amb_out, hashes, dup_of, self_idx, aut, can, dbase, dref, dref_idx, docpos, head_ref, input, hot_total;
+  // hot (offsets relative to the hot base). Regions after `u0` form a union: the decode cells
+  // (dead once rows are built), the merge arrays (idk .. tour_w) and the encode scratch (used
+  // after the merge) share the same bytes.
+  uint64_t rows, ents, sortrec, scan, succ_cnt, outent, chg, deps, actors, clock, heads, hidx, chghdr, order, rowbase,
+      entbase, ambase, amap, queue, enq, applied, amb_out, hashes, dup_of, self_idx, aut, can, dbase, dref, dref_idx,
+      docpos, head_ref, input;
+  uint64_t u0, idk, elemk, newent, elem_of, parent, first_child, next_sib, tour_nxt, tour_w;
+  uint64_t cells;             // decode: (13 R + 2 E) int64 values
+  uint64_t enc, enc_n;        // encode: V, W (int64) and S, RS, RB, RG (u32), enc_n entries each
+  uint64_t hot_total;
   // cold (offsets relative to the document's global workspace, after the hot mirror)
-  uint64_t scratch, scratch_stride, out, out_cap, total;
+  uint64_t out, out_cap, total;
   uint64_t colbuf[OC_NCOLS + DC_NCOLS];
 };
 
@@ -71,16 +77,7 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   const uint64_t PR = am_pow2(b.R ? b.R : 1), PE = am_pow2(b.E ? b.E : 1);
   L.rows = take(R * AM_SZ_ROW);
   L.ents = take(E * AM_SZ_ENT);
-  L.idk = take(PR * AM_SZ_IDKEY);
-  L.elemk = take(PR * AM_SZ_ELEMKEY);
   L.sortrec = take(PR * AM_SZ_SORTREC);
-  L.newent = take(PE * AM_SZ_NEWENT);
-  L.elem_of = take(R * 4);
-  L.parent = take(R * 4);
-  L.first_child = take(R * 4);
-  L.next_sib = take(R * 4);
-  L.tour_nxt = take(4 * R * 4);
-  L.tour_w = take(4 * R * 4);
   L.scan = take(R * 4);
   L.succ_cnt = take(R * 4);
   L.outent = take(E * AM_SZ_ENT);
@@ -111,13 +108,32 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   L.docpos = take((uint64_t)(b.A + N) * 4);
   L.head_ref = take((uint64_t)b.H * 4);
   L.input = take(b.span_hi - b.span_lo);
+  // union region
+  L.u0 = o;
+  L.idk = take(PR * AM_SZ_IDKEY);
+  L.elemk = take(PR * AM_SZ_ELEMKEY);
+  L.newent = take(PE * AM_SZ_NEWENT);
+  L.elem_of = take(R * 4);
+  L.parent = take(R * 4);
+  L.first_child = take(R * 4);
+  L.next_sib = take(R * 4);
+  L.tour_nxt = take(4 * R * 4);
+  L.tour_w = take(4 * R * 4);
+  uint64_t uend = o;
+  L.cells = L.u0;
+  const uint64_t cells_end = L.u0 + (((13 * R + 2 * E) * 8 + 15) & ~(uint64_t)15);
+  if (cells_end > uend) uend = cells_end;
+  uint64_t nm = R;
+  if (E > nm) nm = E;
+  if (C > nm) nm = C;
+  if (D > nm) nm = D;
+  nm = (nm + 3) & ~(uint64_t)3;
+  L.enc = L.u0;
+  L.enc_n = nm;
+  const uint64_t enc_end = L.u0 + 32 * nm;
+  if (enc_end > uend) uend = enc_end;
+  o = uend;
   L.hot_total = o;
-  uint64_t stride = R;
-  if (E > stride) stride = E;
-  if (C > stride) stride = C;
-  if (D > stride) stride = D;
-  L.scratch_stride = stride;
-  L.scratch = take(8 * stride * 8);
   // column buffers: a value costs at most 8 LEB bytes plus 2 bytes of RLE headers
   uint64_t cap = 0;
   for (int c = 0; c < OC_NCOLS + DC_NCOLS; c++) {

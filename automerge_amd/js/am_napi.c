@@ -1,0 +1,348 @@
+// am_napi.c -- Node N-API addon over the C ABI of libautomerge_amd.so (include/automerge_amd.h).
+//
+// This is the binding a reference maintainer adds to load the MI355X engine through
+// Automerge.setDefaultBackend() (src/automerge.js:147-149): backend.js in this directory wraps
+// these functions into the Backend module surface of backend/backend.js:8-197.
+// Document handles are N-API externals; errors become JS exceptions of the reference's class
+// (RangeError / TypeError) and message.
+#include <node_api.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/automerge_amd.h"
+
+typedef struct { am_doc* doc; } DocBox;
+
+static am_engine* g_engine = NULL;
+
+#define NAPI_OK(call)                                                         \
+  do {                                                                        \
+    if ((call) != napi_ok) {                                                  \
+      napi_throw_error(env, NULL, "automerge_amd: N-API call failed: " #call); \
+      return NULL;                                                            \
+    }                                                                         \
+  } while (0)
+
+static napi_value throw_am(napi_env env, const am_error* e) {
+  if (e->is_type_error) napi_throw_type_error(env, NULL, e->message);
+  else napi_throw_range_error(env, NULL, e->message);
+  return NULL;
+}
+
+static am_engine* engine(napi_env env) {
+  if (!g_engine) {
+    am_error e;
+    const char* dev = getenv("AM_DEVICE");
+    g_engine = am_engine_create(dev ? atoi(dev) : 0, &e);
+    if (!g_engine) throw_am(env, &e);
+  }
+  return g_engine;
+}
+
+static void box_finalize(napi_env env, void* data, void* hint) {
+  (void)env; (void)hint;
+  DocBox* b = (DocBox*)data;
+  if (b->doc) am_doc_free(b->doc);
+  free(b);
+}
+
+static napi_value wrap_doc(napi_env env, am_doc* d) {
+  DocBox* b = (DocBox*)malloc(sizeof(DocBox));
+  b->doc = d;
+  napi_value v;
+  NAPI_OK(napi_create_external(env, b, box_finalize, NULL, &v));
+  return v;
+}
+
+static DocBox* get_box(napi_env env, napi_value v) {
+  void* p = NULL;
+  if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+    napi_throw_type_error(env, NULL, "automerge_amd: not a document handle");
+    return NULL;
+  }
+  DocBox* b = (DocBox*)p;
+  if (!b->doc) {
+    napi_throw_error(env, NULL, "automerge_amd: document handle was freed");
+    return NULL;
+  }
+  return b;
+}
+
+static int get_bytes(napi_env env, napi_value v, const uint8_t** data, size_t* len) {
+  bool is_ta = false;
+  napi_is_typedarray(env, v, &is_ta);
+  if (is_ta) {
+    napi_typedarray_type t;
+    void* p;
+    napi_value ab;
+    size_t off;
+    if (napi_get_typedarray_info(env, v, &t, len, &p, &ab, &off) != napi_ok || t != napi_uint8_array) return 0;
+    *data = (const uint8_t*)p;
+    return 1;
+  }
+  bool is_buf = false;
+  napi_is_buffer(env, v, &is_buf);
+  if (is_buf) {
+    void* p;
+    if (napi_get_buffer_info(env, v, &p, len) != napi_ok) return 0;
+    *data = (const uint8_t*)p;
+    return 1;
+  }
+  return 0;
+}
+
+static napi_value new_u8(napi_env env, const uint8_t* data, size_t len) {
+  napi_value ab, ta;
+  void* p;
+  NAPI_OK(napi_create_arraybuffer(env, len, &p, &ab));
+  if (len) memcpy(p, data, len);
+  NAPI_OK(napi_create_typedarray(env, napi_uint8_array, len, ab, 0, &ta));
+  return ta;
+}
+
+static napi_value hex_list(napi_env env, const uint8_t* h32, size_t n) {
+  static const char* hx = "0123456789abcdef";
+  napi_value arr;
+  NAPI_OK(napi_create_array_with_length(env, n, &arr));
+  for (size_t i = 0; i < n; i++) {
+    char s[65];
+    for (int k = 0; k < 32; k++) { s[2 * k] = hx[h32[32 * i + k] >> 4]; s[2 * k + 1] = hx[h32[32 * i + k] & 15]; }
+    s[64] = 0;
+    napi_value str;
+    NAPI_OK(napi_create_string_utf8(env, s, 64, &str));
+    NAPI_OK(napi_set_element(env, arr, (uint32_t)i, str));
+  }
+  return arr;
+}
+
+// ---- exported functions ----
+static napi_value js_doc_init(napi_env env, napi_callback_info info) {
+  (void)info;
+  am_engine* e = engine(env);
+  if (!e) return NULL;
+  return wrap_doc(env, am_doc_init(e));
+}
+
+static napi_value js_doc_load(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  const uint8_t* data;
+  size_t len;
+  if (argc < 1 || !get_bytes(env, argv[0], &data, &len)) {
+    napi_throw_type_error(env, NULL, "Not a byte array");
+    return NULL;
+  }
+  am_engine* e = engine(env);
+  if (!e) return NULL;
+  am_error err;
+  am_doc* d = am_doc_load(e, data, len, &err);
+  if (!d) return throw_am(env, &err);
+  return wrap_doc(env, d);
+}
+
+static napi_value js_doc_clone(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  DocBox* b = get_box(env, argv[0]);
+  if (!b) return NULL;
+  return wrap_doc(env, am_doc_clone(b->doc));
+}
+
+static napi_value js_doc_free(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  void* p = NULL;
+  if (napi_get_value_external(env, argv[0], &p) == napi_ok && p) {
+    DocBox* b = (DocBox*)p;
+    if (b->doc) am_doc_free(b->doc);
+    b->doc = NULL;
+  }
+  return NULL;
+}
+
+// applyChanges(handle, [Uint8Array...]) -> undefined (throws on error; the document is unchanged then)
+static napi_value js_doc_apply(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  DocBox* b = get_box(env, argv[0]);
+  if (!b) return NULL;
+  bool is_arr = false;
+  napi_is_array(env, argv[1], &is_arr);
+  if (!is_arr) {
+    napi_throw_type_error(env, NULL, "Pass an array of changes");
+    return NULL;
+  }
+  uint32_t n = 0;
+  NAPI_OK(napi_get_array_length(env, argv[1], &n));
+  const uint8_t** bufs = (const uint8_t**)malloc(sizeof(uint8_t*) * (n ? n : 1));
+  size_t* lens = (size_t*)malloc(sizeof(size_t) * (n ? n : 1));
+  for (uint32_t i = 0; i < n; i++) {
+    napi_value el;
+    if (napi_get_element(env, argv[1], i, &el) != napi_ok || !get_bytes(env, el, &bufs[i], &lens[i])) {
+      free(bufs); free(lens);
+      napi_throw_type_error(env, NULL, "Change is not a byte array");
+      return NULL;
+    }
+  }
+  am_error err;
+  int rc = am_doc_apply_changes(b->doc, bufs, lens, n, &err);
+  free(bufs); free(lens);
+  if (rc) return throw_am(env, &err);
+  return NULL;
+}
+
+static napi_value js_doc_save(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  DocBox* b = get_box(env, argv[0]);
+  if (!b) return NULL;
+  uint8_t* out = NULL;
+  size_t len = 0;
+  am_error err;
+  if (am_doc_save(b->doc, &out, &len, &err)) return throw_am(env, &err);
+  napi_value v = new_u8(env, out, len);
+  am_free(out);
+  return v;
+}
+
+static napi_value js_doc_heads(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  DocBox* b = get_box(env, argv[0]);
+  if (!b) return NULL;
+  size_t n = am_doc_get_heads(b->doc, NULL, 0);
+  uint8_t* h = (uint8_t*)malloc(32 * (n ? n : 1));
+  am_doc_get_heads(b->doc, h, n);
+  napi_value v = hex_list(env, h, n);
+  free(h);
+  return v;
+}
+
+// changes(handle) -> [{hash, bytes}] in application order
+static napi_value js_doc_changes(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  DocBox* b = get_box(env, argv[0]);
+  if (!b) return NULL;
+  const size_t n = am_doc_num_changes(b->doc);
+  napi_value arr;
+  NAPI_OK(napi_create_array_with_length(env, n, &arr));
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t* data;
+    size_t len;
+    uint8_t h[32];
+    if (am_doc_change(b->doc, i, &data, &len, h)) {
+      napi_throw_range_error(env, NULL, "automerge_amd: change history unavailable for this document");
+      return NULL;
+    }
+    napi_value o, hv, hs, bv;
+    NAPI_OK(napi_create_object(env, &o));
+    hv = hex_list(env, h, 1);
+    NAPI_OK(napi_get_element(env, hv, 0, &hs));
+    bv = new_u8(env, data, len);
+    NAPI_OK(napi_set_named_property(env, o, "hash", hs));
+    NAPI_OK(napi_set_named_property(env, o, "bytes", bv));
+    NAPI_OK(napi_set_element(env, arr, (uint32_t)i, o));
+  }
+  return arr;
+}
+
+static napi_value js_doc_counts(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  DocBox* b = get_box(env, argv[0]);
+  if (!b) return NULL;
+  napi_value o, a, c, m;
+  NAPI_OK(napi_create_object(env, &o));
+  NAPI_OK(napi_create_double(env, (double)am_doc_pending(b->doc), &a));
+  NAPI_OK(napi_create_double(env, (double)am_doc_num_changes(b->doc), &c));
+  NAPI_OK(napi_create_double(env, (double)am_doc_max_op(b->doc), &m));
+  NAPI_OK(napi_set_named_property(env, o, "pending", a));
+  NAPI_OK(napi_set_named_property(env, o, "changes", c));
+  NAPI_OK(napi_set_named_property(env, o, "maxOp", m));
+  return o;
+}
+
+// queued(handle) -> [Uint8Array] changes waiting for missing dependencies
+static napi_value js_doc_queued(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  DocBox* b = get_box(env, argv[0]);
+  if (!b) return NULL;
+  const size_t n = am_doc_pending(b->doc);
+  napi_value arr;
+  NAPI_OK(napi_create_array_with_length(env, n, &arr));
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t* data;
+    size_t len;
+    if (am_doc_queued(b->doc, i, &data, &len)) break;
+    NAPI_OK(napi_set_element(env, arr, (uint32_t)i, new_u8(env, data, len)));
+  }
+  return arr;
+}
+
+// changeHashes([Uint8Array]) -> [hex]: SHA-256 hashes of change chunks (decodeChangeMeta hash)
+static napi_value js_change_hashes(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  uint32_t n = 0;
+  NAPI_OK(napi_get_array_length(env, argv[0], &n));
+  const uint8_t** bufs = (const uint8_t**)malloc(sizeof(uint8_t*) * (n ? n : 1));
+  size_t* lens = (size_t*)malloc(sizeof(size_t) * (n ? n : 1));
+  uint8_t* h = (uint8_t*)malloc(32 * (size_t)(n ? n : 1));
+  for (uint32_t i = 0; i < n; i++) {
+    napi_value el;
+    if (napi_get_element(env, argv[0], i, &el) != napi_ok || !get_bytes(env, el, &bufs[i], &lens[i])) {
+      free(bufs); free(lens); free(h);
+      napi_throw_type_error(env, NULL, "Change is not a byte array");
+      return NULL;
+    }
+  }
+  am_engine* e = engine(env);
+  am_error err;
+  if (!e || am_change_hashes(e, bufs, lens, n, h, &err)) {
+    free(bufs); free(lens); free(h);
+    return e ? throw_am(env, &err) : NULL;
+  }
+  napi_value v = hex_list(env, h, n);
+  free(bufs); free(lens); free(h);
+  return v;
+}
+
+static napi_value js_version(napi_env env, napi_callback_info info) {
+  (void)info;
+  napi_value v;
+  NAPI_OK(napi_create_string_utf8(env, am_version(), NAPI_AUTO_LENGTH, &v));
+  return v;
+}
+
+static napi_value init_module(napi_env env, napi_value exports) {
+  napi_property_descriptor props[] = {
+      {"docInit", 0, js_doc_init, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docLoad", 0, js_doc_load, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docClone", 0, js_doc_clone, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docFree", 0, js_doc_free, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docApplyChanges", 0, js_doc_apply, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docSave", 0, js_doc_save, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docHeads", 0, js_doc_heads, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docChanges", 0, js_doc_changes, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docCounts", 0, js_doc_counts, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docQueued", 0, js_doc_queued, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"changeHashes", 0, js_change_hashes, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"version", 0, js_version, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+  };
+  if (napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props) != napi_ok) return NULL;
+  return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init_module)

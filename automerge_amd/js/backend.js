@@ -1,0 +1,221 @@
+'use strict'
+/**
+ * backend.js -- the Automerge Backend module on the MI355X engine.
+ *
+ * Same exports, argument meaning, state handles and error behaviour as the reference's
+ * backend/backend.js:8-197 (+ util.js:1-10 frozen-state rule), so it loads through
+ *   Automerge.setDefaultBackend(require('<repo>/automerge_amd/js/backend'))
+ * (src/automerge.js:147-149). Document state lives in libautomerge_amd.so (the GPU engine) and
+ * is reached through the N-API addon am_napi.node (am_napi.c); there is no JS or CPU fallback:
+ * if the addon or the HIP device is missing, require() or the first call throws.
+ *
+ * Hash-graph queries (getChanges, getChangesAdded, getChangeByHash, getMissingDeps) are host
+ * traversals over the applied change buffers, as in new.js:1913-2020.
+ * Not on the GPU path yet: getPatch / patch diffs (SURVEY.md 8 a20/a21), applyLocalChange
+ * (8(f) row 3), and the change history of a loaded document (8(f) row 2); those throw.
+ */
+const path = require('path')
+const zlib = require('zlib')
+const native = require(process.env.AM_NAPI_PATH || path.join(__dirname, 'am_napi.node'))
+
+const FROZEN_MESSAGE =
+  'Attempting to use an outdated Automerge document that has already been updated. ' +
+  'Please use the latest document state, or call Automerge.clone() if you really ' +
+  'need to use this old document state.'
+
+function backendState(backend) {
+  if (backend.frozen) throw new Error(FROZEN_MESSAGE)
+  return backend.state
+}
+
+function init() {
+  return {state: native.docInit(), heads: []}
+}
+
+function clone(backend) {
+  return {state: native.docClone(backendState(backend)), heads: backend.heads}
+}
+
+// Only the latest handle owns the engine document; older (frozen) handles share it.
+function free(backend) {
+  if (!backend.frozen && backend.state) native.docFree(backend.state)
+  backend.state = null
+  backend.frozen = true
+}
+
+function patchFor(state, heads) {
+  const c = native.docCounts(state)
+  return {maxOp: c.maxOp, deps: heads, pendingChanges: c.pending}
+}
+
+function applyChanges(backend, changes) {
+  const state = backendState(backend)
+  native.docApplyChanges(state, changes)
+  backend.frozen = true
+  const heads = native.docHeads(state)
+  return [{state, heads}, patchFor(state, heads)]
+}
+
+function applyLocalChange(backend) {
+  backendState(backend)
+  throw new RangeError('automerge_amd: applyLocalChange is not implemented by this backend')
+}
+
+function save(backend) {
+  return native.docSave(backendState(backend))
+}
+
+function load(data) {
+  const state = native.docLoad(data)
+  return {state, heads: native.docHeads(state)}
+}
+
+function loadChanges(backend, changes) {
+  const state = backendState(backend)
+  native.docApplyChanges(state, changes)
+  backend.frozen = true
+  return {state, heads: native.docHeads(state)}
+}
+
+function getPatch(backend) {
+  backendState(backend)
+  throw new RangeError('automerge_amd: getPatch is not implemented by this backend yet')
+}
+
+function getHeads(backend) {
+  return backend.heads
+}
+
+// ---- hash graph (host side) ----
+function readUleb(buf, pos) {
+  let v = 0, mul = 1, b
+  do {
+    b = buf[pos++]
+    v += (b & 0x7f) * mul
+    mul *= 128
+  } while (b & 0x80)
+  return [v, pos]
+}
+
+function toHex(bytes) {
+  return Buffer.from(bytes.buffer, bytes.byteOffset, bytes.byteLength).toString('hex')
+}
+
+// dependency hashes of a change chunk (decodeChangeMeta, columnar.js:768-811)
+function changeDeps(bytes) {
+  const type = bytes[8]
+  let [len, pos] = readUleb(bytes, 9)
+  let body = bytes.subarray(pos, pos + len)
+  if (type === 2) body = zlib.inflateRawSync(body)
+  let [n, q] = readUleb(body, 0)
+  const deps = []
+  for (let i = 0; i < n; i++, q += 32) deps.push(toHex(body.subarray(q, q + 32)))
+  return deps
+}
+
+function hashGraph(state) {
+  const changes = native.docChanges(state)
+  const index = {}, depsOf = {}, dependents = {}
+  changes.forEach((c, i) => {
+    index[c.hash] = i
+    depsOf[c.hash] = changeDeps(c.bytes)
+    dependents[c.hash] = []
+  })
+  for (const c of changes) {
+    for (const d of depsOf[c.hash]) {
+      if (!dependents[d]) dependents[d] = []
+      dependents[d].push(c.hash)
+    }
+  }
+  return {changes, index, depsOf, dependents, heads: native.docHeads(state)}
+}
+
+// BackendDoc.getChanges (new.js:1913-1966)
+function getChanges(backend, haveDeps) {
+  if (!Array.isArray(haveDeps)) {
+    throw new TypeError('Pass an array of hashes to Backend.getChanges()')
+  }
+  const g = hashGraph(backendState(backend))
+  if (haveDeps.length === 0) return g.changes.map(c => c.bytes)
+
+  let stack = [], seen = {}, toReturn = []
+  for (const hash of haveDeps) {
+    seen[hash] = true
+    const succ = g.dependents[hash]
+    if (!succ) throw new RangeError(`hash not found: ${hash}`)
+    stack.push(...succ)
+  }
+  while (stack.length > 0) {
+    const hash = stack.pop()
+    seen[hash] = true
+    toReturn.push(hash)
+    if (!g.depsOf[hash].every(dep => seen[dep])) break
+    stack.push(...g.dependents[hash])
+  }
+  if (stack.length === 0 && g.heads.every(head => seen[head])) {
+    return toReturn.map(hash => g.changes[g.index[hash]].bytes)
+  }
+  stack = haveDeps.slice()
+  seen = {}
+  while (stack.length > 0) {
+    const hash = stack.pop()
+    if (!seen[hash]) {
+      const deps = g.depsOf[hash]
+      if (!deps) throw new RangeError(`hash not found: ${hash}`)
+      stack.push(...deps)
+      seen[hash] = true
+    }
+  }
+  return g.changes.filter(c => !seen[c.hash]).map(c => c.bytes)
+}
+
+function getAllChanges(backend) {
+  return getChanges(backend, [])
+}
+
+// BackendDoc.getChangesAdded (new.js:1971-1988)
+function getChangesAdded(backend1, backend2) {
+  const other = hashGraph(backendState(backend1))
+  const g = hashGraph(backendState(backend2))
+  let stack = g.heads.slice(), seen = {}, toReturn = []
+  while (stack.length > 0) {
+    const hash = stack.pop()
+    if (!seen[hash] && other.index[hash] === undefined) {
+      seen[hash] = true
+      toReturn.push(hash)
+      stack.push(...g.depsOf[hash])
+    }
+  }
+  return toReturn.reverse().map(hash => g.changes[g.index[hash]].bytes)
+}
+
+// BackendDoc.getChangeByHash (new.js:1990-1993)
+function getChangeByHash(backend, hash) {
+  const g = hashGraph(backendState(backend))
+  const i = g.index[hash]
+  return i === undefined ? undefined : g.changes[i].bytes
+}
+
+// BackendDoc.getMissingDeps (new.js:2005-2020)
+function getMissingDeps(backend, heads = []) {
+  const state = backendState(backend)
+  const g = hashGraph(state)
+  const queued = native.docQueued(state)
+  const qhashes = queued.length ? native.changeHashes(queued) : []
+  const allDeps = new Set(heads), inQueue = new Set()
+  queued.forEach((bytes, i) => {
+    inQueue.add(qhashes[i])
+    for (const dep of changeDeps(bytes)) allDeps.add(dep)
+  })
+  const missing = []
+  for (const hash of allDeps) {
+    if (g.index[hash] === undefined && !inQueue.has(hash)) missing.push(hash)
+  }
+  return missing.sort()
+}
+
+module.exports = {
+  init, clone, free, applyChanges, applyLocalChange, save, load, loadChanges, getPatch,
+  getHeads, getAllChanges, getChanges, getChangesAdded, getChangeByHash, getMissingDeps,
+  engineVersion: native.version
+}

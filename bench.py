@@ -49,7 +49,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--docs", type=int, default=262144, help="documents per GPU")
+    ap.add_argument("--docs", type=int, default=131072, help="documents per GPU (8 GPUs x 131072 = the 1M-doc C4 job)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", type=int, default=32, help="documents verified against the oracle (rank 0)")
     args = ap.parse_args()

@@ -6,14 +6,16 @@
  * backend/index.js:1-8). This library replaces the hot path behind it:
  *   am_doc_load            <- Backend.load             backend/backend.js:104-107, new.js:1695-1768
  *   am_doc_apply_changes   <- Backend.applyChanges     backend/backend.js:27-32,   new.js:1796-1871
- *   am_doc_load_changes    <- Backend.loadChanges      backend/backend.js:115-120
+ *   (loadChanges = am_doc_apply_changes without a patch)   backend/backend.js:115-120
  *   am_doc_save            <- Backend.save             backend/backend.js:96-98,   new.js:2025-2047
  *   am_doc_get_heads       <- Backend.getHeads         backend/backend.js:134-136
  *   am_doc_clone / _free   <- Backend.clone / free     backend/backend.js:12-19
- *   am_change_hash         <- decodeChangeMeta(.., true).hash   columnar.js:783-793
+ *   am_doc_change/_queued  <- this.changes / this.queue (getChanges & getMissingDeps, new.js:1913-2020)
+ *   am_change_hashes       <- decodeChangeMeta(.., true).hash   columnar.js:783-793
  *   am_batch_*             batched load + applyChanges over thousands of documents per launch
  *                          (no reference counterpart: the reference processes one document per call)
- * Bindings: Python ctypes (automerge_amd/_native.py) and the Node-API stub in INTEGRATION.md.
+ * Bindings: Node-API addon automerge_amd/js/am_napi.c (+ backend.js, the Backend module) and
+ * Python ctypes (automerge_amd/_native.py); see INTEGRATION.md.
  * All entry points are synchronous and return 0 on success; errors carry the reference's
  * message text (see am_error).
  */
@@ -129,7 +131,7 @@ const char *am_version(void);
 am_batch *am_batch_create(am_engine *eng);
 void am_batch_destroy(am_batch *b);
 /* Copies the input arena and descriptors to the device and sizes the per-document workspaces.
- * Chunks must be uncompressed (chunk type 0/1, no DEFLATE bit): am_inflate_* is the host stage. */
+ * Chunks must be uncompressed (chunk type 0/1, no DEFLATE bit): am_stage_change / am_stage_document are the host stage. */
 int am_batch_stage(am_batch *b, const uint8_t *arena, uint64_t arena_len, const am_chunk_desc *chunks,
                    uint32_t nchunks, const am_doc_desc *docs, uint32_t ndocs, const am_known_hash *known,
                    uint32_t nknown, am_error *err);
@@ -164,6 +166,8 @@ int64_t am_doc_max_op(const am_doc *doc);
 size_t am_doc_num_changes(const am_doc *doc);
 /* i-th applied change buffer (as given by the caller) / its hash; for getChanges-style callers. */
 int am_doc_change(const am_doc *doc, size_t i, const uint8_t **data, size_t *len, uint8_t *hash32);
+/* i-th enqueued change (this.queue, new.js:1796-1871: changes waiting for missing deps), as given */
+int am_doc_queued(const am_doc *doc, size_t i, const uint8_t **data, size_t *len);
 void am_free(void *p);
 
 /* ---- host stage for batch callers (DEFLATE, columnar.js:798-823, 1052-1067) ----

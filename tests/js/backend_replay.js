@@ -1,0 +1,54 @@
+'use strict'
+// Replays the golden scenarios (tests/golden/docs.json, produced by the reference backend) through
+// automerge_amd/js/backend.js -- the Node host over the N-API addon -- and reports mismatches of
+// save() bytes, heads, pending counts and thrown error class/message as one JSON line.
+const fs = require('fs')
+const path = require('path')
+const B = require(path.join(__dirname, '..', '..', 'automerge_amd', 'js', 'backend.js'))
+
+const hex = s => Uint8Array.from(Buffer.from(s, 'hex'))
+const toHex = u8 => Buffer.from(u8.buffer, u8.byteOffset, u8.byteLength).toString('hex')
+const docs = JSON.parse(fs.readFileSync(path.join(__dirname, '..', 'golden', 'docs.json'))).scenarios
+const bad = []
+let steps = 0
+for (const sc of docs) {
+  let st = null
+  for (let i = 0; i < sc.steps.length; i++) {
+    const step = sc.steps[i], exp = sc.results[i]
+    let res = {}
+    try {
+      if (step.op === 'load') st = B.load(hex(step.bytes))
+      else {
+        if (st === null) st = B.init()
+        const old = st
+        ;[st] = B.applyChanges(st, step.changes.map(hex))
+        try { B.save(old); bad.push([sc.name, i, 'old handle not frozen']) } catch (e) {
+          if (!/outdated Automerge document/.test(e.message)) bad.push([sc.name, i, 'frozen message', e.message])
+        }
+      }
+      res = {save: toHex(B.save(st)), heads: B.getHeads(st)}
+    } catch (e) {
+      res = {error: e.message, cls: e.constructor.name}
+    }
+    steps++
+    if (exp.error) {
+      if (res.error !== exp.error.message) bad.push([sc.name, i, 'error', res.error, exp.error.message])
+      break
+    }
+    if (res.error) { bad.push([sc.name, i, 'unexpected', res.cls, res.error]); break }
+    if (res.save !== exp.save) bad.push([sc.name, i, 'save'])
+    else if (JSON.stringify(res.heads) !== JSON.stringify(exp.heads)) bad.push([sc.name, i, 'heads'])
+  }
+}
+// hash-graph queries on a fresh document built from the first multi-change scenario
+const sc = docs.find(s => s.steps.length >= 2 && s.steps.every(x => x.op === 'apply') && !s.results.some(r => r.error))
+let graph = null
+if (sc) {
+  let st = B.init()
+  const all = []
+  for (const step of sc.steps) { all.push(...step.changes); [st] = B.applyChanges(st, step.changes.map(hex)) }
+  const got = B.getAllChanges(st).map(toHex)
+  graph = {changes: got.length, applied_equal_given: JSON.stringify(got.slice().sort()) === JSON.stringify(all.slice().sort()),
+           missing: B.getMissingDeps(st), since_heads: B.getChanges(st, B.getHeads(st)).length}
+}
+console.log(JSON.stringify({scenarios: docs.length, steps, bad: bad.slice(0, 20), nbad: bad.length, graph}))

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Per-phase k_doc cycle profile (probe build with -DAM_PHASE_CLOCK, see tools/build_probe.sh).
+
+  AM_LIB_PATH=tools/probe/libam_clock.so python tools/phase_clock.py [--docs D]
+Prints, for each k_doc phase, the average s_memtime cycles per sampled document (every 64th).
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+NAMES = ["P0 stage input", "P1 headers", "P2a lookups", "P2b plan (serial)", "P4 decode streams+ranks",
+         "P4 gather+place", "P5a-c checks+id sort", "P5d-e preds+elements", "P5f RGA", "P5g row sort",
+         "P5h succ merge", "P6 encode", "header+copy"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--docs", type=int, default=65536)
+    args = ap.parse_args()
+    from automerge_amd import _native, workload
+    from automerge_amd.batch import Batch
+    lib = _native.lib
+    f = lib.amx_phase_cycles
+    f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    arena, chunks, docs, ops = workload.c4(0, args.docs)
+    b = Batch(device=0)
+    b.stage(arena, chunks, docs)
+    b.run(); b.sync()
+    buf = (ctypes.c_ulonglong * 16)()
+    f(buf, 1)
+    b.run(); b.sync()
+    f(buf, 1)
+    sampled = (args.docs + 63) // 64
+    tot = 0
+    for i, n in enumerate(NAMES):
+        c = buf[i] / sampled
+        tot += c
+        print("%-26s %10.0f cycles/doc" % (n, c))
+    print("%-26s %10.0f cycles/doc   k_doc stage ms: %s" % ("total", tot, b.stage_times()))
+
+
+if __name__ == "__main__":
+    main()
