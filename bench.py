@@ -64,12 +64,12 @@ def main():
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
 
-    from automerge_amd import workload
+    from automerge_amd import shard, workload
     from automerge_amd.batch import Batch
 
-    D = args.docs
+    first, D = shard.shard_range(rank, world, args.docs)
     t_gen = time.perf_counter()
-    arena, chunks, docs, ops_per_rank = workload.c4(rank * D, D)
+    arena, chunks, docs, ops_per_rank = workload.c4(first, D)
     t_gen = time.perf_counter() - t_gen
     b = Batch(device=local)
     b.stage(arena, chunks, docs)  # H2D once: inputs resident in HBM before timing
@@ -104,13 +104,7 @@ def main():
     out_bytes = int(res["out_len"].sum())
     in_bytes = int(arena.nbytes)
     # per-shard digest exchanged with one RCCL all-gather (never inside the timed region)
-    digest = torch.tensor([D, ops_per_rank, nerr, out_bytes], dtype=torch.int64, device="cuda")
-    if dist is not None:
-        parts = [torch.zeros_like(digest) for _ in range(world)]
-        dist.all_gather(parts, digest)
-        tot = torch.stack(parts).sum(0).tolist()
-    else:
-        tot = digest.tolist()
+    tot, _ = shard.exchange(dist, [D, ops_per_rank, nerr, out_bytes, shard.out_digest(res)], "cuda")
     if rank != 0:
         dist.destroy_process_group() if dist is not None else None
         return

@@ -1,0 +1,74 @@
+"""N>1 path of bench.py on CPU: two ranks (gloo, 127.0.0.1) shard the C4 documents, merge their
+shard (here with the CPU checker; on the GPU box with the engine) and exchange the per-rank
+digest with one all-gather. The gathered totals must equal one process over all documents, and
+the shards must be disjoint and cover the range."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DOCS_PER_RANK = 5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _merge_shard(first, n):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    from automerge_amd import shard, workload
+    arena, chunks, docs, ops = workload.c4(first, n)
+    lens = []
+    for i in range(n):
+        base, changes = workload.doc_chunks(arena, chunks, docs, i)
+        d = O.Doc.load(base)
+        d.apply(changes)
+        lens.append(len(d.save()))
+    res = np.zeros(n, dtype=[("out_len", "<u8")])
+    res["out_len"] = lens
+    return [n, ops, 0, int(res["out_len"].sum()), shard.out_digest(res)], lens
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    from automerge_amd import shard
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    first, n = shard.shard_range(rank, world, DOCS_PER_RANK)
+    digest, lens = _merge_shard(first, n)
+    tot, rows = shard.exchange(dist, digest, "cpu")
+    np.save(os.path.join(outdir, "rank%d.npy" % rank), np.array(tot + [first, n], dtype=np.int64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_range():
+    from automerge_amd import shard
+    spans = [shard.shard_range(r, 4, 7) for r in range(4)]
+    assert spans == [(0, 7), (7, 7), (14, 7), (21, 7)]
+    with pytest.raises(ValueError):
+        shard.shard_range(4, 4, 7)
+
+
+def test_two_rank_gloo_digest_matches_single_process(tmp_path):
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    got = [np.load(os.path.join(tmp_path, "rank%d.npy" % r)).tolist() for r in range(world)]
+    assert got[0][:5] == got[1][:5]  # every rank sees the same gathered totals
+    firsts = sorted((g[5], g[6]) for g in got)
+    assert firsts == [(0, DOCS_PER_RANK), (DOCS_PER_RANK, DOCS_PER_RANK)]  # disjoint, covering
+    single, _ = _merge_shard(0, world * DOCS_PER_RANK)
+    assert got[0][:4] == single[:4]
+    assert got[0][4] == single[4]
