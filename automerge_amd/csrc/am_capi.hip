@@ -302,6 +302,10 @@ static bool set_device(am_engine* e) { return hipSetDevice(e->device) == hipSucc
 
 extern "C" const char* am_version(void) { return "automerge_amd 0.1 (gfx950)"; }
 
+// accessors for the other translation units (am_launch.h)
+hipStream_t am_engine_stream(am_engine* e) { return e->stream; }
+int am_engine_device(am_engine* e) { return e->device; }
+
 extern "C" am_engine* am_engine_create(int device, am_error* err) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) {

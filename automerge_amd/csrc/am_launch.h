@@ -32,3 +32,15 @@ void am_launch_doc(const BatchDev& b, hipStream_t s);
 void am_launch_out_hash(const BatchDev& b, hipStream_t s);
 void am_launch_sha256(const uint8_t* arena, const am_chunk_desc* msgs, uint32_t n, uint8_t* out, hipStream_t s);
 size_t am_scan_tmp_elems(uint32_t n);
+
+// engine internals shared with am_sync.hip
+struct am_engine;
+hipStream_t am_engine_stream(am_engine* e);
+int am_engine_device(am_engine* e);
+void am_launch_bloom_build(const uint8_t* d_hashes, const uint64_t* d_hoff, uint32_t nfilt, uint8_t* d_out,
+                           const uint64_t* d_foff, hipStream_t s);
+void am_launch_bloom_probe(const uint8_t* d_filters, const uint64_t* d_foff, uint32_t nfilt, const uint8_t* d_probes,
+                           const uint32_t* d_pfilt, uint64_t nprobe, uint8_t* d_contains, hipStream_t s);
+void am_launch_sync_select(uint32_t npairs, const uint64_t* d_coff, const uint8_t* d_hashes, const uint64_t* d_doff,
+                           const int32_t* d_didx, const uint64_t* d_pfoff, const uint8_t* d_filters, const uint64_t* d_foff,
+                           uint8_t* d_send, uint8_t* d_status, hipStream_t s);

@@ -185,6 +185,29 @@ int am_stage_document(am_engine *eng, const uint8_t *in, size_t len, uint8_t **o
 int am_change_hashes(am_engine *eng, const uint8_t *const *bufs, const size_t *lens, size_t n, uint8_t *out32,
                      am_error *err);
 
+/* ---- sync.js Bloom filters and change selection, batched ----
+ * am_bloom_build      <- new BloomFilter(hashes).bytes            sync.js:38-47, 66-77, 90-110
+ *   Filter f holds hashes [hoff[f], hoff[f+1]) of hashes32 (32 bytes each). The encoded filters
+ *   are written back to back into out; foff (nfilt + 1 entries) receives their offsets. A filter
+ *   with no hashes encodes to 0 bytes. am_bloom_encoded_size(n) = size of one filter of n hashes.
+ * am_bloom_probe      <- new BloomFilter(bytes).containsHash(h)   sync.js:48-59, 112-125
+ *   Probe i tests hash probes32[i] against filter pfilt[i] (filters/foff as produced above or
+ *   received from peers); contains[i] = 1 / 0. A malformed filter fails with the RangeError text
+ *   of its decode (number out of range / incomplete number / subarray exceeds buffer size).
+ * am_sync_select      <- getChangesToSend with non-empty `have`   sync.js:246-306
+ *   For pair p: changes [coff[p], coff[p+1]) (hashes32, in getChanges order), change c's deps
+ *   didx[doff[c] .. doff[c+1]) as indexes within the pair's list (-1 = not in the list), the
+ *   pair's filters [pfoff[p], pfoff[p+1]) of filters/foff. send[c] = 1 for changes absent from
+ *   every filter and their transitive dependents; the caller appends the explicit `need` hashes. */
+uint64_t am_bloom_encoded_size(uint64_t nhashes);
+int am_bloom_build(am_engine *eng, const uint8_t *hashes32, const uint64_t *hoff, uint32_t nfilt, uint8_t *out,
+                   uint64_t cap, uint64_t *foff, am_error *err);
+int am_bloom_probe(am_engine *eng, const uint8_t *filters, const uint64_t *foff, uint32_t nfilt, const uint8_t *probes32,
+                   const uint32_t *pfilt, uint64_t nprobe, uint8_t *contains, am_error *err);
+int am_sync_select(am_engine *eng, uint32_t npairs, const uint64_t *coff, const uint8_t *hashes32, const uint64_t *doff,
+                   const int32_t *didx, const uint64_t *pfoff, const uint8_t *filters, const uint64_t *foff,
+                   uint8_t *send, am_error *err);
+
 /* ---- synthetic workloads (bench.py input preparation, host side) ----
  * C4: document i = base document (change 0 saved) + 12 concurrent changes (4 actors x 3), seeded
  * by i. Returns the arena bytes needed; fills arena/chunks (13 per doc)/docs when arena != NULL

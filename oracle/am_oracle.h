@@ -70,6 +70,15 @@ size_t oc_doc_num_ops(const oc_doc *doc);
 int64_t oc_doc_max_op(const oc_doc *doc);
 void oc_free(void *p);
 
+/* ---- sync.js Bloom filter + change selection (am_sync_oracle.c) ---- */
+/* new BloomFilter(hashes).bytes: returns the encoded length (0 for no hashes); writes when cap suffices */
+size_t oc_bloom_build(const uint8_t *hashes32, size_t n, uint8_t *out, size_t cap);
+/* new BloomFilter(bytes).containsHash(hash): 1 / 0, -1 for a malformed filter */
+int oc_bloom_contains(const uint8_t *filter, size_t len, const uint8_t *hash32);
+/* getChangesToSend selection mask (see am_sync_oracle.c) */
+void oc_sync_select(size_t n, const uint8_t *hashes32, const uint32_t *dep_off, const int32_t *dep_idx,
+                    size_t nfilt, const uint8_t *const *filters, const size_t *flens, uint8_t *send);
+
 #ifdef __cplusplus
 }
 #endif

@@ -41,6 +41,11 @@ def lib():
         L.oc_doc_max_op.restype = I64
         L.oc_doc_max_op.argtypes = [P]
         L.oc_free.argtypes = [P]
+        L.oc_bloom_build.restype = S
+        L.oc_bloom_build.argtypes = [C.c_char_p, S, C.c_char_p, S]
+        L.oc_bloom_contains.restype = C.c_int
+        L.oc_bloom_contains.argtypes = [C.c_char_p, S, C.c_char_p]
+        L.oc_sync_select.argtypes = [S, C.c_char_p, P, P, S, C.POINTER(C.c_char_p), C.POINTER(S), C.c_char_p]
         _lib = L
     return _lib
 
@@ -192,3 +197,34 @@ class Doc:
 
     def max_op(self):
         return lib().oc_doc_max_op(self._p)
+
+
+# ---- sync.js Bloom filter / change selection ----
+def bloom_build(hashes):
+    """new BloomFilter(hashes).bytes for a list of 32-byte hashes."""
+    L = lib()
+    flat = b"".join(hashes)
+    n = L.oc_bloom_build(flat, len(hashes), None, 0)
+    buf = C.create_string_buffer(max(n, 1))
+    L.oc_bloom_build(flat, len(hashes), buf, n)
+    return buf.raw[:n]
+
+
+def bloom_contains(filt, h):
+    return lib().oc_bloom_contains(bytes(filt), len(filt), bytes(h))
+
+
+def sync_select(hashes, deps, filters):
+    """Send mask of getChangesToSend: hashes (32 B each), deps[i] = indexes of change i's deps in
+    the list (-1 = outside), filters = encoded Bloom filters."""
+    import numpy as np
+    n = len(hashes)
+    off = np.zeros(n + 1, dtype=np.uint32)
+    for i, d in enumerate(deps):
+        off[i + 1] = off[i] + len(d)
+    idx = np.array([x for d in deps for x in d] or [0], dtype=np.int32)
+    fl = (C.c_char_p * max(len(filters), 1))(*[bytes(f) for f in filters])
+    fn = (C.c_size_t * max(len(filters), 1))(*[len(f) for f in filters])
+    out = C.create_string_buffer(max(n, 1))
+    lib().oc_sync_select(n, b"".join(hashes), off.ctypes.data, idx.ctypes.data, len(filters), fl, fn, out)
+    return list(out.raw[:n])
