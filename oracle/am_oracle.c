@@ -1689,3 +1689,5 @@ int oc_col_decode(int type, const uint8_t *buf, size_t len, size_t maxn, size_t 
   afree_all(&c);
   return 0;
 }
+
+#include "am_patch_oracle.inc"

@@ -70,6 +70,9 @@ size_t oc_doc_num_ops(const oc_doc *doc);
 int64_t oc_doc_max_op(const oc_doc *doc);
 void oc_free(void *p);
 
+/* Backend.getPatch(doc) as JSON text (malloc'd, free with oc_free); NULL on error (message in err) */
+char *oc_doc_patch(const oc_doc *doc, char *err, size_t errcap);
+
 /* ---- sync.js Bloom filter + change selection (am_sync_oracle.c) ---- */
 /* new BloomFilter(hashes).bytes: returns the encoded length (0 for no hashes); writes when cap suffices */
 size_t oc_bloom_build(const uint8_t *hashes32, size_t n, uint8_t *out, size_t cap);

@@ -41,6 +41,8 @@ def lib():
         L.oc_doc_max_op.restype = I64
         L.oc_doc_max_op.argtypes = [P]
         L.oc_free.argtypes = [P]
+        L.oc_doc_patch.restype = C.c_void_p
+        L.oc_doc_patch.argtypes = [P, C.c_char_p, S]
         L.oc_bloom_build.restype = S
         L.oc_bloom_build.argtypes = [C.c_char_p, S, C.c_char_p, S]
         L.oc_bloom_contains.restype = C.c_int
@@ -176,6 +178,17 @@ class Doc:
         rc = lib().oc_doc_apply(self._p, arr, lens, n, err, 512)
         if rc:
             raise OracleError(err.value.decode(), rc)
+
+    def patch(self):
+        """Backend.getPatch(doc) as a dict (JSON from the C restatement)."""
+        import json
+        err = C.create_string_buffer(512)
+        p = lib().oc_doc_patch(self._p, err, 512)
+        if not p:
+            raise OracleError(err.value.decode())
+        txt = C.string_at(p).decode("utf-8")
+        lib().oc_free(p)
+        return json.loads(txt)
 
     def save(self):
         n = C.c_size_t()
