@@ -73,6 +73,24 @@ void oc_free(void *p);
 /* Backend.getPatch(doc) as JSON text (malloc'd, free with oc_free); NULL on error (message in err) */
 char *oc_doc_patch(const oc_doc *doc, char *err, size_t errcap);
 
+/* Flat export of a decoded (saved) document: ops in document order -- for host checks of the
+ * engine's patch scan. Nulls: obj/key ctr and actor -1, key_len -1, action -1, val_len 0. */
+typedef struct {
+  int64_t obj_ctr, key_ctr, id_ctr, action, val_len;
+  int32_t obj_actor, key_actor, id_actor, insert;
+  int32_t key_len;
+  uint32_t val_n, nsucc, succ_off;
+  const uint8_t *key, *val;
+} oc_op;
+typedef struct {
+  size_t nops; oc_op *ops; int64_t *succ_ctr; int32_t *succ_actor;
+  size_t nactors; const uint8_t **actors; uint32_t *actor_lens;
+  size_t nchg; int64_t *chg_actor; int64_t *chg_seq;
+  void *priv;
+} oc_export;
+oc_export *oc_doc_export(const uint8_t *buf, size_t len, char *err, size_t errcap);
+void oc_export_free(oc_export *e);
+
 /* ---- sync.js Bloom filter + change selection (am_sync_oracle.c) ---- */
 /* new BloomFilter(hashes).bytes: returns the encoded length (0 for no hashes); writes when cap suffices */
 size_t oc_bloom_build(const uint8_t *hashes32, size_t n, uint8_t *out, size_t cap);
