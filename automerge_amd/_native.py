@@ -76,6 +76,8 @@ _sigs = {
     "am_bloom_build": (C.c_int, [P, C.c_char_p, P, C.c_uint32, P, C.c_uint64, P, C.POINTER(Error)]),
     "am_bloom_probe": (C.c_int, [P, P, P, C.c_uint32, C.c_char_p, P, C.c_uint64, P, C.POINTER(Error)]),
     "am_sync_select": (C.c_int, [P, C.c_uint32, P, C.c_char_p, P, P, P, P, P, P, C.POINTER(Error)]),
+    "am_doc_get_patch": (C.c_int, [P, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
+    "am_batch_doc_patch": (C.c_int, [P, C.c_uint32, P, C.c_uint64, C.POINTER(C.c_uint64)]),
     "am_doc_queued": (C.c_int, [P, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]),
     "am_free": (None, [P]),
     "am_change_hashes": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t, P, C.POINTER(Error)]),

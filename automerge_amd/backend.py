@@ -113,6 +113,19 @@ def save(backend):
     return data
 
 
+def getPatch(backend):
+    """Backend.getPatch() (backend/backend.js:125-127, new.js:2052-2060): documentPatch runs on the
+    GPU (k_doc phase P7); automerge_amd/patch.py turns its log into the reference patch object."""
+    from . import patch as P
+    s = _backend_state(backend)
+    out, n, err = N.u8p(), C.c_size_t(), N.Error()
+    if N.lib.am_doc_get_patch(s.ptr, C.byref(out), C.byref(n), C.byref(err)):
+        N.raise_for(err)
+    blob = C.string_at(out, n.value)
+    N.lib.am_free(out)
+    return P.materialize(blob, s.heads(), N.lib.am_doc_pending(s.ptr), N.lib.am_doc_max_op(s.ptr))
+
+
 def getHeads(backend):
     """Backend.getHeads() (backend/backend.js:134-136)."""
     return backend.heads

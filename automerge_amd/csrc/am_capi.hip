@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "am_launch.h"
+#include "am_patch.h"
 
 namespace {
 
@@ -464,6 +465,36 @@ extern "C" int am_batch_doc_heads(am_batch* b, uint32_t doc, uint8_t* dst32, uin
   return hipMemcpy(dst32, b->ws.p + r.ws_off + L.heads, 32ull * k, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
 
+extern "C" int am_batch_doc_patch(am_batch* b, uint32_t doc, uint8_t* dst, uint64_t cap, uint64_t* len) {
+  if (!set_device(b->eng) || doc >= b->ndocs) return 1;
+  am_doc_result r;
+  DocBounds bd;
+  if (hipMemcpy(&r, b->results.p + doc, sizeof r, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  if (hipMemcpy(&bd, b->bounds.p + doc, sizeof bd, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  if (r.status) return 3;  // the document failed: there is no patch
+  if (!bd.P) return 4;     // not staged with AM_DOC_WANT_PATCH
+  const WsLayout L = ws_layout(bd);
+  const uint8_t* base = b->ws.p + r.ws_off + L.patch;
+  PatchHdr h;
+  if (hipMemcpy(&h, base, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  if (h.nrec > L.patch_nrec || h.nmval > L.patch_nmval || h.nheap > L.patch_heap) return 1;
+  const uint64_t total = sizeof h + sizeof(PatchRec) * h.nrec + sizeof(PatchVal) * h.nmval + h.nheap;
+  *len = total;
+  if (cap == 0) return 0;
+  if (cap < total) return 2;
+  std::memcpy(dst, &h, sizeof h);
+  uint8_t* o = dst + sizeof h;
+  const uint8_t* rec = base + sizeof h;
+  const uint8_t* mval = rec + sizeof(PatchRec) * L.patch_nrec;
+  const uint8_t* heap = mval + sizeof(PatchVal) * L.patch_nmval;
+  if (h.nrec && hipMemcpy(o, rec, sizeof(PatchRec) * h.nrec, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  o += sizeof(PatchRec) * h.nrec;
+  if (h.nmval && hipMemcpy(o, mval, sizeof(PatchVal) * h.nmval, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  o += sizeof(PatchVal) * h.nmval;
+  if (h.nheap && hipMemcpy(o, heap, h.nheap, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  return 0;
+}
+
 extern "C" int am_batch_stage_times(am_batch* b, float* ms4) {
   if (!b->timed) return 1;
   for (int i = 0; i < 4; i++) {
@@ -529,11 +560,13 @@ struct OneResult {
   std::vector<int32_t> chg_state;
   std::vector<std::array<uint8_t, 32>> hashes;
   std::vector<std::array<uint8_t, 32>> heads;
+  std::vector<uint8_t> patch;  // getPatch log (want_patch)
 };
 
 // Runs one document (optional base chunk + change list) through the GPU pipeline.
 bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified, const std::vector<std::vector<uint8_t>>& chg,
-             const std::vector<am_known_hash>& known, bool have_graph, OneResult& res, std::vector<uint8_t>& arena, Err& err) {
+             const std::vector<am_known_hash>& known, bool have_graph, OneResult& res, std::vector<uint8_t>& arena, Err& err,
+             bool want_patch = false) {
   arena.clear();
   std::vector<am_chunk_desc> cds;
   am_doc_desc dd{};
@@ -551,7 +584,7 @@ bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified,
   }
   dd.known_begin = 0;
   dd.known_count = (uint32_t)known.size();
-  dd.flags = have_graph ? 1 : 0;
+  dd.flags = (have_graph ? 1u : 0u) | (want_patch ? AM_DOC_WANT_PATCH : 0u);
   am_batch* b = scratch_batch(e);
   am_error ce;
   if (am_batch_stage(b, arena.data(), arena.size(), cds.data(), (uint32_t)cds.size(), &dd, 1, known.data(),
@@ -587,6 +620,18 @@ bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified,
   am_batch_doc_heads(b, 0, hb.data(), res.r.nheads, &nh);
   res.heads.resize(nh);
   for (uint32_t i = 0; i < nh; i++) std::memcpy(res.heads[i].data(), hb.data() + 32 * i, 32);
+  if (want_patch) {
+    uint64_t plen = 0;
+    if (am_batch_doc_patch(b, 0, nullptr, 0, &plen)) {
+      err = {AM_U_CAPACITY, false, "automerge_amd: patch copy failed"};
+      return false;
+    }
+    res.patch.resize(plen);
+    if (am_batch_doc_patch(b, 0, res.patch.data(), plen, &plen)) {
+      err = {AM_U_CAPACITY, false, "automerge_amd: patch copy failed"};
+      return false;
+    }
+  }
   return true;
 }
 
@@ -803,6 +848,52 @@ extern "C" int am_doc_change(const am_doc* d, size_t i, const uint8_t** data, si
   *data = d->changes[i].data();
   *len = d->changes[i].size();
   if (hash32) std::memcpy(hash32, d->hashes[i].data(), 32);
+  return 0;
+}
+
+extern "C" int am_doc_get_patch(am_doc* d, uint8_t** out, size_t* len, am_error* err) {
+  if (err) err->code = 0;
+  std::vector<uint8_t> log;
+  if (d->state.empty()) {  // Backend.init(): documentPatch of an empty document
+    PatchHdr h{};
+    log.resize(sizeof h);
+    std::memcpy(log.data(), &h, sizeof h);
+  } else {
+    OneResult res;
+    std::vector<uint8_t> arena;
+    Err e;
+    if (!run_one(d->eng, &d->state, false, {}, {}, d->have_hash_graph, res, arena, e, true)) { to_c(e, err); return 1; }
+    log.swap(res.patch);
+  }
+  PatchHdr h;
+  std::memcpy(&h, log.data(), sizeof h);
+  if (h.status) {  // the RangeError getPatch throws (new.js:944, columnar.js:318)
+    Err e{h.status, false, ""};
+    if (h.status == AM_E_FLOAT_LEN) {
+      e.msg = fmt("Invalid length for floating point number: %lld", (long long)h.arg0);
+    } else if (h.status == AM_E_UNKNOWN_COUNTER) {
+      std::string actor = "?";
+      const PatchRec* recs = reinterpret_cast<const PatchRec*>(log.data() + sizeof h);
+      for (uint64_t i = 0; i < h.nrec && recs[i].tag == PR_ACTOR; i++)
+        if ((int64_t)recs[i].a1 == h.arg1) {
+          const uint8_t* heap = log.data() + sizeof h + sizeof(PatchRec) * h.nrec + sizeof(PatchVal) * h.nmval;
+          actor = hexs(heap + recs[i].v0, (size_t)recs[i].v1);
+        }
+      e.msg = fmt("increment operation %lld@%s for unknown counter", (long long)h.arg0, actor.c_str());
+    } else {
+      e.msg = fmt("automerge_amd: getPatch is not supported for this document (code %u)", h.status);
+    }
+    to_c(e, err);
+    return 1;
+  }
+  *out = static_cast<uint8_t*>(std::malloc(log.size()));
+  if (!*out) {
+    Err e{AM_U_CAPACITY, false, "automerge_amd: out of host memory"};
+    to_c(e, err);
+    return 1;
+  }
+  std::memcpy(*out, log.data(), log.size());
+  *len = log.size();
   return 0;
 }
 

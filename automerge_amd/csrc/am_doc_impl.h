@@ -729,6 +729,72 @@ __device__ static int32_t id_lookup(const IdKey* idk, uint32_t n, int64_t ctr, i
 }
 
 
+// ---- P7: getPatch log (am_patch.h) over the merged rows in document order ----
+struct RowSrc {
+  const Row* rows;
+  const SortRec* sr;
+  const uint32_t* soff;  // exclusive scan of succ counts (document order)
+  const Ent* ent;        // succ entries
+  uint32_t nout, nsucc_total;
+  const ActorRef* actors;
+  uint32_t na;
+  const ChgRow* chg;
+  uint32_t nc;
+  APtr A;
+  __device__ const Row& r(uint32_t i) const { return rows[sr[i].row]; }
+  __device__ uint32_t n() const { return nout; }
+  __device__ int64_t obj_ctr(uint32_t i) const { const int64_t v = r(i).obj_ctr; return v == AM_NULL64 ? -1 : v; }
+  __device__ int32_t obj_actor(uint32_t i) const { return r(i).obj_actor; }
+  __device__ bool has_key(uint32_t i) const { return r(i).key_len != AM_NOSTR; }
+  __device__ uint32_t key_len(uint32_t i) const { return r(i).key_len; }
+  __device__ bool key_eq(uint32_t i, uint32_t j) const {
+    const Row& a = r(i);
+    const Row& b = r(j);
+    return a.key_len == b.key_len && bytes_eq(A + a.key_off, A + b.key_off, a.key_len);
+  }
+  __device__ void copy_key(uint32_t i, uint8_t* d) const {
+    const Row& a = r(i);
+    const uint8_t* p = A + a.key_off;
+    for (uint32_t q = 0; q < a.key_len; q++) d[q] = p[q];
+  }
+  __device__ int64_t key_ctr(uint32_t i) const { const int64_t v = r(i).key_ctr; return v == AM_NULL64 ? -1 : v; }
+  __device__ int32_t key_actor(uint32_t i) const { return r(i).key_actor; }
+  __device__ int64_t id_ctr(uint32_t i) const { return r(i).id_ctr; }
+  __device__ int32_t id_actor(uint32_t i) const { return r(i).id_actor; }
+  __device__ bool insert(uint32_t i) const { return r(i).insert != 0; }
+  __device__ int64_t action(uint32_t i) const { const int64_t v = r(i).action; return v == AM_NULL64 ? -1 : v; }
+  __device__ int64_t val_len(uint32_t i) const { const int64_t v = r(i).val_len; return v == AM_NULL64 ? 0 : v; }
+  __device__ uint32_t vbytes(uint32_t i) const { return (uint32_t)((uint64_t)val_len(i) >> 4); }
+  __device__ void copy_value(uint32_t i, uint8_t* d) const {
+    const uint8_t* p = A + r(i).val_off;
+    const uint32_t nb = vbytes(i);
+    for (uint32_t q = 0; q < nb; q++) d[q] = p[q];
+  }
+  // new Decoder(bytes).readUint53() / readInt53() (columnar.js:316-325)
+  __device__ bool value_int(uint32_t i, bool is_uint, int64_t& out) const {
+    Rd rd{A + r(i).val_off, vbytes(i), 0};
+    return (is_uint ? rd_u53(rd, out) : rd_i53(rd, out)) == AM_OK;
+  }
+  __device__ int64_t value_f64_bits(uint32_t i) const {
+    const uint8_t* p = A + r(i).val_off;
+    uint64_t b = 0;
+    for (int q = 7; q >= 0; q--) b = (b << 8) | p[q];
+    return (int64_t)b;
+  }
+  __device__ uint32_t nsucc(uint32_t i) const { return (i + 1 < nout ? soff[i + 1] : nsucc_total) - soff[i]; }
+  __device__ int64_t succ_ctr(uint32_t i, uint32_t k) const { return ent[soff[i] + k].ctr; }
+  __device__ int32_t succ_actor(uint32_t i, uint32_t k) const { return ent[soff[i] + k].actor; }
+  __device__ uint32_t nactors() const { return na; }
+  __device__ uint32_t actor_len(uint32_t a) const { return actors[a].len; }
+  __device__ void copy_actor(uint32_t a, uint8_t* d) const {
+    const uint8_t* p = A + actors[a].off;
+    for (uint32_t q = 0; q < actors[a].len; q++) d[q] = p[q];
+  }
+  __device__ uint32_t nchg() const { return nc; }
+  __device__ int64_t chg_actor(uint32_t c) const { return chg[c].actor; }
+  __device__ int64_t chg_seq(uint32_t c) const { return chg[c].seq; }
+};
+
 __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
                                                const am_doc_desc* __restrict__ docs, const am_known_hash* __restrict__ known,
                                                const ChunkInfo* __restrict__ info, const DocBounds* __restrict__ bounds,
@@ -744,7 +810,7 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
     s.ws = ws_base + ws_off[doc];
     s.L = ws_layout(s.b);
     // hot working set in LDS when it fits (this namespace's mode decides who runs the document)
-    s.hot = kHotLds ? am_lds : s.ws;
+    s.hot = s.ws;  // global mode only; LDS mode addresses am_lds directly (hp)
     s.A = arena;
     s.status = AM_OK; s.errchg = 0xffffffffu; s.arg0 = s.arg1 = 0; s.arg_actor_off = 0; s.arg_actor_len = 0;
     s.has_base = dd.base_chunk >= 0;
@@ -770,7 +836,9 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
     if (s.b.R == 0 && s.b.N == 0 && !s.has_base && dd.chg_count) set_err(s, AM_U_CAPACITY);
   }
   __syncthreads();
-  if ((s.L.hot_total <= lds_bytes) != kHotLds) return;  // the other mode's document
+  // LDS mode: the hot set fits and the input span is contiguous (chunks of a scattered document
+  // are read from the arena by the global mode; k_max_hot forces that launch)
+  if ((s.L.hot_total <= lds_bytes && !doc_scattered(s.b)) != kHotLds) return;  // the other mode's document
   const WsLayout& L = s.L;
   if (s.status) goto done;
   // P0: stage the document's input bytes (base + changes, adjacent in the arena) into the hot
@@ -1299,6 +1367,38 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
       const uint8_t* src = wsg + L.colbuf[c];
       uint8_t* dst = out + s.col_pos[c];
       for (uint32_t q = t; q < s.col_len[c]; q += T) dst[q] = src[q];
+    }
+    // P7: getPatch log (lane 0; the merge arrays of the union region are dead, reuse them)
+    if (s.b.P && t == 0) {
+      const uint64_t R1 = (uint64_t)s.b.R + 1, E1 = (uint64_t)s.b.E + 1;
+      uint8_t* ps = hp<uint8_t>(s, L.pscr);
+      PatchScratch w;
+      w.mk_ctr = reinterpret_cast<int64_t*>(ps);
+      w.cs_ctr = w.mk_ctr + R1;
+      w.cs_val = w.cs_ctr + R1;
+      w.cm_ctr = w.cs_val + R1;
+      w.mk_actor = reinterpret_cast<int32_t*>(w.cm_ctr + E1);
+      w.cs_actor = w.mk_actor + R1;
+      w.cs_left = w.cs_actor + R1;
+      w.cm_actor = w.cs_left + R1;
+      w.cm_state = w.cm_actor + E1;
+      w.mk_vis = reinterpret_cast<uint8_t*>(w.cm_state + E1);
+      w.mk_cap = (uint32_t)R1; w.cs_cap = (uint32_t)R1; w.cm_cap = (uint32_t)E1;
+      uint8_t* pbase = wsg + L.patch;
+      PatchOut po;
+      po.rec = reinterpret_cast<PatchRec*>(pbase + 64);
+      po.mval = reinterpret_cast<PatchVal*>(pbase + 64 + 64 * L.patch_nrec);
+      po.heap = pbase + 64 + 64 * L.patch_nrec + 32 * L.patch_nmval;
+      po.cap_rec = L.patch_nrec; po.cap_mval = L.patch_nmval; po.cap_heap = L.patch_heap;
+      po.arg0 = po.arg1 = 0;
+      RowSrc src{rows, sr, succ_cnt, outent, NOUT, NSUCC, actors, s.nactors, chg, NC, A};
+      int64_t pmax = 0;
+      patch_scan(src, po, w, pmax);
+      PatchHdr* ph = reinterpret_cast<PatchHdr*>(pbase);
+      ph->status = po.status; ph->pad0 = 0;
+      ph->arg0 = po.arg0; ph->arg1 = po.arg1;
+      ph->nrec = po.nrec; ph->nmval = po.nmval; ph->nheap = po.nheap;
+      ph->max_op = pmax; ph->pad1 = 0;
     }
     // heads for the host (hot region may be LDS): mirror into the global workspace
     if (kHotLds)

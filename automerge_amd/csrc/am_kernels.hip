@@ -263,6 +263,8 @@ __global__ void __launch_bounds__(256) k_bounds(const am_doc_desc* __restrict__ 
   b.R = (uint32_t)R; b.E = (uint32_t)E; b.C = (uint32_t)C; b.D = (uint32_t)D; b.A = (uint32_t)A;
   b.H = (uint32_t)H; b.N = dd.chg_count; b.K = (uint32_t)(H + dd.known_count); b.AM = (uint32_t)AM;
   b.ND = (uint32_t)ND; b.S = S; b.B = B; b.span_lo = lo; b.span_hi = hi;
+  b.P = (dd.flags & AM_DOC_WANT_PATCH) ? 1u : 0u;
+  b.pad = 0;
   WsLayout L = ws_layout(b);
   bounds[d] = b;
   ws_bytes[d] = L.total;
@@ -393,6 +395,12 @@ __device__ __forceinline__ int hash_cmp(const uint8_t* a, const uint8_t* b) {
 }
 
 // index of a base head in changeIndexByHash (new.js:1729-1739)
+#include "am_patch.h"
+
+// a document whose chunks are not adjacent in the arena has no input span (k_bounds): it runs in
+// the global mode, reading the arena directly
+__host__ __device__ inline bool doc_scattered(const DocBounds& b) { return b.span_hi == b.span_lo && b.B > 0; }
+
 extern __shared__ __attribute__((aligned(16))) uint8_t am_lds[];
 
 namespace lds_mode {
@@ -450,6 +458,9 @@ __global__ void __launch_bounds__(256) k_sha256(const uint8_t* __restrict__ aren
 #include "am_launch.h"
 
 static_assert(sizeof(Row) == AM_SZ_ROW, "Row");
+static_assert(sizeof(PatchRec) == 64 && sizeof(PatchVal) == 32 && sizeof(PatchHdr) == 64, "patch log layout");
+static_assert(PATCH_E_FLOAT_LEN == AM_E_FLOAT_LEN && PATCH_E_UNKNOWN_COUNTER == AM_E_UNKNOWN_COUNTER &&
+              PATCH_U_CAPACITY == AM_U_CAPACITY && PATCH_U_VALUE == AM_U_VALUE, "patch status codes");
 static_assert(sizeof(Ent) == AM_SZ_ENT, "Ent");
 static_assert(sizeof(IdKey) == AM_SZ_IDKEY, "IdKey");
 static_assert(sizeof(ElemKey) == AM_SZ_ELEMKEY, "ElemKey");
@@ -464,8 +475,11 @@ size_t am_scan_tmp_elems(uint32_t n) { return (n + SCAN_T - 1) / SCAN_T + 1; }
 __global__ void __launch_bounds__(256) k_max_hot(const DocBounds* __restrict__ bounds, uint32_t ndocs, uint64_t* __restrict__ max_hot) {
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= ndocs) return;
-  WsLayout L = ws_layout(bounds[d]);
-  atomicMax(reinterpret_cast<unsigned long long*>(max_hot), (unsigned long long)L.hot_total);
+  const DocBounds b = bounds[d];
+  WsLayout L = ws_layout(b);
+  // a scattered document needs the global-mode launch: report a hot set above any LDS budget
+  const uint64_t h = doc_scattered(b) ? (1ull << 40) : L.hot_total;
+  atomicMax(reinterpret_cast<unsigned long long*>(max_hot), (unsigned long long)h);
 }
 
 void am_launch_chunks(const BatchDev& b, hipStream_t s) {

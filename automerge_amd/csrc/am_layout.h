@@ -31,6 +31,8 @@ struct DocBounds {
   uint32_t K;   // changeIndexByHash entries
   uint32_t AM;  // actor-map entries (sum of change actor lists)
   uint32_t ND;  // sum of change deps (plan)
+  uint32_t P;   // 1: write the getPatch() log (am_doc_desc.flags & AM_DOC_WANT_PATCH)
+  uint32_t pad;
   uint64_t S;   // key + message string bytes over all rows
   uint64_t B;   // input bytes (base + changes)
   uint64_t span_lo, span_hi;  // arena byte span covering the document's chunks
@@ -46,9 +48,11 @@ struct WsLayout {
   uint64_t u0, idk, elemk, newent, elem_of, parent, first_child, next_sib, tour_nxt, tour_w;
   uint64_t cells;             // decode: (13 R + 2 E) int64 values
   uint64_t enc, enc_n;        // encode: V, W (int64) and S, RS, RB, RG (u32), enc_n entries each
+  uint64_t pscr;              // getPatch scratch (PatchScratch arrays, after the encode)
   uint64_t hot_total;
   // cold (offsets relative to the document's global workspace, after the hot mirror)
   uint64_t out, out_cap, total;
+  uint64_t patch, patch_nrec, patch_nmval, patch_heap;  // getPatch log (when P)
   uint64_t colbuf[OC_NCOLS + DC_NCOLS];
 };
 
@@ -132,6 +136,11 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   L.enc_n = nm;
   const uint64_t enc_end = L.u0 + 32 * nm;
   if (enc_end > uend) uend = enc_end;
+  // getPatch scratch: make ops (8+4+1 B) and counter states (8+4+8+4 B) per row, counter map
+  // (8+4+4 B) per succ entry
+  L.pscr = L.u0;
+  const uint64_t pscr_end = L.u0 + (b.P ? 13 * (R + 1) + 24 * (R + 1) + 16 * (E + 1) + 16 * 10 : 0);
+  if (pscr_end > uend) uend = pscr_end;
   o = uend;
   L.hot_total = o;
   // column buffers: a value costs at most 8 LEB bytes plus 2 bytes of RLE headers
@@ -155,6 +164,14 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   cap += 64 + 10 * (uint64_t)b.A + b.B + 42 * (uint64_t)b.H + 25 * 20 + b.B;
   L.out_cap = cap;
   L.out = take(cap);
+  if (b.P) {
+    L.patch_nrec = 3 * R + b.A + C + 2;
+    L.patch_nmval = R + 1;
+    L.patch_heap = b.S + 2 * b.B + 16;
+    L.patch = take(64 + 64 * L.patch_nrec + 32 * L.patch_nmval + L.patch_heap);
+  } else {
+    L.patch = L.patch_nrec = L.patch_nmval = L.patch_heap = 0;
+  }
   L.total = o;
   return L;
 }

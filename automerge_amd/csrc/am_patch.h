@@ -12,10 +12,12 @@
 #pragma once
 #include <stdint.h>
 
+// Everything is force-inlined into the caller: on the device the op source and the scratch live in
+// LDS, and inlining keeps that address space a compile-time fact (ds_* accesses, no flat casts).
 #ifdef __HIPCC__
-#define AM_PHD __host__ __device__
+#define AM_PHD __host__ __device__ __attribute__((always_inline))
 #else
-#define AM_PHD
+#define AM_PHD __attribute__((always_inline))
 #endif
 
 // ---- log layout: PatchHdr, then nrec PatchRec, then nmval PatchVal, then nheap bytes ----
@@ -80,7 +82,7 @@ struct PatchOut {
 #define PATCH_E_FLOAT_LEN 31u   // Invalid length for floating point number: arg0
 #define PATCH_E_UNKNOWN_COUNTER 32u  // increment operation arg0@actor(arg1) for unknown counter
 #define PATCH_U_CAPACITY 106u
-#define PATCH_U_VALUE 103u
+#define PATCH_U_VALUE 105u
 
 // ---- value decode (decodeValue, columnar.js:300-329) ----
 template <class Src>
@@ -228,7 +230,7 @@ AM_PHD inline bool patch_append_update(PatchOut& o, int64_t index, int64_t ec, i
 }
 
 template <class Src>
-AM_PHD bool patch_scan(const Src& src, PatchOut& o, PatchScratch& w, int64_t& max_op) {
+AM_PHD inline bool patch_scan(const Src& src, PatchOut& o, PatchScratch& w, int64_t& max_op) {
   o.nrec = o.nmval = o.nheap = 0;
   o.status = 0;
   max_op = 0;

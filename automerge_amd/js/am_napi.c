@@ -271,6 +271,22 @@ static napi_value js_doc_counts(napi_env env, napi_callback_info info) {
   return o;
 }
 
+// patch(handle) -> Uint8Array: the getPatch() log (am_doc_get_patch; materialized in backend.js)
+static napi_value js_doc_patch(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  DocBox* b = get_box(env, argv[0]);
+  if (!b) return NULL;
+  uint8_t* out = NULL;
+  size_t len = 0;
+  am_error err;
+  if (am_doc_get_patch(b->doc, &out, &len, &err)) return throw_am(env, &err);
+  napi_value v = new_u8(env, out, len);
+  am_free(out);
+  return v;
+}
+
 // queued(handle) -> [Uint8Array] changes waiting for missing dependencies
 static napi_value js_doc_queued(napi_env env, napi_callback_info info) {
   size_t argc = 1;
@@ -337,6 +353,7 @@ static napi_value init_module(napi_env env, napi_value exports) {
       {"docHeads", 0, js_doc_heads, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
       {"docChanges", 0, js_doc_changes, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
       {"docCounts", 0, js_doc_counts, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docPatch", 0, js_doc_patch, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
       {"docQueued", 0, js_doc_queued, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
       {"changeHashes", 0, js_change_hashes, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
       {"version", 0, js_version, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},

@@ -11,7 +11,8 @@
  *
  * Hash-graph queries (getChanges, getChangesAdded, getChangeByHash, getMissingDeps) are host
  * traversals over the applied change buffers, as in new.js:1913-2020.
- * Not on the GPU path yet: getPatch / patch diffs (SURVEY.md 8 a20/a21), applyLocalChange
+ * getPatch runs documentPatch on the GPU and materializes its log here.
+ * Not on the GPU path yet: applyChanges patch diffs (SURVEY.md 8 a20), applyLocalChange
  * (8(f) row 3), and the change history of a loaded document (8(f) row 2); those throw.
  */
 const path = require('path')
@@ -77,9 +78,92 @@ function loadChanges(backend, changes) {
   return {state, heads: native.docHeads(state)}
 }
 
+// ---- getPatch: documentPatch runs on the GPU (k_doc phase P7, automerge_amd/csrc/am_patch.h); this
+// turns its binary log into the patch object (new.js:2052-2060). Deserialization only: every
+// merge decision was taken on the device.
+const PR = {ACTOR: 1, CLOCK: 2, OBJ: 3, KEY: 4, PROP: 5, INSERT: 6, MULTI: 7, UPDATE: 8, REMOVE: 9}
+const PV = {NULL: 1, FALSE: 2, TRUE: 3, STR: 4, UINT: 5, INT: 6, F64: 7, COUNTER: 8, TIMESTAMP: 9, BYTES: 10, CHILD: 11}
+const NAMED_DT = {5: 'uint', 6: 'int', 7: 'float64', 8: 'counter', 9: 'timestamp'}
+const OBJ_TYPES = ['map', 'list', 'text', 'table']
+const utf8 = new TextDecoder('utf-8')
+
+function materializePatch(log, deps, pendingChanges, maxOp) {
+  const dv = new DataView(log.buffer, log.byteOffset, log.byteLength)
+  const i64 = o => Number(dv.getBigInt64(o, true))
+  const nrec = i64(24), nmval = i64(32), nheap = i64(40)
+  const recAt = k => 64 + 64 * k, valAt = k => 64 + 64 * nrec + 32 * k
+  const heapOff = 64 + 64 * nrec + 32 * nmval
+  const heap = log.subarray(heapOff, heapOff + nheap)
+  const actors = [], clock = {}, nodes = new Map()
+  const opid = (c, a) => `${c}@${actors[a]}`
+  const node = (c, a, t) => {
+    const k = `${c}@${a}`
+    let n = nodes.get(k)
+    if (!n) {
+      const type = OBJ_TYPES[t]
+      n = (type === 'list' || type === 'text') ? {objectId: opid(c, a), type, edits: []} : {objectId: opid(c, a), type, props: {}}
+      nodes.set(k, n)
+    }
+    return n
+  }
+  const prim = (vtag, dt, o) => {
+    switch (vtag) {
+      case PV.NULL: return null
+      case PV.FALSE: return false
+      case PV.TRUE: return true
+      case PV.STR: return utf8.decode(heap.subarray(i64(o), i64(o) + i64(o + 8)))
+      case PV.F64: return dv.getFloat64(o, true)
+      case PV.BYTES: return heap.slice(i64(o), i64(o) + i64(o + 8))
+      default: return i64(o)
+    }
+  }
+  const value = (vtag, dt, o) => {
+    if (vtag === PV.CHILD) return node(i64(o), i64(o + 8), dt)
+    const v = {type: 'value', value: prim(vtag, dt, o)}
+    if (NAMED_DT[vtag]) v.datatype = NAMED_DT[vtag]
+    else if (vtag === PV.BYTES) v.datatype = dt
+    return v
+  }
+  const root = {objectId: '_root', type: 'map', props: {}}
+  let cur = root, key = null, mv = 0
+  for (let k = 0; k < nrec; k++) {
+    const r = recAt(k)
+    const tag = dv.getUint32(r, true), vtag = dv.getUint32(r + 4, true)
+    const index = i64(r + 8), c1 = i64(r + 16), c2 = i64(r + 24)
+    const a1 = dv.getInt32(r + 32, true), a2 = dv.getInt32(r + 36, true)
+    const dt = dv.getUint32(r + 56, true), n = dv.getUint32(r + 60, true)
+    switch (tag) {
+      case PR.ACTOR: actors.push(toHex(heap.subarray(i64(r + 40), i64(r + 40) + i64(r + 48)))); break
+      case PR.CLOCK: clock[actors[a1]] = index; break
+      case PR.OBJ: cur = a1 < 0 ? root : nodes.get(`${c1}@${a1}`); break
+      case PR.KEY: key = utf8.decode(heap.subarray(i64(r + 40), i64(r + 40) + i64(r + 48))); cur.props[key] = {}; break
+      case PR.PROP: cur.props[key][opid(c2, a2)] = value(vtag, dt, r + 40); break
+      case PR.INSERT:
+        cur.edits.push({action: 'insert', index, elemId: opid(c1, a1), opId: opid(c2, a2), value: value(vtag, dt, r + 40)})
+        break
+      case PR.MULTI: {
+        const e = {action: 'multi-insert', index, elemId: opid(c1, a1)}
+        if (dt) e.datatype = dt < 100 ? NAMED_DT[PV.UINT + dt - 1] : dt - 100
+        e.values = []
+        for (let q = 0; q < n; q++, mv++) {
+          const vo = valAt(mv)
+          e.values.push(prim(dv.getUint32(vo, true), dv.getUint32(vo + 4, true), vo + 8))
+        }
+        cur.edits.push(e)
+        break
+      }
+      case PR.UPDATE: cur.edits.push({action: 'update', index, opId: opid(c2, a2), value: value(vtag, dt, r + 40)}); break
+      case PR.REMOVE: cur.edits.push({action: 'remove', index, count: n}); break
+    }
+  }
+  return {maxOp, clock, deps, pendingChanges, diffs: root}
+}
+
 function getPatch(backend) {
-  backendState(backend)
-  throw new RangeError('automerge_amd: getPatch is not implemented by this backend yet')
+  const state = backendState(backend)
+  const log = native.docPatch(state)
+  const c = native.docCounts(state)
+  return materializePatch(log, native.docHeads(state), c.pending, c.maxOp)
 }
 
 function getHeads(backend) {
@@ -217,5 +301,6 @@ function getMissingDeps(backend, heads = []) {
 module.exports = {
   init, clone, free, applyChanges, applyLocalChange, save, load, loadChanges, getPatch,
   getHeads, getAllChanges, getChanges, getChangesAdded, getChangeByHash, getMissingDeps,
-  engineVersion: native.version
+  engineVersion: native.version,
+  _materializePatch: materializePatch  // host stage of getPatch (exported for tests)
 }

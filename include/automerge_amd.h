@@ -63,6 +63,8 @@ enum am_status {
   AM_E_DUP_OPID,            // duplicate operation ID: %a0@%s
   AM_E_DOC_SEQ,             // Expected seq %a0, got %a1 for actor %s
   AM_E_LAST_REFERENCE_ERROR,
+  AM_E_FLOAT_LEN = 31,      // Invalid length for floating point number: %a0 (getPatch)
+  AM_E_UNKNOWN_COUNTER = 32,// increment operation %a0@%s for unknown counter (getPatch)
   AM_U_HASH_GRAPH = 100,    // needs the deferred hash graph of a loaded document (new.js:1826-1832)
   AM_U_UNKNOWN_COLUMN,      // column id outside DOC_OPS_COLUMNS / CHANGE_COLUMNS (new.js:1387-1425)
   AM_U_NONCAUSAL,           // opId counters violate Lamport order (insert after a later element, ...)
@@ -83,8 +85,10 @@ typedef struct am_doc_desc {
   uint32_t chg_begin, chg_count;   // change chunks [chg_begin, chg_begin + chg_count)
   uint32_t known_begin, known_count; // extra changeIndexByHash entries (hash, index)
   uint32_t flags;           // bit0: haveHashGraph (fresh doc, or host knows all change hashes)
+                            // bit1: AM_DOC_WANT_PATCH -- also write the getPatch() log of the result
   uint32_t pad;
 } am_doc_desc;
+#define AM_DOC_WANT_PATCH 2u
 typedef struct am_known_hash {      // changeIndexByHash entry supplied by the host
   uint8_t hash[32];
   int64_t index;
@@ -146,6 +150,10 @@ int am_batch_chunk_results(am_batch *b, uint8_t *hashes32, int32_t *chg_state, u
 /* Merged document chunk (uncompressed columns) of one document. */
 int am_batch_doc_output(am_batch *b, uint32_t doc, uint8_t *dst, uint64_t cap, uint64_t *len);
 int am_batch_doc_heads(am_batch *b, uint32_t doc, uint8_t *dst32, uint32_t cap, uint32_t *n);
+/* getPatch() log of document `doc` (staged with AM_DOC_WANT_PATCH): PatchHdr | records | values |
+ * heap as described in automerge_amd/csrc/am_patch.h; materialized by automerge_amd/patch.py or
+ * automerge_amd/js/backend.js. cap = 0 returns the size in *len. */
+int am_batch_doc_patch(am_batch *b, uint32_t doc, uint8_t *dst, uint64_t cap, uint64_t *len);
 /* Device time of each pipeline stage in the last run (ms): [chunks, bounds+scan, doc, out_hash]. */
 int am_batch_stage_times(am_batch *b, float *ms4);
 /* Device pointer + size of the staged arena / merged outputs (for bench byte accounting). */
@@ -166,6 +174,10 @@ int64_t am_doc_max_op(const am_doc *doc);
 size_t am_doc_num_changes(const am_doc *doc);
 /* i-th applied change buffer (as given by the caller) / its hash; for getChanges-style callers. */
 int am_doc_change(const am_doc *doc, size_t i, const uint8_t **data, size_t *len, uint8_t *hash32);
+/* Backend.getPatch(doc) (backend/backend.js:125-127, new.js:2052-2060): documentPatch over the
+ * current document on the GPU; returns the patch log (malloc'd, am_free) -- see am_batch_doc_patch.
+ * maxOp / deps / pendingChanges come from am_doc_max_op / am_doc_get_heads / am_doc_pending. */
+int am_doc_get_patch(am_doc *doc, uint8_t **out, size_t *len, am_error *err);
 /* i-th enqueued change (this.queue, new.js:1796-1871: changes waiting for missing deps), as given */
 int am_doc_queued(const am_doc *doc, size_t i, const uint8_t **data, size_t *len);
 void am_free(void *p);

@@ -9,8 +9,15 @@ const B = require(path.join(__dirname, '..', '..', 'automerge_amd', 'js', 'backe
 const hex = s => Uint8Array.from(Buffer.from(s, 'hex'))
 const toHex = u8 => Buffer.from(u8.buffer, u8.byteOffset, u8.byteLength).toString('hex')
 const docs = JSON.parse(fs.readFileSync(path.join(__dirname, '..', 'golden', 'docs.json'))).scenarios
+// canonical JSON (sorted keys, Uint8Array -> {__bytes: hex}) for deep comparison
+const canon = x => {
+  if (x instanceof Uint8Array) return {__bytes: toHex(x)}
+  if (Array.isArray(x)) return x.map(canon)
+  if (x && typeof x === 'object') { const o = {}; for (const k of Object.keys(x).sort()) o[k] = canon(x[k]); return o }
+  return x
+}
 const bad = []
-let steps = 0
+let steps = 0, patches = 0
 for (const sc of docs) {
   let st = null
   for (let i = 0; i < sc.steps.length; i++) {
@@ -26,7 +33,7 @@ for (const sc of docs) {
           if (!/outdated Automerge document/.test(e.message)) bad.push([sc.name, i, 'frozen message', e.message])
         }
       }
-      res = {save: toHex(B.save(st)), heads: B.getHeads(st)}
+      res = {save: toHex(B.save(st)), heads: B.getHeads(st), patch: B.getPatch(st)}
     } catch (e) {
       res = {error: e.message, cls: e.constructor.name}
     }
@@ -38,6 +45,11 @@ for (const sc of docs) {
     if (res.error) { bad.push([sc.name, i, 'unexpected', res.cls, res.error]); break }
     if (res.save !== exp.save) bad.push([sc.name, i, 'save'])
     else if (JSON.stringify(res.heads) !== JSON.stringify(exp.heads)) bad.push([sc.name, i, 'heads'])
+    else if (exp.getPatch) {
+      patches++
+      const want = Object.assign({}, exp.getPatch, {pendingChanges: exp.pending})
+      if (JSON.stringify(canon(res.patch)) !== JSON.stringify(canon(want))) bad.push([sc.name, i, 'getPatch'])
+    }
   }
 }
 // hash-graph queries on a fresh document built from the first multi-change scenario
@@ -51,4 +63,4 @@ if (sc) {
   graph = {changes: got.length, applied_equal_given: JSON.stringify(got.slice().sort()) === JSON.stringify(all.slice().sort()),
            missing: B.getMissingDeps(st), since_heads: B.getChanges(st, B.getHeads(st)).length}
 }
-console.log(JSON.stringify({scenarios: docs.length, steps, bad: bad.slice(0, 20), nbad: bad.length, graph}))
+console.log(JSON.stringify({scenarios: docs.length, steps, patches, bad: bad.slice(0, 20), nbad: bad.length, graph}))

@@ -125,3 +125,42 @@ def test_frozen_state():
     with pytest.raises(RuntimeError, match="outdated Automerge document"):
         B.save(s0)
     assert B.save(s1).hex() == sc["results"][0]["save"]
+
+
+def _jsonable(x):
+    if isinstance(x, (bytes, bytearray)):
+        return {"__bytes": bytes(x).hex()}
+    if isinstance(x, dict):
+        return {k: _jsonable(v) for k, v in x.items()}
+    if isinstance(x, list):
+        return [_jsonable(v) for v in x]
+    return x
+
+
+def test_getpatch_per_step_matches_reference(docs):
+    """Backend.getPatch() after every step (documentPatch on the GPU, k_doc phase P7) against the
+    reference's getPatch of the same document state (tests/golden/docs.json)."""
+    from automerge_amd import _native as N
+    from automerge_amd import backend as B
+    n, bad = 0, []
+    for sc in docs:
+        st = None
+        for i, (step, exp) in enumerate(zip(sc["steps"], sc["results"])):
+            if "error" in exp:
+                break
+            if step["op"] == "load":
+                st = B.load(bytes.fromhex(step["bytes"]))
+            else:
+                if st is None:
+                    st = B.init()
+                st, _ = B.applyChanges(st, [bytes.fromhex(c) for c in step["changes"]])
+            want = dict(exp["getPatch"], pendingChanges=exp["pending"])
+            try:
+                got = _jsonable(B.getPatch(st))
+            except N.AutomergeError as e:
+                got = {"error": str(e)}
+            n += 1
+            if got != want:
+                bad.append((sc["name"], i))
+    assert n > 400
+    assert not bad, bad[:10]

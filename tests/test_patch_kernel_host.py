@@ -66,3 +66,23 @@ def test_patch_scan_matches_reference_getpatch(patch_host, docs, tmp_path):
         if got != exp:
             bad.append((name, i))
     assert not bad, bad[:10]
+
+
+def test_js_host_stage_materializes_same_logs(patch_host, docs, tmp_path):
+    """The Node host stage (backend.js materializePatch) on the same engine logs."""
+    import json
+    node = shutil.which("node")
+    if not node or not os.path.exists(os.path.join(ROOT, "automerge_amd", "js", "am_napi.node")):
+        pytest.skip("node or am_napi.node missing")
+    cases = [res for sc in docs for res in sc["results"] if "getPatch" in res and "save" in res]
+    logs = run_logs(patch_host, [bytes.fromhex(res["save"]) for res in cases], str(tmp_path))
+    payload = [{"log": log.hex(), "deps": res["getPatch"]["deps"], "pending": res["getPatch"]["pendingChanges"],
+                "expect": res["getPatch"]} for res, log in zip(cases, logs)]
+    f = os.path.join(str(tmp_path), "cases.json")
+    with open(f, "w") as fh:
+        json.dump(payload, fh)
+    out = subprocess.run([node, os.path.join(ROOT, "tests", "js", "patch_materialize.js"), f], capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["n"] > 400 and res["nbad"] == 0, res
