@@ -85,6 +85,7 @@ _sigs = {
     "am_stage_document": (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t),
                                     C.POINTER(C.c_int), C.POINTER(Error)]),
     "am_workload_c4": (C.c_uint64, [C.c_uint64, C.c_uint32, P, C.c_uint64, P, P, C.POINTER(C.c_uint64), C.c_int]),
+    "am_workload_c2": (C.c_uint64, [C.c_uint64, C.c_uint32, P, C.c_uint64, P, P, C.POINTER(C.c_uint64), C.c_int]),
 }
 for _name, (_res, _args) in _sigs.items():
     _f = getattr(lib, _name)

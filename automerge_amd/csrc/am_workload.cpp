@@ -326,23 +326,33 @@ void gen_c4(uint32_t doc_index, DocOut& out) {
   out.ops = 60;
 }
 
-}  // namespace
+// C2 (SURVEY.md §8(d), configs[1]): change 1 by actor 0 sets k0..k7 (int), a counter 'count' and a
+// string 'name'; two concurrent changes (actors 1, 2) increment the counter and overwrite k1.
+// JS generator: tests/golden/gen/make_fixtures.js c2Doc (same LCG call order).
+void gen_c2(uint32_t doc_index, DocOut& out) {
+  uint32_t s = doc_index;
+  std::vector<Actor> actors;
+  make_actors(s, 3, actors);
+  std::vector<Op> ops;
+  for (int k = 0; k < 8; k++)
+    ops.push_back({-1, 0, "k" + std::to_string(k), -1, 0, false, 1, 4, (int64_t)(lcg(s) % 100000), "", {}});
+  ops.push_back({-1, 0, "count", -1, 0, false, 1, 8, (int64_t)(lcg(s) % 100), "", {}});
+  ops.push_back({-1, 0, "name", -1, 0, false, 1, 6, 0, "doc-" + std::to_string(doc_index), {}});
+  uint8_t h1[32];
+  out.changes.push_back(encode_change(actors, 0, 1, 1, {}, ops, h1));
+  for (int i = 1; i <= 2; i++) {
+    std::vector<Op> o2;
+    o2.push_back({-1, 0, "count", -1, 0, false, 5, 4, (int64_t)(1 + lcg(s) % 9), "", {{9, 0}}});
+    o2.push_back({-1, 0, "k1", -1, 0, false, 1, 4, (int64_t)(lcg(s) % 100000), "", {{2, 0}}});
+    uint8_t h[32];
+    out.changes.push_back(encode_change(actors, i, 1, 11, {std::vector<uint8_t>(h1, h1 + 32)}, o2, h));
+  }
+  out.ops = 14;
+}
 
-extern "C" {
-
-/* Generates C4 documents [first, first + n): each = base document (change 0 saved) + 12 change
- * chunks. Returns the number of bytes needed; fills the outputs when `arena` is non-NULL and
- * cap suffices. chunks: n * 13 entries; docs: n entries. ops_out: total ops in the changes. */
-uint64_t am_workload_c4(uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks, am_doc_desc* docs,
-                        uint64_t* ops_out, int nthreads) {
-  std::vector<DocOut> outs(n);
-  if (nthreads < 1) nthreads = 1;
-  std::vector<std::thread> th;
-  for (int t = 0; t < nthreads; t++)
-    th.emplace_back([&, t]() {
-      for (uint32_t d = t; d < n; d += nthreads) gen_c4((uint32_t)(first + d), outs[d]);
-    });
-  for (auto& x : th) x.join();
+// Lays out documents [base?][changes...] back to back in the arena
+uint64_t layout(std::vector<DocOut>& outs, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks, am_doc_desc* docs,
+                uint64_t* ops_out) {
   uint64_t total = 0, ops = 0;
   for (auto& o : outs) {
     total += o.base.size();
@@ -353,12 +363,15 @@ uint64_t am_workload_c4(uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap
   if (!arena || cap < total) return total;
   uint64_t off = 0;
   uint32_t ci = 0;
-  for (uint32_t d = 0; d < n; d++) {
+  for (size_t d = 0; d < outs.size(); d++) {
     DocOut& o = outs[d];
-    docs[d].base_chunk = ci;
-    chunks[ci++] = {off, (uint32_t)o.base.size(), 0};
-    memcpy(arena + off, o.base.data(), o.base.size());
-    off += o.base.size();
+    docs[d].base_chunk = -1;
+    if (!o.base.empty()) {
+      docs[d].base_chunk = ci;
+      chunks[ci++] = {off, (uint32_t)o.base.size(), 0};
+      memcpy(arena + off, o.base.data(), o.base.size());
+      off += o.base.size();
+    }
     docs[d].chg_begin = ci;
     docs[d].chg_count = (uint32_t)o.changes.size();
     docs[d].known_begin = 0;
@@ -372,6 +385,38 @@ uint64_t am_workload_c4(uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap
     }
   }
   return total;
+}
+
+template <class Gen>
+uint64_t generate(Gen gen, uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks,
+                  am_doc_desc* docs, uint64_t* ops_out, int nthreads) {
+  std::vector<DocOut> outs(n);
+  if (nthreads < 1) nthreads = 1;
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; t++)
+    th.emplace_back([&, t]() {
+      for (uint32_t d = t; d < n; d += nthreads) gen((uint32_t)(first + d), outs[d]);
+    });
+  for (auto& x : th) x.join();
+  return layout(outs, arena, cap, chunks, docs, ops_out);
+}
+
+}  // namespace
+
+extern "C" {
+
+/* Generates C4 documents [first, first + n): each = base document (change 0 saved) + 12 change
+ * chunks. Returns the number of bytes needed; fills the outputs when `arena` is non-NULL and
+ * cap suffices. chunks: n * 13 entries; docs: n entries. ops_out: total ops in the changes. */
+uint64_t am_workload_c4(uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks, am_doc_desc* docs,
+                        uint64_t* ops_out, int nthreads) {
+  return generate(gen_c4, first, n, arena, cap, chunks, docs, ops_out, nthreads);
+}
+
+/* C2: documents [first, first + n), each = Backend.init() + 3 change chunks (no base chunk). */
+uint64_t am_workload_c2(uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks, am_doc_desc* docs,
+                        uint64_t* ops_out, int nthreads) {
+  return generate(gen_c2, first, n, arena, cap, chunks, docs, ops_out, nthreads);
 }
 
 }  // extern "C"

@@ -226,6 +226,10 @@ int am_sync_select(am_engine *eng, uint32_t npairs, const uint64_t *coff, const 
  * and cap suffices. ops_out receives the number of ops in the 12 changes of all documents. */
 uint64_t am_workload_c4(uint64_t first_doc, uint32_t ndocs, uint8_t *arena, uint64_t cap, am_chunk_desc *chunks,
                         am_doc_desc *docs, uint64_t *ops_out, int nthreads);
+/* C2 (configs[1]): document i = Backend.init() + 3 changes (10 map/counter/string sets by actor 0;
+ * two concurrent changes incrementing the counter and overwriting k1), 3 chunks per document. */
+uint64_t am_workload_c2(uint64_t first_doc, uint32_t ndocs, uint8_t *arena, uint64_t cap, am_chunk_desc *chunks,
+                        am_doc_desc *docs, uint64_t *ops_out, int nthreads);
 
 #ifdef __cplusplus
 }

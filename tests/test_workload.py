@@ -39,3 +39,32 @@ def test_c4_oracle_merge_of_generated_docs():
         doc.apply(changes)
         assert sha(doc.save()) == w[i]["merged"]
         assert doc.heads() == w[i]["heads"]
+
+
+def test_c2_generator_matches_reference_encoder():
+    from automerge_amd import workload
+    w = golden("workload.json")["c2"]
+    arena, chunks, docs, ops = workload.c2(0, len(w))
+    assert ops == 14 * len(w)
+    for i, v in enumerate(w):
+        base, changes = workload.doc_chunks(arena, chunks, docs, i)
+        assert base is None
+        assert [sha(c) for c in changes] == v["changes"], i
+
+
+def test_c2_oracle_merge_and_getpatch_of_generated_docs():
+    """init + applyChanges of the generated changes gives the reference's saved document, whose
+    getPatch (documentPatch) the oracle reproduces."""
+    import json
+    import oracle_ffi as O
+    from automerge_amd import workload
+    w = golden("workload.json")["c2"]
+    arena, chunks, docs, _ = workload.c2(0, 16)
+    for i in range(16):
+        _, changes = workload.doc_chunks(arena, chunks, docs, i)
+        doc = O.Doc.init()
+        doc.apply(changes)
+        saved = doc.save()
+        assert sha(saved) == w[i]["doc_sha"]
+        if w[i].get("getPatch"):
+            assert O.Doc.load(saved).patch() == json.loads(json.dumps(w[i]["getPatch"]))
