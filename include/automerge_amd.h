@@ -10,6 +10,8 @@
  *   am_doc_save            <- Backend.save             backend/backend.js:96-98,   new.js:2025-2047
  *   am_doc_get_heads       <- Backend.getHeads         backend/backend.js:134-136
  *   am_doc_clone / _free   <- Backend.clone / free     backend/backend.js:12-19
+ *   am_doc_get_patch       <- Backend.getPatch         backend/backend.js:125-127, new.js:2052-2060
+ *   am_bloom_* / am_sync_select <- BloomFilter / getChangesToSend   sync.js:38-125, 246-306
  *   am_doc_change/_queued  <- this.changes / this.queue (getChanges & getMissingDeps, new.js:1913-2020)
  *   am_change_hashes       <- decodeChangeMeta(.., true).hash   columnar.js:783-793
  *   am_batch_*             batched load + applyChanges over thousands of documents per launch
