@@ -728,8 +728,8 @@ extern "C" am_doc* am_doc_load(am_engine* eng, const uint8_t* data, size_t len, 
   d->have_hash_graph = false;
   d->heads = res.heads;
   d->nchanges = res.r.nchanges;
-  d->max_op = 0;
-  // maxOp of a loaded document: the largest op counter in ids and succs (documentPatch, new.js:1627-1630)
+  // maxOp of a loaded document: the largest op counter in ids and succs (documentPatch,
+  // new.js:1627-1630, 1749) -- reduced by k_doc over the base rows
   d->max_op = res.r.max_op;
   if (err) err->code = 0;
   return d;

@@ -939,6 +939,18 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
     wave_excl_scan_arr(psum, R);
     __syncthreads();
     for (uint32_t i = t; i < R; i += T) place_row(s, i, vsum, psum);
+    // maxOp of the loaded document: the largest counter among its op ids and succs
+    // (documentPatch, new.js:1627-1630 -> this.maxOp, new.js:1749); applied changes raise it
+    {
+      int64_t m = 0;
+      for (uint32_t i = t; i < s.nb; i += T) m = rows[i].id_ctr > m ? rows[i].id_ctr : m;
+      for (uint32_t j = t; j < s.nbe; j += T) m = ents[j].ctr > m ? ents[j].ctr : m;
+      for (int o = 32; o > 0; o >>= 1) {
+        const int64_t x = __shfl_xor(m, o, 64);
+        m = x > m ? x : m;
+      }
+      if (t == 0 && m > s.max_op) s.max_op = m;
+    }
     __syncthreads();
     if (s.status) goto done;
 #if defined(AM_STOP_PHASE) && AM_STOP_PHASE == 3

@@ -108,7 +108,7 @@ typedef struct am_doc_result {
   uint32_t nheads;
   uint32_t nops;            // op rows in the merged document
   uint32_t nchanges;        // change rows in the merged document
-  int64_t max_op;           // docState.maxOp over the applied changes
+  int64_t max_op;           // this.maxOp of the result: max(base op ids / succ counters, applied changes)
   uint64_t out_off;         // merged document chunk (uncompressed columns) in the output arena
   uint64_t out_len;
   uint64_t ws_off, ws_bytes;
