@@ -123,5 +123,12 @@ class Batch:
             return None
         return list(ms)
 
+    def digest(self, first_doc=0):
+        """Device-side output digest (am_batch_digest; host restatement: shard.doc_digest)."""
+        out = C.c_uint64()
+        if N.lib.am_batch_digest(self._b, first_doc, C.byref(out)):
+            raise N.AutomergeError("automerge_amd: digest failed")
+        return int(out.value)
+
     def workspace_bytes(self):
         return N.lib.am_batch_workspace_bytes(self._b)

@@ -503,6 +503,18 @@ extern "C" int am_batch_stage_times(am_batch* b, float* ms4) {
   return 0;
 }
 
+extern "C" int am_batch_digest(am_batch* b, uint64_t first_doc, uint64_t* digest) {
+  if (!set_device(b->eng) || !digest) return 1;
+  DevBuf<uint64_t> d;
+  if (!d.ensure(1)) return 1;
+  hipStream_t s = b->eng->stream;
+  am_launch_digest(b->dev(), first_doc, d.p, s);
+  if (hipMemcpyAsync(digest, d.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s) != hipSuccess) return 1;
+  if (hipStreamSynchronize(s) != hipSuccess) return 1;
+  *digest &= 0x7FFFFFFFFFFFFFFFull;
+  return 0;
+}
+
 extern "C" uint64_t am_batch_workspace_bytes(am_batch* b) { return b->ws_need; }
 
 // =============================================================================================

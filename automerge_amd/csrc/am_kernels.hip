@@ -520,6 +520,37 @@ __global__ void __launch_bounds__(256) k_out_hash_ws(am_doc_result* __restrict__
   sha256_dev(p + 8, len - 8, h);
   p[4] = h[0]; p[5] = h[1]; p[6] = h[2]; p[7] = h[3];
 }
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27; x *= 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+// per-document output digest (am_batch_digest): thread per document, one atomic per workgroup
+__global__ void __launch_bounds__(256) k_digest(const am_doc_result* __restrict__ res, uint32_t ndocs, const uint8_t* __restrict__ ws,
+                                                uint64_t first, unsigned long long* __restrict__ out) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t v = 0;
+  if (d < ndocs) {
+    const am_doc_result r = res[d];
+    uint32_t chk = 0;
+    if (r.status == 0 && r.out_len >= 8) {
+      const uint8_t* p = ws + r.out_off + 4;
+      chk = (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+    }
+    v = mix64(((first + d) << 32) | chk) + (r.status ? 0 : r.out_len) * 0x9E3779B97F4A7C15ull + r.status;
+  }
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __shared__ uint64_t part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, (unsigned long long)(part[0] + part[1] + part[2] + part[3]));
+}
+void am_launch_digest(const BatchDev& b, uint64_t first, uint64_t* d_out, hipStream_t s) {
+  (void)hipMemsetAsync(d_out, 0, sizeof(uint64_t), s);
+  if (b.ndocs)
+    hipLaunchKernelGGL(k_digest, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, b.results, b.ndocs, b.ws, first,
+                       reinterpret_cast<unsigned long long*>(d_out));
+}
 void am_launch_out_hash(const BatchDev& b, hipStream_t s) {
   if (!b.ndocs) return;
   hipLaunchKernelGGL(k_out_hash_ws, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, b.results, b.ndocs, b.ws, b.bounds);

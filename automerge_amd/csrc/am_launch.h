@@ -30,6 +30,7 @@ void am_launch_chunks(const BatchDev& b, hipStream_t s);
 void am_launch_bounds(const BatchDev& b, hipStream_t s);   // k_bounds + scan of ws bytes
 void am_launch_doc(const BatchDev& b, hipStream_t s);
 void am_launch_out_hash(const BatchDev& b, hipStream_t s);
+void am_launch_digest(const BatchDev& b, uint64_t first, uint64_t* d_out, hipStream_t s);
 void am_launch_sha256(const uint8_t* arena, const am_chunk_desc* msgs, uint32_t n, uint8_t* out, hipStream_t s);
 size_t am_scan_tmp_elems(uint32_t n);
 

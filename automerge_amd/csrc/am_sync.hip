@@ -122,21 +122,34 @@ __host__ __device__ static inline uint8_t rd_uleb32(const uint8_t* p, uint64_t l
   return BP_INCOMPLETE;
 }
 
-// BloomFilter(bytes).containsHash(hash): BP_YES / BP_NO, or an error code for a malformed filter
-__host__ __device__ static uint8_t bloom_test(const uint8_t* f, uint64_t len, const uint8_t* h) {
+// new BloomFilter(bytes) header decode (sync.js:47-58): BP_NO when well formed (or empty), else the
+// error code; the filter's bits are at f + pos, nbytes long.
+__host__ __device__ static uint8_t bloom_header(const uint8_t* f, uint64_t len, uint64_t& pos, uint32_t& ne, uint32_t& np,
+                                                uint64_t& nbytes) {
+  pos = 0; ne = 0; np = 0; nbytes = 0;
   if (len == 0) return BP_NO;
-  uint64_t pos = 0;
-  uint32_t ne, bpe, np;
+  uint32_t bpe;
   uint8_t e;
   if ((e = rd_uleb32(f, len, pos, ne)) || (e = rd_uleb32(f, len, pos, bpe)) || (e = rd_uleb32(f, len, pos, np))) return e;
-  const uint64_t nbytes = ((uint64_t)ne * bpe + 7) / 8;
+  nbytes = ((uint64_t)ne * bpe + 7) / 8;
   if (pos + nbytes > len) return BP_SUBARRAY;
+  return BP_NO;
+}
+
+// BloomFilter(bytes).containsHash(hash): BP_YES / BP_NO, or an error code for a malformed filter
+__host__ __device__ static uint8_t bloom_test(const uint8_t* f, uint64_t len, const uint8_t* h) {
+  uint64_t pos, nbytes;
+  uint32_t ne, np;
+  const uint8_t e = bloom_header(f, len, pos, ne, np, nbytes);
+  if (e) return e;
   if (ne == 0 || nbytes == 0) return BP_NO;
   if (np > BLOOM_MAX_PROBES) return BP_TOO_MANY;
   const uint8_t* bits = f + pos;
   Probe p;
   p.init(h, 8 * nbytes);
-  for (uint32_t k = 0; k < np; k++) {
+  // getProbes always returns [x] before its loop (sync.js:95-100): numProbes 0 still tests one bit
+  const uint32_t nprobe = np > 0 ? np : 1;
+  for (uint32_t k = 0; k < nprobe; k++) {
     if (k) p.step();
     if (!(bits[p.x >> 3] & (1u << (p.x & 7)))) return BP_NO;
   }
@@ -161,6 +174,17 @@ __host__ __device__ static uint8_t sync_select_one(uint32_t pr, const uint64_t* 
                                                    const uint64_t* doff, const int32_t* didx, const uint64_t* pfoff,
                                                    const uint8_t* filters, const uint64_t* foff, uint8_t* send) {
   const uint64_t c0 = coff[pr], c1 = coff[pr + 1], f0 = pfoff[pr], f1 = pfoff[pr + 1];
+  // every `have` filter is decoded before selection (sync.js:252-256): the first malformed one fails
+  // the pair even when no change would probe it
+  for (uint64_t f = f0; f < f1; f++) {
+    uint64_t pos, nbytes;
+    uint32_t ne, np;
+    const uint8_t e = bloom_header(filters + foff[f], foff[f + 1] - foff[f], pos, ne, np, nbytes);
+    if (e) {
+      for (uint64_t c = c0; c < c1; c++) send[c] = 0;
+      return e;
+    }
+  }
   uint8_t st = BP_NO;
   for (uint64_t c = c0; c < c1; c++) {
     uint8_t neg = 1;

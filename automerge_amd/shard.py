@@ -3,7 +3,7 @@ independent, so rank r merges documents [r*D, (r+1)*D) with no collective on the
 The only exchange is one all-gather of a small per-rank digest after the timed region (RCCL over
 xGMI on the GPU box; gloo in the CPU tests)."""
 
-DIGEST_FIELDS = ("docs", "ops", "errors", "out_bytes", "out_xor")
+DIGEST_FIELDS = ("docs", "ops", "errors", "out_bytes", "out_digest")
 
 
 def shard_range(rank, world, docs_per_rank):
@@ -13,16 +13,35 @@ def shard_range(rank, world, docs_per_rank):
     return rank * docs_per_rank, docs_per_rank
 
 
-def out_digest(res):
-    """Order-independent digest of a batch's results (numpy structured array of am_doc_result)."""
-    import numpy as np
-    x = np.bitwise_xor.reduce(res["out_len"].astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)) if len(res) else 0
-    return int(x) & 0x7FFFFFFFFFFFFFFF
+M64 = (1 << 64) - 1
+
+
+def _mix64(x):
+    """splitmix64 finalizer (the device's mix64 in am_kernels.hip)."""
+    x ^= x >> 30
+    x = (x * 0xBF58476D1CE4E5B9) & M64
+    x ^= x >> 27
+    x = (x * 0x94D049BB133111EB) & M64
+    return x ^ (x >> 31)
+
+
+def doc_digest(index, status, out):
+    """Digest term of one document: its global index, the container checksum (bytes 4..8 of the
+    merged chunk, columnar.js:659-686), its length and status. Equal lengths no longer cancel,
+    and a wrong or missing byte anywhere in a document changes its checksum."""
+    chk = int.from_bytes(out[4:8], "little") if status == 0 and len(out) >= 8 else 0
+    n = len(out) if status == 0 else 0
+    return (_mix64(((index << 32) | chk) & M64) + n * 0x9E3779B97F4A7C15 + status) & M64
+
+
+def combine(terms):
+    """Sum of per-document terms mod 2^63 (order independent; am_batch_digest computes the same)."""
+    return sum(terms) & 0x7FFFFFFFFFFFFFFF
 
 
 def exchange(dist, digest, device):
     """All-gather of the per-rank digest (len(DIGEST_FIELDS) int64); returns the summed fields
-    (out_xor is XOR-combined) and the per-rank rows. `dist` None means a single process."""
+    (out_digest summed mod 2^63) and the per-rank rows. `dist` None means a single process."""
     import torch
     t = torch.tensor([int(v) for v in digest], dtype=torch.int64, device=device)
     if dist is None:
@@ -32,7 +51,4 @@ def exchange(dist, digest, device):
         dist.all_gather(parts, t)
         rows = [p.tolist() for p in parts]
     tot = [sum(r[i] for r in rows) for i in range(len(DIGEST_FIELDS) - 1)]
-    x = 0
-    for r in rows:
-        x ^= r[-1]
-    return tot + [x], rows
+    return tot + [combine(r[-1] for r in rows)], rows

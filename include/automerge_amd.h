@@ -158,6 +158,12 @@ int am_batch_doc_heads(am_batch *b, uint32_t doc, uint8_t *dst32, uint32_t cap, 
 int am_batch_doc_patch(am_batch *b, uint32_t doc, uint8_t *dst, uint64_t cap, uint64_t *len);
 /* Device time of each pipeline stage in the last run (ms): [chunks, bounds+scan, doc, out_hash]. */
 int am_batch_stage_times(am_batch *b, float *ms4);
+/* Order-independent digest of the batch's merged outputs, for the cross-rank exchange: the sum
+ * mod 2^63 over documents d of mix64(((first_doc + d) << 32) | checksum32_le(output d)) +
+ * out_len(d) * 0x9E3779B97F4A7C15 + status(d), where checksum32 = bytes 4..8 of the merged
+ * container (columnar.js:659-686) and mix64 is the splitmix64 finalizer. Host restatement:
+ * automerge_amd/shard.py doc_digest. */
+int am_batch_digest(am_batch *b, uint64_t first_doc, uint64_t *digest);
 /* Device pointer + size of the staged arena / merged outputs (for bench byte accounting). */
 uint64_t am_batch_workspace_bytes(am_batch *b);
 

@@ -95,7 +95,9 @@ int oc_bloom_contains(const uint8_t *f, size_t len, const uint8_t *hash32) {
     y = ((uint64_t)h[4] | (uint64_t)h[5] << 8 | (uint64_t)h[6] << 16 | (uint64_t)h[7] << 24) % modulo;
     z = ((uint64_t)h[8] | (uint64_t)h[9] << 8 | (uint64_t)h[10] << 16 | (uint64_t)h[11] << 24) % modulo;
   }
-  for (uint32_t i = 0; i < np; i++) {
+  /* getProbes returns [x] before its loop (sync.js:95-100): numProbes 0 still tests one bit */
+  const uint32_t nprobe = np > 0 ? np : 1;
+  for (uint32_t i = 0; i < nprobe; i++) {
     if (i) {
       x = (x + y) % modulo;
       y = (y + z) % modulo;

@@ -573,6 +573,36 @@ function bloomVectors() {
   return out
 }
 
+// Hand-made filter headers (numProbes 0/1/2, bits shorter than the header, incomplete numbers):
+// containsHash as the reference decodes them (new BloomFilter(bytes), sync.js:47-58, 112-120).
+function bloomEdgeVectors() {
+  const r = lcg(4242)
+  const rh = () => { let h = ''; for (let j = 0; j < 8; j++) h += r().toString(16).padStart(8, '0'); return h }
+  const out = []
+  const hdr = (ne, bpe, np) => { const e = new enc.Encoder(); e.appendUint32(ne); e.appendUint32(bpe); e.appendUint32(np); return e.buffer }
+  for (let t = 0; t < 24; t++) {
+    const ne = 1 + r() % 12, bpe = [10, 3, 1, 0][t % 4], np = [0, 1, 2, 7][(t >> 2) % 4]
+    const nbytes = Math.ceil(ne * bpe / 8)
+    const bits = new Uint8Array(nbytes)
+    for (let i = 0; i < nbytes; i++) bits[i] = r() & 0xff
+    const h = hdr(ne, bpe, np)
+    const bytes = new Uint8Array(h.byteLength + nbytes)
+    bytes.set(h, 0); bytes.set(bits, h.byteLength)
+    const probes = []
+    for (let i = 0; i < 16; i++) probes.push(rh())
+    const err = errOf(() => new sync.BloomFilter(bytes))
+    const f = err ? null : new sync.BloomFilter(bytes)
+    out.push({bytes: hex(bytes), probes, contains: f ? probes.map(x => f.containsHash(x)) : null, error: err})
+  }
+  // malformed: truncated bits, incomplete header numbers, out-of-range uint32
+  const bad = [hex(hdr(4, 10, 7)) + 'ff', '80', '0a80', '0a0a', 'ffffffff7f0a07']
+  for (const b of bad) {
+    const bytes = unhex(b)
+    out.push({bytes: b, probes: [rh()], contains: null, error: errOf(() => new sync.BloomFilter(bytes))})
+  }
+  return out
+}
+
 function main() {
   const write = (name, obj) => {
     fs.writeFileSync(path.join(OUT, name), JSON.stringify(obj) + '\n')
@@ -585,6 +615,7 @@ function main() {
   write('changes.json', changeVectors(hand.concat(rand)))
   write('workload.json', workloadVectors())
   write('bloom.json', bloomVectors())
+  write('bloom_edge.json', bloomEdgeVectors())
 }
 
 main()

@@ -164,3 +164,29 @@ def test_getpatch_per_step_matches_reference(docs):
                 bad.append((sc["name"], i))
     assert n > 400
     assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("kind,first,n", [("c4", 1000, 1500), ("c2", 77, 1500)])
+def test_workload_batch_matches_oracle_and_digest(kind, first, n):
+    """Seeded C4 / C2 batches (the bench's generator, am_workload.cpp): every merged document equals
+    the CPU oracle's save(), and the device digest (am_batch_digest) equals the host restatement
+    (shard.doc_digest) over the oracle's bytes."""
+    import oracle_ffi as O
+    from automerge_amd import shard, workload
+    from automerge_amd.batch import Batch
+    arena, chunks, docs, _ = getattr(workload, kind)(first, n)
+    b = Batch()
+    b.stage(arena, chunks, docs)
+    b.run()
+    b.sync()
+    r = b.results()
+    terms = []
+    for i in range(n):
+        base, changes = workload.doc_chunks(arena, chunks, docs, i)
+        ref = O.Doc.load(base) if base else O.Doc.init()
+        ref.apply(changes)
+        want = ref.save()
+        assert int(r[i]["status"]) == 0, (i, int(r[i]["status"]))
+        assert b.doc_output(i, r[i]) == want, i
+        terms.append(shard.doc_digest(first + i, 0, want))
+    assert b.digest(first) == shard.combine(terms)

@@ -60,3 +60,33 @@ def test_gpu_select_changes_matches_oracle():
     got = sync.select_changes(pairs)
     for (hashes, deps, filters), g in zip(pairs, got):
         assert g == O.sync_select(hashes, deps, filters)
+
+
+def test_gpu_bloom_edge_vectors_match_reference():
+    """numProbes 0/1/2 and sparse filters (tests/golden/bloom_edge.json) probed on the GPU."""
+    from automerge_amd import _native as N
+    from automerge_amd import sync
+    good = [v for v in golden("bloom_edge.json") if not v["error"]]
+    filters = [bytes.fromhex(v["bytes"]) for v in good]
+    probes = [(i, h) for i, v in enumerate(good) for h in v["probes"]]
+    assert sync.probe(filters, probes) == [bool(c) for v in good for c in v["contains"]]
+    for v in golden("bloom_edge.json"):
+        if v["error"]:
+            with pytest.raises(N.AutomergeError, match=v["error"]["message"]):
+                sync.BloomFilter(bytes.fromhex(v["bytes"]))
+
+
+def test_gpu_select_rejects_malformed_second_filter():
+    """The reference decodes every `have` filter before selecting (sync.js:252-256): a malformed
+    second filter raises even when the first already contains every change, and a pair with no
+    changes still raises."""
+    from automerge_amd import _native as N
+    from automerge_amd import sync
+    rnd = random.Random(3)
+    hashes = [rnd.randbytes(32) for _ in range(3)]
+    first = O.bloom_build(hashes)
+    bad = first[:-1]
+    with pytest.raises(N.AutomergeError, match="subarray exceeds buffer size"):
+        sync.select_changes([(hashes, [[], [0], [1]], [first, bad])])
+    with pytest.raises(N.AutomergeError, match="buffer ended with incomplete number"):
+        sync.select_changes([([], [], [first, b"\x80"])])

@@ -28,15 +28,15 @@ def _merge_shard(first, n):
     import oracle_ffi as O
     from automerge_amd import shard, workload
     arena, chunks, docs, ops = workload.c4(first, n)
-    lens = []
+    lens, terms = [], []
     for i in range(n):
         base, changes = workload.doc_chunks(arena, chunks, docs, i)
         d = O.Doc.load(base)
         d.apply(changes)
-        lens.append(len(d.save()))
-    res = np.zeros(n, dtype=[("out_len", "<u8")])
-    res["out_len"] = lens
-    return [n, ops, 0, int(res["out_len"].sum()), shard.out_digest(res)], lens
+        out = d.save()
+        lens.append(len(out))
+        terms.append(shard.doc_digest(first + i, 0, out))
+    return [n, ops, 0, sum(lens), shard.combine(terms)], lens
 
 
 def _worker(rank, world, port, outdir):
@@ -72,3 +72,16 @@ def test_two_rank_gloo_digest_matches_single_process(tmp_path):
     single, _ = _merge_shard(0, world * DOCS_PER_RANK)
     assert got[0][:4] == single[:4]
     assert got[0][4] == single[4]
+
+
+def test_digest_detects_one_wrong_byte_and_equal_lengths():
+    """Documents of equal length do not cancel, and one changed output byte changes the digest."""
+    from automerge_amd import shard
+    outs = [bytes([0x85, 0x6F, 0x4A, 0x83, i, 7, 7, 7]) + bytes(20) for i in range(6)]
+    base = shard.combine(shard.doc_digest(i, 0, o) for i, o in enumerate(outs))
+    assert base != 0
+    bad = list(outs)
+    bad[3] = outs[3][:5] + b"\x08" + outs[3][6:]
+    assert shard.combine(shard.doc_digest(i, 0, o) for i, o in enumerate(bad)) != base
+    swapped = [outs[1], outs[0]] + outs[2:]  # same multiset, wrong owners
+    assert shard.combine(shard.doc_digest(i, 0, o) for i, o in enumerate(swapped)) != base

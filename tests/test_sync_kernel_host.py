@@ -104,3 +104,17 @@ def test_kernel_select_body_matches_oracle(harness):
                                          pfoff.ctypes.data, C.addressof(fbuf), foff.ctypes.data, C.addressof(send))
         assert st == 0
         assert list(send.raw[:n]) == ref, (trial, deps)
+
+
+def test_kernel_bloom_edge_vectors(harness):
+    """numProbes 0 still tests one bit (getProbes returns [x], sync.js:95-100); malformed headers
+    decode to the reference's RangeError kinds (tests/golden/bloom_edge.json)."""
+    kinds = {"subarray exceeds buffer size": 4, "buffer ended with incomplete number": 3, "number out of range": 2}
+    for v in golden("bloom_edge.json"):
+        f = bytes.fromhex(v["bytes"])
+        for i, h in enumerate(v["probes"]):
+            got = harness.amx_bloom_test(f, len(f), bytes.fromhex(h))
+            if v["error"]:
+                assert got == kinds[v["error"]["message"]], v
+            else:
+                assert got == int(v["contains"][i]), (v["bytes"], i)

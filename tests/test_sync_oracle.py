@@ -38,3 +38,16 @@ def test_select_transitive_dependents():
     assert O.sync_select(hashes, deps, [have2])[:3] == [1, 1, 1]
     # a change present in either filter is not sent
     assert O.sync_select(hashes, deps, [have, have2])[0] == 0 or O.bloom_contains(have, hashes[0]) == 0
+
+
+def test_bloom_edge_vectors_match_reference():
+    """numProbes 0/1/2/7, 0-3 bits per entry and malformed headers (tests/golden/bloom_edge.json,
+    made by the reference's BloomFilter): containsHash results and decode errors."""
+    for v in golden("bloom_edge.json"):
+        f = bytes.fromhex(v["bytes"])
+        for i, h in enumerate(v["probes"]):
+            got = O.bloom_contains(f, bytes.fromhex(h))
+            if v["error"]:
+                assert got == -1, v
+            else:
+                assert got == int(v["contains"][i]), (v["bytes"], i)
