@@ -62,6 +62,7 @@ _sigs = {
     "am_batch_stage_times": (C.c_int, [P, C.POINTER(C.c_float)]),
     "am_batch_workspace_bytes": (C.c_uint64, [P]),
     "am_batch_digest": (C.c_int, [P, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "am_batch_fast_flags": (C.c_int, [P, P]),
     "am_doc_init": (P, [P]),
     "am_doc_load": (P, [P, C.c_char_p, C.c_size_t, C.POINTER(Error)]),
     "am_doc_clone": (P, [P]),

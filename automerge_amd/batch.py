@@ -130,5 +130,12 @@ class Batch:
             raise N.AutomergeError("automerge_amd: digest failed")
         return int(out.value)
 
+    def fast_flags(self):
+        """Per document of the last run: True when k_doc_fast merged it."""
+        out = np.zeros(self.ndocs, np.uint8)
+        if self.ndocs and N.lib.am_batch_fast_flags(self._b, out.ctypes.data):
+            raise N.AutomergeError("automerge_amd: flag copy failed")
+        return out.astype(bool)
+
     def workspace_bytes(self):
         return N.lib.am_batch_workspace_bytes(self._b)

@@ -9,6 +9,7 @@
 #include <array>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -281,6 +282,9 @@ struct am_batch {
   DevBuf<ChunkInfo> info;
   DevBuf<DocBounds> bounds;
   DevBuf<uint64_t> ws_bytes, ws_off, scan_tmp, ws_total, max_hot;
+  DevBuf<uint8_t> fast_done;
+  uint32_t fast_lds = 0;
+  bool fast_only = false;
   uint32_t lds_bytes = 0;
   uint64_t max_hot_v = 0;
   DevBuf<uint8_t> ws;
@@ -294,6 +298,7 @@ struct am_batch {
     BatchDev b;
     b.arena = arena.p; b.chunks = chunks.p; b.docs = docs.p; b.known = known.p; b.info = info.p; b.bounds = bounds.p;
     b.ws_bytes = ws_bytes.p; b.ws_off = ws_off.p; b.scan_tmp = scan_tmp.p; b.ws_total = ws_total.p; b.max_hot = max_hot.p; b.lds_bytes = lds_bytes; b.max_hot_host = max_hot_v; b.ws = ws.p;
+    b.fast_lds = fast_lds; b.fast_done = fast_done.p; b.fast_only = fast_only;
     b.ws_cap = ws.cap; b.results = results.p; b.chg_state = chg_state.p; b.nchunks = nchunks; b.ndocs = ndocs;
     return b;
   }
@@ -353,9 +358,11 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   am_engine* e = b->eng;
   if (!set_device(e)) return false;
   hipStream_t s = e->stream;
-  if (!b->arena.ensure(arena_len) || !b->chunks.ensure(nchunks) || !b->docs.ensure(ndocs) || !b->known.ensure(nknown) ||
+  // 64 bytes of slack: k_doc_fast stages whole 16-byte words of a document's span
+  if (!b->arena.ensure(arena_len + 64) || !b->chunks.ensure(nchunks) || !b->docs.ensure(ndocs) || !b->known.ensure(nknown) ||
       !b->info.ensure(nchunks) || !b->bounds.ensure(ndocs) || !b->ws_bytes.ensure(ndocs) || !b->ws_off.ensure(ndocs) ||
-      !b->scan_tmp.ensure(am_scan_tmp_elems(ndocs)) || !b->ws_total.ensure(1) || !b->max_hot.ensure(1) || !b->results.ensure(ndocs) ||
+      !b->scan_tmp.ensure(am_scan_tmp_elems(ndocs)) || !b->ws_total.ensure(1) || !b->max_hot.ensure(2) ||
+      !b->fast_done.ensure(ndocs) || !b->results.ensure(ndocs) ||
       !b->chg_state.ensure(nchunks))
     return false;
   if (arena_len) HIPCHECK(hipMemcpyAsync(b->arena.p, arena, arena_len, hipMemcpyHostToDevice, s));
@@ -368,9 +375,10 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   BatchDev d = b->dev();
   am_launch_chunks(d, s);
   am_launch_bounds(d, s);
-  uint64_t total = 0, max_hot = 0;
+  uint64_t total = 0, max_hot = 0, max_fast = 0;
   if (ndocs) HIPCHECK(hipMemcpyAsync(&total, b->ws_total.p, sizeof total, hipMemcpyDeviceToHost, s));
   if (ndocs) HIPCHECK(hipMemcpyAsync(&max_hot, b->max_hot.p, sizeof max_hot, hipMemcpyDeviceToHost, s));
+  if (ndocs) HIPCHECK(hipMemcpyAsync(&max_fast, b->max_hot.p + 1, sizeof max_fast, hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
   HIPCHECK(hipGetLastError());
   b->ws_need = total;
@@ -379,6 +387,11 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   if (lds > AM_LDS_BUDGET) lds = AM_LDS_BUDGET;
   b->lds_bytes = (uint32_t)lds;
   b->max_hot_v = max_hot;
+  // k_doc_fast (am_doc_fast.h) for the documents in its envelope; AM_FAST=0 turns it off
+  const char* fe = std::getenv("AM_FAST");
+  const bool fast_on = !(fe && fe[0] == '0');
+  b->fast_lds = fast_on ? (uint32_t)((max_fast + 15) & ~(uint64_t)15) : 0u;
+  b->fast_only = false;
   if (!b->ws.ensure(total + 16)) return false;
   return true;
 }
@@ -513,6 +526,13 @@ extern "C" int am_batch_digest(am_batch* b, uint64_t first_doc, uint64_t* digest
   if (hipStreamSynchronize(s) != hipSuccess) return 1;
   *digest &= 0x7FFFFFFFFFFFFFFFull;
   return 0;
+}
+
+extern "C" int am_batch_fast_flags(am_batch* b, uint8_t* flags) {
+  if (!set_device(b->eng)) return 1;
+  if (!b->ndocs) return 0;
+  if (!b->fast_lds) { std::memset(flags, 0, b->ndocs); return 0; }
+  return hipMemcpy(flags, b->fast_done.p, b->ndocs, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
 
 extern "C" uint64_t am_batch_workspace_bytes(am_batch* b) { return b->ws_need; }

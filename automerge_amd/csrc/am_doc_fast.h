@@ -1,0 +1,1291 @@
+// am_doc_fast.h -- k_doc_fast: the merge of a small document with its op rows, changes, entries
+// and columns held one per lane (one wave per document, four documents per workgroup).
+//
+// This is the common case of Backend.load + Backend.applyChanges (backend/new.js:1550-1597,
+// 1695-1871): every change of the call applies in list order during the first pass of the
+// causal queue, and the document has at most 64 op rows, 64 pred/succ entries, 64 change rows,
+// 64 actor references and 64 dependencies. Anything else -- a change that waits in the queue, a
+// duplicate, any reference or range error, a value outside 31 bits, a getPatch request -- leaves
+// fast_done[doc] = 0 and the document is merged by k_doc (am_doc_impl.h), which reports the
+// reference's exact error. The sort keys are the ones k_doc sorts by (object, UTF-16 key |
+// RGA position, opId; succ order of new.js:1173-1188) and the encoders produce the canonical
+// RLE / delta / boolean forms of encoding.js:558-1207, so documents merged here are byte-for-byte
+// the documents k_doc (and the reference) produce. tests/test_gpu_parity.py runs every golden
+// scenario through both paths.
+//
+// Per document, everything lives in the wave's LDS slice and in registers:
+//   input   the document's chunk bytes (16-byte loads of [span_lo, span_hi))
+//   hashes  change hashes | base heads | host-known hashes, 32 B each (word compares)
+//   refs    actor references: base actors, then every change's actor list
+//   chg     parsed change headers
+//   misc    small per-document tables (DocHdr, ranks, sort results, succ lists)
+//   cells   decoded column values (4 B per value); reused as the output image afterwards
+#pragma once
+
+#define FD_MAX 64
+#define FD_SPAN_MAX 8192
+#define FD_LDS_CAP (24 * 1024)
+#define FD_DOCS_PER_WG 4
+#define FD_NULL ((int32_t)0x80000000)
+
+// misc region (byte offsets)
+enum : uint32_t {
+  FM_DH = 0,                      // DocHdr (240 B)
+  FM_BHIDX = 256,                 // int64 [64] base head -> changeIndexByHash index
+  FM_KIDX = FM_BHIDX + 512,       // int64 [64] known hash -> index
+  FM_IDT = FM_KIDX + 512,         // uint64 [64] sorted op ids (ctr << 12 | rank << 6 | row)
+  FM_NSORT = FM_IDT + 512,        // uint64 [64] sorted new succ entries
+  FM_BENT = FM_NSORT + 512,       // uint64 [64] base entries (ctr << 6 | rank)
+  FM_OUTC = FM_BENT + 512,        // int32 [64] output succ ctr
+  FM_SRCR = FM_OUTC + 256,        // int32 [64] row -> source marks
+  FM_SRCE = FM_SRCR + 256,        // int32 [64] entry -> source marks
+  FM_CNTN = FM_SRCE + 256,        // uint32 [64] new succs per target row
+  FM_CLOCK = FM_CNTN + 256,       // uint32 [64] base clock per doc actor
+  FM_FIRST = FM_CLOCK + 256,      // uint32 [64] first change authored by a canonical ref
+  FM_ROW0 = FM_FIRST + 256,       // uint32 [65] first row of each source
+  FM_ENT0 = FM_ROW0 + 272,        // uint32 [65] first entry of each source
+  FM_COLLEN = FM_ENT0 + 272,      // uint32 [32] encoded column lengths
+  FM_OWN = FM_COLLEN + 128,       // uint8 [64] owner row of each entry
+  FM_CANON = FM_OWN + 64,         // uint8 [64] canonical ref of each ref
+  FM_RANKC = FM_CANON + 64,       // uint8 [64] rank of each canonical ref
+  FM_DPC = FM_RANKC + 64,         // uint8 [64] doc actor index of each canonical ref
+  FM_DP2REF = FM_DPC + 64,        // uint8 [64] doc actor index -> ref
+  FM_RANKDP = FM_DP2REF + 64,     // uint8 [64] doc actor index -> rank
+  FM_OPR = FM_RANKDP + 64,        // uint8 [64] row -> opId rank
+  FM_FC = FM_OPR + 64,            // int8 [64] first child (RGA)
+  FM_NS = FM_FC + 64,             // int8 [64] next sibling (RGA)
+  FM_LON = FM_NS + 64,            // uint8 [64] first sorted new succ of each target row
+  FM_DEPD = FM_LON + 64,          // uint8 [128] hash candidate is depended on
+  FM_OUTA = FM_DEPD + 128,        // uint8 [64] output succ actor
+  FM_DOWN = FM_OUTA + 64,         // uint8 [64] owner change of each dep slot
+  FM_HOUT = FM_DOWN + 64,         // uint8 [64 * 32] sorted heads
+  FM_HIDX = FM_HOUT + 2048,       // int64 [64] sorted heads' indexes
+  FM_TOTAL = FM_HIDX + 512
+};
+
+struct FastLayout {
+  uint32_t input, hashes, refs, misc, chg, cells, cells_cap, total;
+};
+
+// Per-document LDS slice of k_doc_fast (bytes, 16-aligned regions).
+__host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t nknown) {
+  FastLayout F;
+  uint32_t o = 0;
+  auto take = [&](uint32_t n) { const uint32_t at = o; o += (n + 15) & ~15u; return at; };
+  const uint32_t span = (uint32_t)(b.span_hi - b.span_lo);
+  const uint32_t nbh = b.H - b.N, nrefs = (b.A - b.N) + b.AM;
+  F.input = take(span + 32);
+  F.hashes = take(32 * (b.N + nbh + nknown));
+  F.refs = take(40 * nrefs);  // 32 B padded id words + (off, len)
+  F.misc = take(FM_TOTAL);
+  F.chg = take((uint32_t)sizeof(ChgHdr) * b.N);
+  const uint32_t nbc = b.C - b.N, nbd = b.D - b.ND;
+  uint32_t cells = 4 * (13 * b.R + 2 * b.E);
+  const uint32_t dcc = 8 * (9 * nbc + nbd);
+  if (dcc > cells) cells = dcc;
+  // output image: header (actors, heads, column table) + columns + heads indexes + extra bytes
+  const uint32_t out = 64 + 40 * b.A + 42 * b.H + 25 * 12 + span + 1024;
+  if (out > cells) cells = out;
+  F.cells = take(cells);
+  F.cells_cap = cells;
+  F.total = o;
+  return F;
+}
+
+__host__ __device__ inline bool fast_eligible(const DocBounds& b, const am_doc_desc& dd) {
+  if (dd.flags & AM_DOC_WANT_PATCH) return false;
+  if (b.B == 0 || doc_scattered(b)) return false;
+  if (dd.base_chunk < 0 && dd.chg_count == 0) return false;
+  if (b.span_hi - b.span_lo > FD_SPAN_MAX) return false;
+  if (b.R > FD_MAX || b.E > FD_MAX || b.C > FD_MAX || b.N > FD_MAX || b.D > FD_MAX || b.ND > FD_MAX || b.H > FD_MAX)
+    return false;
+  if (dd.known_count > FD_MAX || b.N + (b.H - b.N) + dd.known_count > 2 * FD_MAX) return false;
+  if ((b.A - b.N) + b.AM > FD_MAX) return false;
+  return fast_layout(b, dd.known_count).total <= FD_LDS_CAP;
+}
+
+namespace fastdoc {
+using lds_mode::kOpColDec;
+using lds_mode::kEncKind;
+using lds_mode::EK_U;
+using lds_mode::EK_D;
+using lds_mode::EK_S;
+using lds_mode::EK_B;
+using lds_mode::EK_W;
+
+__device__ __forceinline__ uint32_t lane() { return threadIdx.x & 63; }
+// Orders this wave's LDS accesses (a wave's DS instructions execute in order; this stops the
+// compiler from moving them across a cross-lane hand-off)
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ uint64_t lt_mask() {
+  const uint32_t l = lane();
+  return l ? (~0ull >> (64 - l)) : 0ull;
+}
+__device__ __forceinline__ uint32_t ctz64(uint64_t m) { return m ? (uint32_t)__builtin_ctzll(m) : 64u; }
+__device__ __forceinline__ uint32_t excl_add(uint32_t v, uint32_t& total) {
+  const uint32_t l = lane();
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (l >= (uint32_t)d) x += y;
+  }
+  total = __shfl(x, 63, 64);
+  return x - v;
+}
+__device__ __forceinline__ int32_t incl_max(int32_t v) {
+  const uint32_t l = lane();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int32_t y = __shfl_up(v, d, 64);
+    if (l >= (uint32_t)d && y > v) v = y;
+  }
+  return v;
+}
+__device__ __forceinline__ int64_t max_all(int64_t v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    const int64_t y = __shfl_xor(v, d, 64);
+    v = y > v ? y : v;
+  }
+  return v;
+}
+__device__ __forceinline__ uint32_t sum_all(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+// ascending bitonic sort of one u64 per lane (padding lanes hold ~0)
+__device__ __forceinline__ uint64_t sort64(uint64_t v) {
+  const uint32_t l = lane();
+#pragma unroll
+  for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      const uint64_t p = __shfl_xor(v, (int)j, 64);
+      const bool up = (l & k) == 0, lo = (l & j) == 0;
+      const uint64_t mn = v < p ? v : p, mx = v < p ? p : v;
+      v = (lo == up) ? mn : mx;
+    }
+  }
+  return v;
+}
+__device__ __forceinline__ bool words_eq(const uint32_t* a, const uint32_t* b) {
+  const uint4 a0 = reinterpret_cast<const uint4*>(a)[0], a1 = reinterpret_cast<const uint4*>(a)[1];
+  const uint4 b0 = reinterpret_cast<const uint4*>(b)[0], b1 = reinterpret_cast<const uint4*>(b)[1];
+  return ((a0.x ^ b0.x) | (a0.y ^ b0.y) | (a0.z ^ b0.z) | (a0.w ^ b0.w) | (a1.x ^ b1.x) | (a1.y ^ b1.y) | (a1.z ^ b1.z) |
+          (a1.w ^ b1.w)) == 0;
+}
+// 32 input bytes -> 8 little-endian words (hash compares; LDS bytes, any alignment)
+__device__ __forceinline__ void load32(const uint8_t* p, uint32_t w[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    w[k] = (uint32_t)p[4 * k] | (uint32_t)p[4 * k + 1] << 8 | (uint32_t)p[4 * k + 2] << 16 | (uint32_t)p[4 * k + 3] << 24;
+}
+__device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+
+// Canonical column encoder over the values of lanes [0, n) (one value per lane, wave-parallel):
+// runs of equal adjacent values -> repetition / null / literal records (RLEEncoder,
+// encoding.js:558-783), deltas against the previous non-null value (DeltaEncoder :932-951),
+// alternating run counts (BooleanEncoder :1061-1135), concatenated raw bytes (valRaw). Writes
+// the column at `out` and returns its length, or ~0u when it would exceed `cap`.
+//   v: value (U / D / B), isnull; S: string bytes at in + soff (len slen), eqs = equal to the
+//   previous lane's string; W: raw bytes at in + soff (len slen).
+__device__ uint32_t enc_col(uint8_t kind, uint32_t n, int64_t v, bool isnull, uint32_t soff, uint32_t slen, bool eqs,
+                            const uint8_t* in, uint8_t* out, uint32_t cap) {
+  if (n == 0) return 0;
+  const uint32_t l = lane();
+  const bool act = l < n;
+  const bool nul = act && isnull && kind != EK_W && kind != EK_B;
+  if (kind == EK_D) {
+    const int32_t pi = incl_max(act && !nul ? (int32_t)l : -1);
+    int32_t prev = __shfl_up(pi, 1, 64);
+    if (l == 0) prev = -1;
+    const int64_t pv = __shfl(v, prev < 0 ? 0 : prev, 64);
+    if (act && !nul) v -= prev < 0 ? 0 : pv;
+  }
+  const int64_t pv = __shfl_up(v, 1, 64);
+  const int32_t pn = __shfl_up((int32_t)nul, 1, 64);
+  bool same = false;
+  if (act && l > 0 && kind != EK_W) {
+    if (nul) same = pn != 0;
+    else if (pn) same = false;
+    else same = (kind == EK_S) ? eqs : (pv == v);
+  }
+  const bool st = act && !same;
+  const uint64_t M = __ballot(st);
+  const uint64_t above = l == 63 ? 0ull : (M >> (l + 1));
+  const uint32_t rl = (above ? l + 1 + ctz64(above) : n) - l;
+  uint32_t bytes = 0, gcnt = 0;
+  bool gs = false;
+  if (kind == EK_W) {
+    bytes = act ? slen : 0;
+  } else if (kind == EK_B) {
+    bytes = st ? (uint32_t)uleb_len(rl) + ((l == 0 && v) ? 1u : 0u) : 0u;
+  } else {
+    if (!__any(act && !nul)) return 0;  // nulls only: nothing is written (RLEEncoder.finish)
+    const bool single = st && !nul && rl == 1;
+    const uint64_t SM = __ballot(single);
+    gs = single && !(l > 0 && ((SM >> (l - 1)) & 1));
+    gcnt = gs ? ctz64(~(SM >> l)) : 0;
+    uint32_t vs = 0;
+    if (kind == EK_U) vs = uleb_len((uint64_t)v);
+    else if (kind == EK_D) vs = sleb_len(v);
+    else vs = uleb_len(slen) + slen;
+    if (st) {
+      if (nul) bytes = 1 + uleb_len(rl);
+      else if (rl >= 2) bytes = sleb_len((int64_t)rl) + vs;
+      else bytes = vs + (gs ? (uint32_t)sleb_len(-(int64_t)gcnt) : 0u);
+    }
+  }
+  uint32_t total;
+  const uint32_t off = excl_add(bytes, total);
+  if (total > cap) return ~0u;
+  if (bytes) {
+    uint8_t* o = out + off;
+    if (kind == EK_W) {
+      for (uint32_t q = 0; q < slen; q++) o[q] = in[soff + q];
+    } else if (kind == EK_B) {
+      if (l == 0 && v) *o++ = 0;
+      put_uleb(o, rl);
+    } else if (nul) {
+      *o++ = 0;
+      put_uleb(o, rl);
+    } else {
+      if (rl >= 2) o = put_sleb(o, (int64_t)rl);
+      else if (gs) o = put_sleb(o, -(int64_t)gcnt);
+      if (kind == EK_U) put_uleb(o, (uint64_t)v);
+      else if (kind == EK_D) put_sleb(o, v);
+      else {
+        o = put_uleb(o, slen);
+        for (uint32_t q = 0; q < slen; q++) o[q] = in[soff + q];
+      }
+    }
+  }
+  return total;
+}
+
+}  // namespace fastdoc
+
+__global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
+    k_doc_fast(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks, const am_doc_desc* __restrict__ docs,
+               const am_known_hash* __restrict__ known, const ChunkInfo* __restrict__ info,
+               const DocBounds* __restrict__ bounds, const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base,
+               uint64_t ws_cap, uint32_t lds_per_doc, uint32_t ndocs, am_doc_result* __restrict__ results,
+               int32_t* __restrict__ chg_state, uint8_t* __restrict__ fast_done) {
+  using namespace fastdoc;
+  const uint32_t l = lane();
+  const uint32_t doc = blockIdx.x * FD_DOCS_PER_WG + (threadIdx.x >> 6);
+  if (doc >= ndocs) return;
+  const am_doc_desc dd = docs[doc];
+  const DocBounds b = bounds[doc];
+  if (!fast_eligible(b, dd)) return;
+  const FastLayout F = fast_layout(b, dd.known_count);
+  if (F.total > lds_per_doc) return;
+  const WsLayout L = ws_layout(b);
+  const uint64_t wso = ws_off[doc];
+  if (wso + L.total > ws_cap) return;  // capacity error: reported by k_doc
+  uint8_t* const wsg = ws_base + wso;
+  uint8_t* const S = am_lds + (threadIdx.x >> 6) * lds_per_doc;
+  uint8_t* const M = S + F.misc;
+  const bool has_base = dd.base_chunk >= 0;
+  const uint32_t N = dd.chg_count;
+  bool bad = false;
+#define FD_CHECK()          \
+  do {                      \
+    if (__any(bad)) return; \
+  } while (0)
+
+  // ---- chunk status (k_chunks) and per-change counts ----
+  uint32_t c_nops = 0, c_nents = 0, c_ndeps = 0, c_nact = 0;
+  if (l < N) {
+    const ChunkInfo& ci = info[dd.chg_begin + l];
+    bad |= ci.status != AM_OK || ci.type != 1;
+    c_nops = ci.nops; c_nents = ci.nents; c_ndeps = ci.ndeps; c_nact = ci.nactors;
+  }
+  uint32_t nb = 0, nbe = 0, nbc = 0, nbd = 0;
+  uint64_t base_data = 0;
+  uint32_t base_len = 0;
+  if (has_base) {
+    const ChunkInfo& ci = info[dd.base_chunk];
+    bad |= ci.status != AM_OK || ci.type != 0;
+    nb = ci.nops; nbe = ci.nents; nbc = ci.nchg; nbd = ci.ndeps;
+    base_data = chunks[dd.base_chunk].off + ci.data_off;
+    base_len = ci.data_len;
+  }
+  FD_CHECK();
+
+  // ---- stage the input span (16-byte loads) ----
+  const uint64_t a0 = b.span_lo & ~15ull;
+  {
+    const uint32_t nv = (uint32_t)((b.span_hi - a0 + 15) / 16);
+    uint4* dst = reinterpret_cast<uint4*>(S + F.input);
+    const uint4* src = reinterpret_cast<const uint4*>(arena + a0);
+    for (uint32_t v = l; v < nv; v += 64) dst[v] = src[v];
+  }
+  const uint8_t* const IN = S + F.input;  // IN[off - a0] = arena[off]
+  wsync();
+
+  // ---- headers: the base document (lane 0) and one change per lane ----
+  DocHdr* dh = reinterpret_cast<DocHdr*>(M + FM_DH);
+  ChgHdr* chh = reinterpret_cast<ChgHdr*>(S + F.chg);
+  if (l == 0) {
+    if (has_base) bad |= parse_doc_hdr(IN + (base_data - a0), base_len, base_data, *dh) != AM_OK;
+    else { dh->nactors = 0; dh->nheads = 0; dh->has_hidx = 0; dh->extra_len = 0; dh->base = 0; }
+  }
+  if (l < N) {
+    const uint64_t cdat = chunks[dd.chg_begin + l].off + info[dd.chg_begin + l].data_off;
+    bad |= parse_change_hdr(IN + (cdat - a0), info[dd.chg_begin + l].data_len, cdat, chh[l]) != AM_OK;
+  }
+  wsync();
+  FD_CHECK();
+  const uint32_t NB = dh->nactors, HB = dh->nheads, K = dd.known_count;
+  bad |= NB + N != b.A || HB + N != b.H;
+  FD_CHECK();
+  // base heads' changeIndexByHash indexes (new.js:1729-1739); -1 = unknown
+  if (l == 0) {
+    int64_t* bh = reinterpret_cast<int64_t*>(M + FM_BHIDX);
+    if (dh->has_hidx) {
+      Rd r{IN + (dh->base + dh->hidx_off - a0), (uint64_t)1 << 40, 0};
+      for (uint32_t h = 0; h < HB; h++) {
+        int64_t v = -1;
+        rd_u53(r, v);
+        bh[h] = v;
+      }
+    } else {
+      for (uint32_t h = 0; h < HB; h++) bh[h] = HB == 1 ? (int64_t)nbc - 1 : -1;
+    }
+  }
+
+  // ---- hash table: changes [0, N) | base heads [N, N+HB) | known [N+HB, N+HB+K) ----
+  uint32_t* HT = reinterpret_cast<uint32_t*>(S + F.hashes);
+  if (l < N) {
+    const uint4* h = reinterpret_cast<const uint4*>(info[dd.chg_begin + l].hash);
+    reinterpret_cast<uint4*>(HT + 8 * l)[0] = h[0];
+    reinterpret_cast<uint4*>(HT + 8 * l)[1] = h[1];
+  }
+  if (l < HB) {
+    uint32_t w[8];
+    load32(IN + (dh->base + dh->heads_off + 32 * l - a0), w);
+#pragma unroll
+    for (int k = 0; k < 8; k++) HT[8 * (N + l) + k] = w[k];
+  }
+  if (l < K) {
+    const am_known_hash& kh = known[dd.known_begin + l];
+    uint32_t w[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint8_t* p = kh.hash + 4 * k;
+      w[k] = (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) HT[8 * (N + HB + l) + k] = w[k];
+    reinterpret_cast<int64_t*>(M + FM_KIDX)[l] = kh.index;
+  }
+
+  // ---- actor references: base actors [0, NB), then each change's actor list ----
+  uint32_t am_total;
+  const uint32_t ambase = excl_add(l < N ? c_nact : 0u, am_total);
+  const uint32_t NR = NB + am_total;
+  bad |= NR > FD_MAX;
+  FD_CHECK();
+  uint32_t* RW = reinterpret_cast<uint32_t*>(S + F.refs);               // 8 words per ref
+  uint32_t* RO = reinterpret_cast<uint32_t*>(S + F.refs + 32 * NR);     // (off - a0, len) per ref
+  if (l == 0 && has_base) {
+    Rd r{IN + (dh->base + dh->actors_off - a0), (uint64_t)1 << 40, 0};
+    for (uint32_t i = 0; i < NB; i++) {
+      int64_t len = 0;
+      bad |= rd_u53(r, len) != AM_OK;
+      RO[2 * i] = (uint32_t)(dh->base + dh->actors_off + r.off - a0);
+      RO[2 * i + 1] = (uint32_t)len;
+      r.off += (uint64_t)len;
+    }
+  }
+  if (l < N) {
+    const ChgHdr& h = chh[l];
+    const uint32_t r0 = NB + ambase;
+    RO[2 * r0] = (uint32_t)(h.base + h.actor_off - a0);
+    RO[2 * r0 + 1] = h.actor_len;
+    Rd r{IN + (h.base + h.actors_off - a0), (uint64_t)1 << 40, 0};
+    for (uint32_t k = 1; k < c_nact; k++) {
+      int64_t len = 0;
+      bad |= rd_u53(r, len) != AM_OK;
+      RO[2 * (r0 + k)] = (uint32_t)(h.base + h.actors_off + r.off - a0);
+      RO[2 * (r0 + k) + 1] = (uint32_t)len;
+      r.off += (uint64_t)len;
+    }
+  }
+  wsync();
+  FD_CHECK();
+  // padded big-endian words of each ref (ids up to 32 bytes)
+  uint32_t r_len = 0;
+  if (l < NR) {
+    const uint32_t off = RO[2 * l];
+    r_len = RO[2 * l + 1];
+    bad |= r_len > 32;
+    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t q = 0; q < r_len && q < 32; q++) w[q >> 2] |= (uint32_t)IN[off + q] << (24 - 8 * (q & 3));
+#pragma unroll
+    for (int k = 0; k < 8; k++) RW[8 * l + k] = w[k];
+  }
+  wsync();
+  FD_CHECK();
+  // canonical ref (first equal id) and rank of the canonical ids (hex order = bytewise, shorter
+  // prefix first: actor_cmp_dev)
+  uint8_t* CANON = M + FM_CANON;
+  {
+    uint32_t canon = l;
+    if (l < NR) {
+      for (uint32_t j = 0; j < NR; j++) {
+        if (j >= l) break;
+        if (RO[2 * j + 1] == r_len && words_eq(RW + 8 * j, RW + 8 * l)) { canon = j; break; }
+      }
+      CANON[l] = (uint8_t)canon;
+    }
+    wsync();
+    uint32_t rank = 0;
+    if (l < NR && canon == l) {
+      for (uint32_t j = 0; j < NR; j++) {
+        if (CANON[j] != j || j == l) continue;
+        int c = 0;
+        for (int k = 0; k < 8 && c == 0; k++) {
+          const uint32_t a = RW[8 * j + k], bb = RW[8 * l + k];
+          c = a < bb ? -1 : (a > bb ? 1 : 0);
+        }
+        if (c == 0) c = RO[2 * j + 1] < r_len ? -1 : 1;
+        if (c < 0) rank++;
+      }
+      M[FM_RANKC + l] = (uint8_t)rank;
+    }
+  }
+  // doc actor table: base actors, then new authors in application order (getActorTable,
+  // new.js:1434-1451); every other actor of a change must already be in the table
+  uint32_t* FIRST = reinterpret_cast<uint32_t*>(M + FM_FIRST);
+  FIRST[l] = 0xffffffffu;
+  wsync();
+  uint32_t a_canon = 0;  // canonical ref of change l's author
+  if (l < NB) bad |= CANON[l] != l;  // repeated base actor ids: k_doc decides
+  if (l < N) {
+    a_canon = CANON[NB + ambase];
+    if (a_canon >= NB) atomicMin(&FIRST[a_canon], l);
+  }
+  wsync();
+  const bool newauth = l < N && a_canon >= NB && FIRST[a_canon] == l;
+  const uint64_t nam = __ballot(newauth);
+  const uint32_t NA = NB + __popcll(nam);
+  if (l < NB) { M[FM_DPC + l] = (uint8_t)l; M[FM_DP2REF + l] = (uint8_t)l; }
+  if (newauth) {
+    const uint32_t dp = NB + __popcll(nam & lt_mask());
+    M[FM_DPC + a_canon] = (uint8_t)dp;
+    M[FM_DP2REF + dp] = (uint8_t)(NB + ambase);
+  }
+  wsync();
+  uint32_t a_dp = 0;  // doc actor index of change l's author
+  if (l < N) {
+    a_dp = a_canon < NB ? a_canon : M[FM_DPC + a_canon];
+    for (uint32_t k = 1; k < c_nact; k++) {
+      const uint32_t cr = CANON[NB + ambase + k];
+      if (cr >= NB && !(FIRST[cr] <= l)) bad = true;  // actorId ... is not known to document
+    }
+  }
+  if (l < NA) M[FM_RANKDP + l] = M[FM_RANKC + CANON[M[FM_DP2REF + l]]];
+  wsync();
+  FD_CHECK();
+  const uint8_t* DPC = M + FM_DPC;
+  const uint8_t* RANKDP = M + FM_RANKDP;
+
+  // ---- base document change rows (DOCUMENT_COLUMNS, lane per column), then lane per row ----
+  int64_t* DCC = reinterpret_cast<int64_t*>(S + F.cells);  // [9][nbc] (+ deps at [9*nbc])
+  if (has_base && l < DC_NCOLS) {
+    const uint32_t col = l;
+    const uint64_t off = dh->base + dh->ccol_off[col];
+    const uint32_t len = dh->ccol_len[col];
+    ColDec d;
+    const uint8_t type = (col == DC_ACTOR || col == DC_DEPS_NUM || col == DC_EXTRA_LEN) ? DT_UINT
+                         : col == DC_MESSAGE                                          ? DT_UTF8
+                                                                                      : DT_INT;
+    cd_init(d, type, IN + (off - a0), len);
+    const uint32_t n = col == DC_DEPS_INDEX ? nbd : (col == DC_EXTRA_RAW ? 0u : nbc);
+    int64_t* dst = col == DC_DEPS_INDEX ? DCC + 9 * nbc : DCC + col * nbc;
+    for (uint32_t i = 0; i < n; i++) {
+      int64_t v = 0;
+      uint32_t e;
+      if (type == DT_UTF8) {
+        uint64_t so;
+        uint32_t sl;
+        e = cd_next_str(d, so, sl);
+        v = sl == AM_NOSTR ? AM_NULL64 : (int64_t)(((off + so - a0) << 32) | sl);
+        if (!e && sl != AM_NOSTR && !utf8_valid_dev(IN + (off + so - a0), sl)) bad = true;
+      } else if (col == DC_SEQ || col == DC_MAXOP || col == DC_TIME || col == DC_DEPS_INDEX) {
+        e = cd_next_delta(d, v);
+      } else {
+        e = cd_next_int(d, v);
+      }
+      if (e) { bad = true; break; }
+      dst[i] = v;
+    }
+  }
+  wsync();
+  FD_CHECK();
+  // base change row l: actor, seq, maxOp, time, message, deps, extra (readDocumentChanges)
+  int64_t bc_seq = 0, bc_max = 0, bc_time = 0, bc_msg = AM_NULL64, bc_xlen = 7;
+  uint32_t bc_actor = 0, bc_nd = 0, bc_xoff = 0, bc_xraw = 0;
+  const int64_t bc_dep = l < nbd ? DCC[9 * nbc + l] : 0;  // base depsIndex value l (cells are reused below)
+  {
+    int64_t a = 0;
+    if (l < nbc) {
+      a = DCC[DC_ACTOR * nbc + l];
+      bc_seq = DCC[DC_SEQ * nbc + l];
+      bc_max = DCC[DC_MAXOP * nbc + l];
+      bc_time = DCC[DC_TIME * nbc + l];
+      bc_msg = DCC[DC_MESSAGE * nbc + l];
+      const int64_t nd = DCC[DC_DEPS_NUM * nbc + l];
+      bc_nd = nd == AM_NULL64 ? 0u : (uint32_t)nd;
+      bc_xlen = DCC[DC_EXTRA_LEN * nbc + l];
+      bc_xraw = bc_xlen == AM_NULL64 ? 0u : (uint32_t)((uint64_t)bc_xlen >> 4);
+      bad |= a == AM_NULL64 || a < 0 || a >= (int64_t)NB || bc_seq == AM_NULL64 || nd > 64;
+      bc_actor = (uint32_t)a;
+    }
+    uint32_t xt, dt;
+    const uint32_t xo = excl_add(l < nbc ? bc_xraw : 0u, xt);
+    excl_add(l < nbc ? bc_nd : 0u, dt);
+    if (has_base) bad |= xt > dh->ccol_len[DC_EXTRA_RAW] || dt != nbd;
+    bc_xoff = (uint32_t)(dh->base + dh->ccol_off[DC_EXTRA_RAW] + xo - a0);
+    // clock: seq must count 1, 2, ... per actor in row order (new.js:1654-1660)
+    uint32_t before = 0;
+    for (uint32_t j = 0; j < nbc; j++) {
+      const uint32_t aj = __shfl(bc_actor, j, 64);
+      if (j < l && aj == bc_actor) before++;
+    }
+    uint32_t* CLK = reinterpret_cast<uint32_t*>(M + FM_CLOCK);
+    CLK[l] = 0;
+    wsync();
+    if (l < nbc) {
+      bad |= bc_seq != (int64_t)before + 1;
+      atomicMax(&CLK[bc_actor], (uint32_t)bc_seq);
+    }
+  }
+  wsync();
+  FD_CHECK();
+
+  // ---- causal queue, first pass (applyChanges, new.js:1550-1597): every change must be new,
+  // ready in list order and carry the next seq of its author ----
+  uint32_t prior = 0;  // earlier changes of this call by the same author
+  for (uint32_t j = 0; j < N; j++) prior += (__shfl(a_dp, j, 64) == a_dp && j < l) ? 1u : 0u;
+  if (l < N) {
+    uint32_t mine[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) mine[k] = HT[8 * l + k];
+    for (uint32_t t = 0; t < N + HB + K; t++) {
+      if (t == l || (t < N && t > l)) continue;
+      if (words_eq(HT + 8 * t, mine)) { bad = true; break; }  // duplicate / already applied
+    }
+    const uint32_t* CLK = reinterpret_cast<const uint32_t*>(M + FM_CLOCK);
+    const int64_t expect = (int64_t)(a_dp < NB ? CLK[a_dp] : 0u) + prior + 1;
+    bad |= chh[l].seq != expect;
+  }
+  uint32_t nd_total;
+  const uint32_t dbase = excl_add(l < N ? c_ndeps : 0u, nd_total);
+  bad |= nd_total != b.ND;
+  uint8_t* DEPD = M + FM_DEPD;
+  DEPD[l] = 0;
+  DEPD[64 + l] = 0;
+  if (l < N)
+    for (uint32_t k = 0; k < c_ndeps; k++) M[FM_DOWN + dbase + k] = (uint8_t)l;
+  wsync();
+  FD_CHECK();
+  // dependency q: a base head, a host-known change or an earlier change of this call
+  int64_t dep_idx = 0;
+  const uint32_t dep_c = l < nd_total ? M[FM_DOWN + l] : 0u;
+  const uint32_t dep_b = __shfl(dbase, dep_c, 64);
+  if (l < nd_total) {
+    const uint32_t c = dep_c;
+    const ChgHdr& h = chh[c];
+    uint32_t w[8];
+    load32(IN + (h.base + h.deps_off + 32 * (l - dep_b) - a0), w);
+    int32_t hit = -1;
+    for (uint32_t t = N; t < N + HB + K && hit < 0; t++)
+      if (words_eq(HT + 8 * t, w)) hit = (int32_t)t;
+    if (hit >= 0) {
+      dep_idx = hit < (int32_t)(N + HB) ? reinterpret_cast<const int64_t*>(M + FM_BHIDX)[hit - N]
+                                        : reinterpret_cast<const int64_t*>(M + FM_KIDX)[hit - N - HB];
+      if (dep_idx < 0) bad = true;
+    } else {
+      for (uint32_t t = 0; t < N && hit < 0; t++)
+        if (words_eq(HT + 8 * t, w)) hit = (int32_t)t;
+      if (hit < 0 || (uint32_t)hit >= c) bad = true;  // missing or later: the change would wait
+      dep_idx = (int64_t)nbc + hit;
+    }
+    if (hit >= 0 && hit < (int32_t)(N + HB)) DEPD[hit] = 1;
+  }
+  wsync();
+  FD_CHECK();
+  // heads: base heads and changes that nothing in this call depends on, sorted (new.js:1581-1593)
+  uint32_t NH;
+  {
+    const uint32_t ncand = N + HB;
+    const bool ishead = l < ncand && !DEPD[l];
+    const uint64_t pre = l < ncand ? bswap64(((uint64_t)HT[8 * l + 1] << 32) | HT[8 * l]) : 0;
+    uint32_t pos = 0;
+    for (uint32_t y = 0; y < ncand; y++) {
+      const uint64_t py = __shfl(pre, y, 64);
+      const int32_t hy = __shfl((int32_t)ishead, y, 64);
+      if (hy && y != l) {
+        if (py < pre) pos++;
+        else if (py == pre) bad = true;  // equal 8-byte prefixes: k_doc sorts full hashes
+      }
+    }
+    NH = __popcll(__ballot(ishead));
+    if (ishead) {
+      const int64_t hidx = l < N ? (int64_t)nbc + l : reinterpret_cast<const int64_t*>(M + FM_BHIDX)[l - N];
+      bad |= hidx < 0;
+      reinterpret_cast<int64_t*>(M + FM_HIDX)[pos] = hidx;
+      uint4* ho = reinterpret_cast<uint4*>(M + FM_HOUT + 32 * pos);
+      ho[0] = reinterpret_cast<const uint4*>(HT + 8 * l)[0];
+      ho[1] = reinterpret_cast<const uint4*>(HT + 8 * l)[1];
+      uint4* hg = reinterpret_cast<uint4*>(wsg + L.heads + 32 * pos);
+      hg[0] = reinterpret_cast<const uint4*>(HT + 8 * l)[0];
+      hg[1] = reinterpret_cast<const uint4*>(HT + 8 * l)[1];
+    }
+  }
+  FD_CHECK();
+
+  // ---- op columns: lane per (source, column) stream into 4-byte cells (readOperation,
+  // new.js:570-611) ----
+  const uint32_t nsrc = (has_base ? 1u : 0u) + N;
+  const uint32_t R = b.R, E = b.E;
+  // source s: rows [row0, row0 + nr), entries [ent0, ent0 + ne)
+  uint32_t s_nr = 0, s_ne = 0;
+  {
+    // lane s holds source s's counts
+    const uint32_t c = has_base ? l - 1 : l;
+    const uint32_t cnops = __shfl(c_nops, c & 63, 64), cnents = __shfl(c_nents, c & 63, 64);
+    if (l < nsrc) {
+      if (has_base && l == 0) { s_nr = nb; s_ne = nbe; }
+      else { s_nr = cnops; s_ne = cnents; }
+    }
+  }
+  uint32_t rtot, etot;
+  const uint32_t s_row0 = excl_add(s_nr, rtot), s_ent0 = excl_add(s_ne, etot);
+  bad |= rtot != R || etot != E || (l < nsrc && s_nr == 0 && s_ne != 0);
+  uint32_t* ROW0 = reinterpret_cast<uint32_t*>(M + FM_ROW0);
+  uint32_t* ENT0 = reinterpret_cast<uint32_t*>(M + FM_ENT0);
+  ROW0[l] = s_row0;
+  ENT0[l] = s_ent0;
+  if (l == 0) { ROW0[64] = rtot; ENT0[64] = etot; }
+  int32_t* SRCR = reinterpret_cast<int32_t*>(M + FM_SRCR);
+  int32_t* SRCE = reinterpret_cast<int32_t*>(M + FM_SRCE);
+  SRCR[l] = -1;
+  SRCE[l] = -1;
+  wsync();
+  if (l < nsrc && s_nr) SRCR[s_row0] = (int32_t)l;
+  if (l < nsrc && s_ne) SRCE[s_ent0] = (int32_t)l;
+  FD_CHECK();
+  int32_t* CELL = reinterpret_cast<int32_t*>(S + F.cells);
+  for (uint32_t it = l; it < nsrc * 15; it += 64) {
+    const uint32_t s = it / 15, j = it % 15;
+    const uint32_t col = j < OC_VAL_RAW ? j : j + 1;
+    const bool chg_src = !(has_base && s == 0);
+    if (chg_src && (col == OC_ID_ACTOR || col == OC_ID_CTR)) continue;  // ids from the header
+    const uint32_t c = has_base ? s - 1 : s;
+    const uint64_t cbase = chg_src ? chh[c].base : dh->base;
+    const uint32_t coff = chg_src ? chh[c].col_off[col] : dh->ocol_off[col];
+    const uint32_t clen = chg_src ? chh[c].col_len[col] : dh->ocol_len[col];
+    const uint32_t r0 = ROW0[s], e0 = ENT0[s];
+    const uint32_t n = j < 13 ? ROW0[s + 1] - r0 : ENT0[s + 1] - e0;
+    int32_t* dst = j < 13 ? CELL + j * R + r0 : CELL + 13 * R + (j - 13) * E + e0;
+    const uint8_t type = kOpColDec[col];
+    ColDec d;
+    cd_init(d, type, IN + (cbase + coff - a0), clen);
+    for (uint32_t i = 0; i < n; i++) {
+      int32_t cv;
+      uint32_t e;
+      if (type == DT_BOOL) {
+        bool bv;
+        e = cd_next_bool(d, bv);
+        cv = bv ? 1 : 0;
+      } else {
+        bool isnull;
+        uint32_t sl;
+        int64_t x;
+        e = cd_next(d, x, isnull, sl);
+        if (isnull) cv = FD_NULL;
+        else if (type == DT_UTF8) {
+          const uint64_t so = cbase + coff + (uint64_t)x - a0;
+          if (sl > 255) bad = true;
+          cv = (int32_t)((so << 8) | (sl & 255));
+        } else {
+          if (type == DT_DELTA) x = (d.absolute += x);
+          if (x <= -0x7fffffffLL || x > 0x7fffffffLL) bad = true;
+          cv = (int32_t)x;
+        }
+      }
+      if (e) { bad = true; break; }
+      dst[i] = cv;
+    }
+  }
+  wsync();
+  FD_CHECK();
+
+  // ---- rows: lane per op row (gather_row) ----
+  const int32_t r_src = incl_max(l < R ? SRCR[l] : -1);
+  const bool isrow = l < R;
+  const bool r_chg = isrow && !(has_base && r_src == 0);
+  const uint32_t r_c = has_base ? (uint32_t)r_src - 1 : (uint32_t)r_src;  // change index of a change row
+  const uint32_t r_q = isrow ? l - ROW0[r_src] : 0;
+  // actor index of a change row maps through its change's actor list
+  const uint32_t cnact = __shfl(c_nact, r_c & 63, 64), cab = __shfl(ambase, r_c & 63, 64);
+  const int64_t cstart = r_chg ? chh[r_c].start_op : 0;
+  const int32_t c_adp = (int32_t)__shfl(a_dp, r_c & 63, 64);
+  auto mapact = [&](int32_t v) -> int32_t {
+    if (v == FD_NULL) return -1;
+    if (r_chg) {
+      if (v < 0 || (uint32_t)v >= cnact) { bad = true; return 0; }
+      return DPC[CANON[NB + cab + v]];
+    }
+    if (v < 0 || (uint32_t)v >= NB) { bad = true; return 0; }
+    return v;
+  };
+  int32_t r_objc = FD_NULL, r_obja = -1, r_keyc = FD_NULL, r_keya = -1, r_key = FD_NULL, r_idc = 0, r_ida = 0;
+  int32_t r_act = 0, r_vlen = FD_NULL, r_chc = FD_NULL, r_cha = -1, r_pcnt = 0;
+  bool r_ins = false;
+  if (isrow) {
+    const int32_t* c = CELL + l;
+    r_obja = mapact(c[0]);
+    r_objc = c[R];
+    r_keya = mapact(c[2 * R]);
+    r_keyc = c[3 * R];
+    r_key = c[4 * R];
+    if (r_chg) { r_ida = c_adp; const int64_t x = cstart + r_q; bad |= x > 0x7fffffffLL; r_idc = (int32_t)x; }
+    else { r_ida = mapact(c[5 * R]); r_idc = c[6 * R]; bad |= c[5 * R] == FD_NULL || r_idc == FD_NULL; }
+    r_ins = c[7 * R] != 0;
+    r_act = c[8 * R];
+    r_vlen = c[9 * R];
+    r_cha = mapact(c[10 * R]);
+    r_chc = c[11 * R];
+    r_pcnt = c[12 * R] == FD_NULL ? 0 : c[12 * R];
+    bad |= r_act == FD_NULL || r_pcnt < 0 || (r_vlen != FD_NULL && r_vlen < 0);
+    if (r_key != FD_NULL && !utf8_valid_dev(IN + ((uint32_t)r_key >> 8), (uint32_t)r_key & 255)) bad = true;
+  }
+  const bool r_del = r_chg && r_act == 3;
+  const uint32_t r_vb = (isrow && r_vlen != FD_NULL) ? ((uint32_t)r_vlen >> 4) : 0u;
+  uint32_t vtot, ptot;
+  const uint32_t vsum = excl_add(r_vb, vtot);
+  const uint32_t r_psoff = excl_add(isrow ? (uint32_t)r_pcnt : 0u, ptot);
+  const uint32_t r_row0 = isrow ? ROW0[r_src] : 0;
+  const uint32_t vsum0 = __shfl(vsum, r_row0 & 63, 64), psum0 = __shfl(r_psoff, r_row0 & 63, 64);
+  uint32_t r_voff = 0;  // valRaw bytes of the row, relative to a0
+  if (isrow) {
+    const uint64_t cbase = r_chg ? chh[r_c].base : dh->base;
+    const uint32_t coff = r_chg ? chh[r_c].col_off[OC_VAL_RAW] : dh->ocol_off[OC_VAL_RAW];
+    const uint32_t clen = r_chg ? chh[r_c].col_len[OC_VAL_RAW] : dh->ocol_len[OC_VAL_RAW];
+    r_voff = (uint32_t)(cbase + coff - a0) + (vsum - vsum0);
+    if (l + 1 == ROW0[r_src + 1] || l + 1 == R) {  // last row of its source
+      bad |= (vsum - vsum0) + r_vb > clen;
+      bad |= r_psoff + (uint32_t)r_pcnt - psum0 != ENT0[r_src + 1] - ENT0[r_src];
+    }
+  }
+  bad |= ptot != E;
+  // entries: lane per pred/succ entry
+  const int32_t e_src = incl_max(l < E ? SRCE[l] : -1);
+  const bool isent = l < E;
+  const bool e_chg = isent && !(has_base && e_src == 0);
+  int32_t e_ctr = 0, e_act = 0;
+  {
+    const uint32_t ec = has_base ? (uint32_t)e_src - 1 : (uint32_t)e_src;
+    const uint32_t enact = __shfl(c_nact, ec & 63, 64), eab = __shfl(ambase, ec & 63, 64);
+    if (isent) {
+      const int32_t a = CELL[13 * R + l], ctr = CELL[13 * R + E + l];
+      if (a == FD_NULL || ctr == FD_NULL) bad = true;
+      else if (e_chg) {
+        if (a < 0 || (uint32_t)a >= enact) bad = true;
+        else e_act = DPC[CANON[NB + eab + a]];
+      } else {
+        if (a < 0 || (uint32_t)a >= NB) bad = true;
+        else e_act = a;
+      }
+      e_ctr = ctr;
+    }
+  }
+  // maxOp: base op ids and succ counters, applied changes' last op (new.js:1627-1630, 1749)
+  int64_t maxop = 0;
+  if (isrow && !r_chg) maxop = r_idc;
+  if (isent && !e_chg && e_ctr > maxop) maxop = e_ctr;
+  if (l < N && c_nops > 0) {
+    const int64_t m = chh[l].start_op + (int64_t)c_nops - 1;
+    if (m > maxop) maxop = m;
+  }
+  maxop = max_all(maxop);
+  // per-op checks of change rows (readNextChangeOp new.js:715-723, mergeDocChangeOps shapes)
+  if (r_chg) {
+    bad |= (r_objc == FD_NULL) != (r_obja < 0);
+    bad |= (r_keyc == FD_NULL && r_keya >= 0) || (r_keyc == 0 && r_keya >= 0) || (r_keyc != FD_NULL && r_keyc > 0 && r_keya < 0);
+    bad |= r_del && (r_ins || r_pcnt == 0);
+    bad |= r_ins && r_pcnt > 0;
+    bad |= r_key == FD_NULL && !r_ins && r_keyc == FD_NULL;
+  }
+  if (isrow) bad |= r_idc < 0 || (r_objc != FD_NULL && r_objc < 0);
+  FD_CHECK();
+
+  // ---- opId order: (counter, actor rank) (new.js:1197-1224) ----
+  const uint32_t r_rank = isrow ? RANKDP[r_ida] : 0;
+  uint64_t* IDT = reinterpret_cast<uint64_t*>(M + FM_IDT);
+  uint32_t r_opr;
+  {
+    const uint64_t key = isrow ? ((uint64_t)(uint32_t)r_idc << 12) | (r_rank << 6) | l : ~0ull;
+    const uint64_t s = sort64(key);
+    const uint64_t prev = __shfl_up(s, 1, 64);
+    if (l > 0 && l < R && (prev >> 6) == (s >> 6)) bad = true;  // duplicate operation ID
+    IDT[l] = s;
+    if (l < R) M[FM_OPR + (s & 63)] = (uint8_t)l;
+    wsync();
+    r_opr = M[FM_OPR + l];
+  }
+  FD_CHECK();
+  auto lookup = [&](int32_t ctr, uint32_t rank) -> int32_t {
+    if (ctr < 0) return -1;
+    const uint64_t want = ((uint64_t)(uint32_t)ctr << 6) | rank;
+    uint32_t lo = 0, hi = R;
+    while (lo < hi) {
+      const uint32_t m = (lo + hi) >> 1;
+      if ((IDT[m] >> 6) < want) lo = m + 1; else hi = m;
+    }
+    return (lo < R && (IDT[lo] >> 6) == want) ? (int32_t)(IDT[lo] & 63) : -1;
+  };
+
+  // ---- map keys: rank in UTF-16 order. Keys whose bytes stay below 0xEE compare in UTF-16
+  // order exactly as bytes (only supplementary characters reorder against U+E000..U+FFFF) ----
+  const bool keyed = isrow && r_key != FD_NULL;
+  uint32_t r_krank = 0;
+  {
+    const uint32_t koff = keyed ? ((uint32_t)r_key >> 8) : 0, klen = keyed ? ((uint32_t)r_key & 255) : 0;
+    uint64_t pre = 0;
+    for (uint32_t q = 0; q < klen; q++) {
+      const uint8_t c = IN[koff + q];
+      if (c >= 0xee) bad = true;
+      if (q < 8) pre |= (uint64_t)c << (56 - 8 * q);
+    }
+    uint64_t km = __ballot(keyed);
+    while (km) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(km);
+      km &= km - 1;
+      const uint64_t pj = __shfl(pre, j, 64);
+      const uint32_t kj = (uint32_t)__shfl(r_key, j, 64);
+      if (!keyed || j == l) continue;
+      bool less = pj < pre;
+      if (pj == pre) {
+        const uint32_t jo = kj >> 8, jl = kj & 255;
+        uint32_t q = 8;
+        while (q < jl && q < klen && IN[jo + q] == IN[koff + q]) q++;
+        less = (q < jl && q < klen) ? IN[jo + q] < IN[koff + q] : jl < klen;
+      }
+      if (less) r_krank++;
+    }
+  }
+  FD_CHECK();
+
+  // ---- preds -> target rows (new.js:1173-1188, 1254-1258) ----
+  uint8_t* OWN = M + FM_OWN;
+  if (r_chg)
+    for (int32_t q = 0; q < r_pcnt; q++) OWN[r_psoff + q] = (uint8_t)l;
+  wsync();
+  const bool e_new = isent && e_chg;
+  int32_t e_tr = -1;
+  uint32_t e_orank = 0, e_octr = 0;
+  {
+    const uint32_t o = e_new ? OWN[l] : 0;
+    const int32_t o_objc = __shfl(r_objc, o, 64), o_obja = __shfl(r_obja, o, 64), o_key = __shfl(r_key, o, 64);
+    const uint32_t o_kr = __shfl(r_krank, o, 64);
+    const int32_t o_keyc = __shfl(r_keyc, o, 64), o_keya = __shfl(r_keya, o, 64), o_idc = __shfl(r_idc, o, 64);
+    const uint32_t o_rank = __shfl(r_rank, o, 64);
+    const int32_t tr = e_new ? lookup(e_ctr, RANKDP[e_act]) : -1;
+    const uint32_t t = tr < 0 ? 0u : (uint32_t)tr;
+    const int32_t t_objc = __shfl(r_objc, t, 64), t_obja = __shfl(r_obja, t, 64), t_key = __shfl(r_key, t, 64);
+    const uint32_t t_kr = __shfl(r_krank, t, 64);
+    const int32_t t_keyc = __shfl(r_keyc, t, 64), t_keya = __shfl(r_keya, t, 64), t_idc = __shfl(r_idc, t, 64);
+    const int32_t t_ida = __shfl(r_ida, t, 64);
+    const uint32_t t_rank = __shfl(r_rank, t, 64);
+    const int32_t t_ins = __shfl((int32_t)r_ins, t, 64), t_del = __shfl((int32_t)r_del, t, 64);
+    if (e_new) {
+      bool ok = tr >= 0 && (uint32_t)tr < o && !t_del && t_objc == o_objc && t_obja == o_obja &&
+                (t_idc < o_idc || (t_idc == o_idc && t_rank < o_rank));
+      if (ok) {
+        if (o_key != FD_NULL) ok = t_key != FD_NULL && t_kr == o_kr;
+        else {
+          const int32_t ec = t_ins ? t_idc : t_keyc, ea = t_ins ? t_ida : t_keya;
+          ok = t_key == FD_NULL && ec == o_keyc && ea == o_keya;
+        }
+      }
+      if (!ok) bad = true;
+      e_tr = tr;
+      e_orank = o_rank;
+      e_octr = (uint32_t)o_idc;
+    }
+  }
+  FD_CHECK();
+
+  // ---- list elements: reference element of inserts, target element of updates ----
+  int32_t r_parent = -1, r_elem = -1;
+  {
+    int32_t want_c = -1;
+    uint32_t want_r = 0;
+    const bool listop = isrow && r_key == FD_NULL && !r_del;
+    if (listop && !(r_ins && (r_keyc == FD_NULL || r_keyc == 0 || r_keya < 0))) {
+      if (r_keya >= 0) { want_c = r_keyc; want_r = RANKDP[r_keya]; }
+    }
+    const int32_t p = want_c >= 0 ? lookup(want_c, want_r) : -1;
+    const uint32_t pu = p < 0 ? 0u : (uint32_t)p;
+    const int32_t p_ins = __shfl((int32_t)r_ins, pu, 64), p_del = __shfl((int32_t)r_del, pu, 64);
+    const int32_t p_objc = __shfl(r_objc, pu, 64), p_obja = __shfl(r_obja, pu, 64), p_key = __shfl(r_key, pu, 64);
+    const int32_t p_idc = __shfl(r_idc, pu, 64);
+    const uint32_t p_rank = __shfl(r_rank, pu, 64);
+    if (listop) {
+      if (r_ins) {
+        r_elem = (int32_t)l;
+        if (!(r_keyc == FD_NULL || r_keyc == 0 || r_keya < 0)) {
+          const bool ok = p >= 0 && p_ins && !p_del && p_objc == r_objc && p_obja == r_obja && p_key == FD_NULL &&
+                          (!r_chg || (uint32_t)p < l) && p_idc < r_idc;
+          if (!ok) bad = true;
+          r_parent = p;
+        }
+      } else {
+        const bool ok = p >= 0 && p_ins && !p_del && p_objc == r_objc && p_obja == r_obja && p_key == FD_NULL &&
+                        (!r_chg || (uint32_t)p < l) && (p_idc < r_idc || (p_idc == r_idc && p_rank < r_rank));
+        if (!ok) bad = true;
+        r_elem = p;
+      }
+    }
+  }
+  FD_CHECK();
+  const uint64_t r_objkey = (!isrow || r_objc == FD_NULL) ? 0ull
+                                                          : (((uint64_t)(uint32_t)r_objc + 1) << 6) | (r_obja < 0 ? 0u : RANKDP[r_obja]);
+
+  // ---- RGA order: preorder of the reference-element tree, children by descending opId
+  // (new.js:145-163); Euler tour + pointer jumping gives each element its suffix count ----
+  int8_t* FC = reinterpret_cast<int8_t*>(M + FM_FC);
+  int8_t* NS = reinterpret_cast<int8_t*>(M + FM_NS);
+  FC[l] = -1;
+  NS[l] = -1;
+  wsync();
+  const bool is_el = isrow && r_elem == (int32_t)l;
+  {
+    const uint64_t key = is_el ? (r_objkey << 19) | ((uint64_t)(r_parent + 1) << 12) | ((uint64_t)(63 - r_opr) << 6) | l : ~0ull;
+    const uint64_t s = sort64(key);
+    const uint64_t nx = __shfl_down(s, 1, 64), pv = __shfl_up(s, 1, 64);
+    if (s != ~0ull) {
+      const uint32_t row = (uint32_t)(s & 63);
+      if (l < 63 && nx != ~0ull && (nx >> 12) == (s >> 12)) NS[row] = (int8_t)(nx & 63);
+      const int32_t par = (int32_t)((s >> 12) & 127) - 1;
+      if ((l == 0 || (pv >> 12) != (s >> 12)) && par >= 0) FC[par] = (int8_t)row;
+    }
+  }
+  wsync();
+  uint32_t r_suffix = 0;
+  {
+    const int32_t END = -1;
+    int32_t n0 = END, n1 = END;
+    uint32_t w0 = 0, w1 = 0;
+    if (is_el) {
+      n0 = FC[l] >= 0 ? 2 * FC[l] : (int32_t)(2 * l + 1);
+      w0 = 1;
+      n1 = NS[l] >= 0 ? 2 * NS[l] : (r_parent >= 0 ? 2 * r_parent + 1 : END);
+    }
+#pragma unroll 1
+    for (int round = 0; round < 7; round++) {
+      const uint32_t t0 = n0 < 0 ? 0u : (uint32_t)n0 >> 1, t1 = n1 < 0 ? 0u : (uint32_t)n1 >> 1;
+      const int32_t a_n0 = __shfl(n0, t0, 64), a_n1 = __shfl(n1, t0, 64);
+      const uint32_t a_w0 = __shfl(w0, t0, 64), a_w1 = __shfl(w1, t0, 64);
+      const int32_t b_n0 = __shfl(n0, t1, 64), b_n1 = __shfl(n1, t1, 64);
+      const uint32_t b_w0 = __shfl(w0, t1, 64), b_w1 = __shfl(w1, t1, 64);
+      if (n0 != END) {
+        const bool odd = n0 & 1;
+        w0 += odd ? a_w1 : a_w0;
+        n0 = odd ? a_n1 : a_n0;
+      }
+      if (n1 != END) {
+        const bool odd = n1 & 1;
+        w1 += odd ? b_w1 : b_w0;
+        n1 = odd ? b_n1 : b_n0;
+      }
+    }
+    bad |= n0 != END || n1 != END;  // chain longer than 128 nodes cannot happen; stay safe
+    r_suffix = w0;
+  }
+  FD_CHECK();
+
+  // ---- document order: object, then key (UTF-16) | list position, then opId ----
+  const bool isout = isrow && !r_del;
+  const uint32_t NOUT = __popcll(__ballot(isout));
+  uint32_t k_row;  // row at output position l
+  {
+    const uint32_t esuf = __shfl(r_suffix, r_elem < 0 ? 0u : (uint32_t)r_elem, 64);
+    const uint64_t k2 = keyed ? r_krank : (uint64_t)(64 - esuf);
+    const uint64_t key = isout ? (r_objkey << 20) | ((uint64_t)(keyed ? 0 : 1) << 19) | (k2 << 12) | ((uint64_t)r_opr << 6) | l
+                               : ~0ull;
+    k_row = (uint32_t)(sort64(key) & 63);
+  }
+
+  // ---- succ lists: base succs merged with the new succs of each row (new.js:1173-1188) ----
+  uint64_t* BENT = reinterpret_cast<uint64_t*>(M + FM_BENT);
+  uint64_t* NSORT = reinterpret_cast<uint64_t*>(M + FM_NSORT);
+  uint32_t* CNTN = reinterpret_cast<uint32_t*>(M + FM_CNTN);
+  uint8_t* LON = M + FM_LON;
+  CNTN[l] = 0;
+  if (isent && !e_chg) BENT[l] = ((uint64_t)(uint32_t)e_ctr << 6) | RANKDP[e_act];
+  wsync();
+  {
+    const uint64_t key = e_new ? ((uint64_t)e_tr << 37) | ((uint64_t)e_octr << 6) | e_orank : ~0ull;
+    const uint64_t s = sort64(key);
+    NSORT[l] = s;
+    const uint64_t pv = __shfl_up(s, 1, 64);
+    if (s != ~0ull) {
+      const uint32_t tg = (uint32_t)(s >> 37);
+      if (l == 0 || (pv >> 37) != tg) LON[tg] = (uint8_t)l;
+      atomicAdd(&CNTN[tg], 1u);
+    }
+  }
+  wsync();
+  int32_t* OUTC = reinterpret_cast<int32_t*>(M + FM_OUTC);
+  uint8_t* OUTA = M + FM_OUTA;
+  uint8_t* const RANK2DP = M + FM_CANON;  // canon table is dead: reuse as rank -> doc actor index
+  wsync();
+  if (l < NA) RANK2DP[RANKDP[l]] = (uint8_t)l;
+  wsync();
+  uint32_t NSUCC, sc_k, so_k;
+  {
+    const uint32_t r = k_row;
+    const int32_t k_chg = __shfl((int32_t)r_chg, r, 64), k_pc = __shfl(r_pcnt, r, 64);
+    const uint32_t k_pso = __shfl(r_psoff, r, 64);
+    const bool out = l < NOUT;
+    const uint32_t nold = (out && !k_chg) ? (uint32_t)k_pc : 0u;
+    const uint32_t nnew = out ? CNTN[r] : 0u;
+    sc_k = nold + nnew;
+    so_k = excl_add(sc_k, NSUCC);
+    if (out) {
+      const uint32_t lo = nnew ? LON[r] : 0;
+      uint32_t a = 0, b2 = 0, w = so_k;
+      while (a < nold || b2 < nnew) {
+        bool take_old;
+        const uint64_t eo = a < nold ? BENT[k_pso + a] : 0, en = b2 < nnew ? NSORT[lo + b2] : 0;
+        if (a >= nold) take_old = false;
+        else if (b2 >= nnew) take_old = true;
+        else {
+          const uint64_t oc = eo >> 6, nc = (en >> 6) & 0x7fffffffull;
+          take_old = oc < nc || (oc == nc && (eo & 63) < (en & 63));
+        }
+        if (take_old) { OUTC[w] = (int32_t)(eo >> 6); OUTA[w] = RANK2DP[eo & 63]; a++; }
+        else { OUTC[w] = (int32_t)((en >> 6) & 0x7fffffffull); OUTA[w] = RANK2DP[en & 63]; b2++; }
+        w++;
+      }
+    }
+  }
+  bad |= NSUCC > FD_MAX;
+  wsync();
+  FD_CHECK();
+
+  // ---- canonical re-encode into the output image (cells are dead) ----
+  uint8_t* const OB = S + F.cells;
+  uint32_t* COLLEN = reinterpret_cast<uint32_t*>(M + FM_COLLEN);
+  // header reserve: magic, checksum, type, body length, actors, heads, column tables
+  uint32_t alen_sum;
+  const uint32_t a_len = l < NA ? RO[2 * M[FM_DP2REF + l] + 1] : 0u;
+  const uint32_t a_pos = excl_add(l < NA ? (uint32_t)uleb_len(a_len) + a_len : 0u, alen_sum);
+  const uint32_t T0 = 9 + 10 + 10 + alen_sum + 10 + 32 * NH + 2 * (10 + 25 * 12);
+  uint32_t cur = T0;
+  const uint32_t NC = nbc + N, ND = nbd + nd_total;
+  // change row l of the merged document: base rows then the applied changes (appendChange,
+  // new.js:1680-1692)
+  {
+    const uint32_t c = l >= nbc ? l - nbc : 0;
+    const uint32_t cs = c & 63;
+    const ChgHdr& h = chh[cs < N ? cs : 0];
+    const uint32_t n_adp = __shfl(a_dp, cs, 64), n_nd = __shfl(c_ndeps, cs, 64), n_nops = __shfl(c_nops, cs, 64);
+    const bool isnew = l >= nbc && l < NC;
+    int64_t v_act = bc_actor, v_seq = bc_seq, v_max = bc_max, v_time = bc_time, v_xlen = bc_xlen;
+    uint32_t v_nd = bc_nd, m_off = 0, m_len = 0, x_off = bc_xoff, x_len = bc_xraw;
+    bool m_null = bc_msg == AM_NULL64;
+    if (!m_null) { m_off = (uint32_t)((uint64_t)bc_msg >> 32); m_len = (uint32_t)(bc_msg & 0xffffffff); }
+    if (isnew) {
+      v_act = n_adp;
+      v_seq = h.seq;
+      v_max = h.start_op + (int64_t)n_nops - 1;
+      v_time = h.time;
+      m_null = false;
+      m_off = (uint32_t)(h.base + h.msg_off - a0);
+      m_len = h.msg_len;
+      v_nd = n_nd;
+      v_xlen = (int64_t)(((uint64_t)(h.has_extra ? h.extra_len : 0u) << 4) | 7);
+      x_off = (uint32_t)(h.base + h.extra_off - a0);
+      x_len = h.has_extra ? h.extra_len : 0u;
+    }
+    // message equality with the previous row (S column run detection)
+    const uint32_t pm_off = __shfl_up(m_off, 1, 64), pm_len = __shfl_up(m_len, 1, 64);
+    bool meq = !m_null && l > 0 && pm_len == m_len;
+    for (uint32_t q = 0; meq && q < m_len; q++) meq = IN[pm_off + q] == IN[m_off + q];
+    const int64_t dep_new = __shfl(dep_idx, (l - nbd) & 63, 64);
+    const int64_t v_deps = l < nbd ? bc_dep : dep_new;
+#pragma unroll 1
+    for (int col = 0; col < DC_NCOLS; col++) {
+      int64_t v = 0;
+      bool nul = false;
+      uint32_t so = 0, sl = 0, n = NC;
+      switch (col) {
+        case DC_ACTOR: v = v_act; break;
+        case DC_SEQ: v = v_seq; break;
+        case DC_MAXOP: v = v_max; break;
+        case DC_TIME: v = v_time; break;
+        case DC_MESSAGE: nul = m_null; so = m_off; sl = m_len; break;
+        case DC_DEPS_NUM: v = v_nd; break;
+        case DC_DEPS_INDEX: v = v_deps; n = ND; break;
+        case DC_EXTRA_LEN: v = v_xlen; break;
+        default: so = x_off; sl = x_len; break;
+      }
+      if (v == AM_NULL64) nul = true;
+      const uint32_t len = enc_col(kEncKind[OC_NCOLS + col], n, v, nul, so, sl, meq, IN, OB + cur, F.cells_cap - cur);
+      if (len == ~0u) { bad = true; break; }
+      if (l == 0) COLLEN[OC_NCOLS + col] = len;
+      cur += len;
+    }
+  }
+  FD_CHECK();
+  {
+    const uint32_t r = k_row;
+    const bool out = l < NOUT;
+    const int32_t objc = __shfl(r_objc, r, 64), obja = __shfl(r_obja, r, 64), keyc = __shfl(r_keyc, r, 64);
+    const int32_t keya = __shfl(r_keya, r, 64), key = __shfl(r_key, r, 64), idc = __shfl(r_idc, r, 64);
+    const int32_t ida = __shfl(r_ida, r, 64), ins = __shfl((int32_t)r_ins, r, 64), act = __shfl(r_act, r, 64);
+    const int32_t vlen = __shfl(r_vlen, r, 64), chc = __shfl(r_chc, r, 64), cha = __shfl(r_cha, r, 64);
+    const uint32_t voff = __shfl(r_voff, r, 64), vb = __shfl(r_vb, r, 64), kr = __shfl(r_krank, r, 64);
+    const uint32_t pkr = __shfl_up(kr, 1, 64);
+    const uint32_t succ_a = OUTA[l], succ_c = (uint32_t)OUTC[l];
+    auto nv = [](int32_t x) -> int64_t { return x == FD_NULL ? AM_NULL64 : (int64_t)x; };
+    auto av = [](int32_t x) -> int64_t { return x < 0 ? AM_NULL64 : (int64_t)x; };
+#pragma unroll 1
+    for (int col = 0; col < OC_NCOLS; col++) {
+      int64_t v = 0;
+      uint32_t so = 0, sl = 0, n = NOUT;
+      switch (col) {
+        case OC_OBJ_ACTOR: v = av(obja); break;
+        case OC_OBJ_CTR: v = nv(objc); break;
+        case OC_KEY_ACTOR: v = av(keya); break;
+        case OC_KEY_CTR: v = nv(keyc); break;
+        case OC_KEY_STR: v = key == FD_NULL ? AM_NULL64 : 0; so = (uint32_t)key >> 8; sl = (uint32_t)key & 255; break;
+        case OC_ID_ACTOR: v = ida; break;
+        case OC_ID_CTR: v = idc; break;
+        case OC_INSERT: v = ins; break;
+        case OC_ACTION: v = act; break;
+        case OC_VAL_LEN: v = nv(vlen); break;
+        case OC_VAL_RAW: so = voff; sl = vb; break;
+        case OC_CHLD_ACTOR: v = av(cha); break;
+        case OC_CHLD_CTR: v = nv(chc); break;
+        case OC_GRP_NUM: v = sc_k; break;
+        case OC_GRP_ACTOR: v = succ_a; n = NSUCC; break;
+        default: v = succ_c; n = NSUCC; break;
+      }
+      const bool nul = out && v == AM_NULL64;
+      const bool eqs = col == OC_KEY_STR && key != FD_NULL && pkr == kr;
+      const uint32_t len = enc_col(kEncKind[col], n, v, nul, so, sl, eqs, IN, OB + cur, F.cells_cap - cur);
+      if (len == ~0u) { bad = true; break; }
+      if (l == 0) COLLEN[col] = len;
+      cur += len;
+    }
+  }
+  wsync();
+  FD_CHECK();
+  // trailer: heads indexes (all known here) and the base document's extra bytes
+  const uint32_t cols_end = cur;
+  const uint32_t xlen = has_base ? dh->extra_len : 0u;
+  uint32_t hib = 0;
+  {
+    const int64_t* HIDX = reinterpret_cast<const int64_t*>(M + FM_HIDX);
+    const uint32_t hb = l < NH ? (uint32_t)uleb_len((uint64_t)HIDX[l]) : 0u;
+    const uint32_t ho = excl_add(hb, hib);
+    if (cols_end + hib + xlen > F.cells_cap) bad = true;
+    else {
+      if (l < NH) put_uleb(OB + cols_end + ho, (uint64_t)HIDX[l]);
+      for (uint32_t q = l; q < xlen; q += 64) OB[cols_end + hib + q] = IN[dh->base + dh->extra_off - a0 + q];
+    }
+  }
+  FD_CHECK();
+  // header, written to end exactly at T0 (encodeDocumentHeader, columnar.js:983-1004)
+  uint32_t nce = 0, noe = 0, ctab = 0, coltot = 0;
+  for (int c = 0; c < DC_NCOLS; c++) {
+    const uint32_t len = COLLEN[OC_NCOLS + c];
+    if (len) { nce++; ctab += uleb_len(kDocChgColIds[c]) + uleb_len(len); coltot += len; }
+  }
+  for (int c = 0; c < OC_NCOLS; c++) {
+    const uint32_t len = COLLEN[c];
+    if (len) { noe++; ctab += uleb_len(kDocOpColIds[c]) + uleb_len(len); coltot += len; }
+  }
+  const uint32_t pre_cols = uleb_len(NA) + alen_sum + uleb_len(NH) + 32 * NH + uleb_len(nce) + uleb_len(noe) + ctab;
+  const uint64_t body = (uint64_t)pre_cols + coltot + hib + xlen;
+  const uint32_t hs = 9 + uleb_len(body) + pre_cols;
+  if (hs > T0) return;  // cannot happen (T0 bounds it); stay safe
+  const uint32_t start = T0 - hs;
+  {
+    const uint32_t act0 = start + 9 + uleb_len(body) + uleb_len(NA);  // first actor record
+    const uint32_t heads0 = act0 + alen_sum;
+    if (l < NA) {
+      uint8_t* o = put_uleb(OB + act0 + a_pos, a_len);
+      const uint32_t src = RO[2 * M[FM_DP2REF + l]];
+      for (uint32_t q = 0; q < a_len; q++) o[q] = IN[src + q];
+    }
+    const uint32_t hbytes0 = heads0 + uleb_len(NH);
+    for (uint32_t q = l; q < 32 * NH; q += 64) OB[hbytes0 + q] = M[FM_HOUT + q];
+    if (l == 0) {
+      uint8_t* o = OB + start;
+      for (int k = 0; k < 4; k++) *o++ = kMagic[k];
+      for (int k = 0; k < 4; k++) *o++ = 0;  // checksum: k_out_hash_ws
+      *o++ = 0;                               // CHUNK_TYPE_DOCUMENT
+      o = put_uleb(o, body);
+      put_uleb(o, NA);
+      o = put_uleb(OB + heads0, NH);
+      o += 32 * NH;
+      o = put_uleb(o, nce);
+      for (int c = 0; c < DC_NCOLS; c++)
+        if (COLLEN[OC_NCOLS + c]) { o = put_uleb(o, kDocChgColIds[c]); o = put_uleb(o, COLLEN[OC_NCOLS + c]); }
+      o = put_uleb(o, noe);
+      for (int c = 0; c < OC_NCOLS; c++)
+        if (COLLEN[c]) { o = put_uleb(o, kDocOpColIds[c]); o = put_uleb(o, COLLEN[c]); }
+    }
+  }
+  wsync();
+  // copy the image [start, cols_end + hib + xlen) to the document's output slot, one dword per lane
+  const uint32_t olen = cols_end + hib + xlen - start;
+  if (olen > L.out_cap) return;
+  {
+    uint32_t* dst = reinterpret_cast<uint32_t*>(wsg + L.out);
+    const uint8_t* src = OB + start;
+    for (uint32_t q = 4 * l; q < olen; q += 256) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) w |= (uint32_t)(q + k < olen ? src[q + k] : 0) << (8 * k);
+      dst[q >> 2] = w;
+    }
+  }
+  if (l < N) chg_state[dd.chg_begin + l] = (int32_t)l;
+  if (l == 0) {
+    am_doc_result r;
+    r.status = AM_OK;
+    r.err_change = 0xffffffffu;
+    r.arg0 = r.arg1 = 0;
+    r.arg_actor_off = 0;
+    r.arg_actor_len = 0;
+    r.napplied = N;
+    r.nqueued = 0;
+    r.nheads = NH;
+    r.nops = NOUT;
+    r.nchanges = NC;
+    r.max_op = maxop;
+    r.out_off = 0;
+    r.out_len = olen;
+    r.ws_off = wso;
+    r.ws_bytes = L.total;
+    results[doc] = r;
+    fast_done[doc] = 1;
+  }
+#undef FD_CHECK
+}

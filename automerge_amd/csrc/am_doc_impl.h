@@ -800,9 +800,10 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
                                                const ChunkInfo* __restrict__ info, const DocBounds* __restrict__ bounds,
                                                const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base,
                                                uint64_t ws_cap, uint32_t lds_bytes, am_doc_result* __restrict__ results,
-                                               int32_t* __restrict__ chg_state) {
+                                               int32_t* __restrict__ chg_state, const uint8_t* __restrict__ fast_done) {
   __shared__ DocShared s;
   const uint32_t doc = blockIdx.x, t = threadIdx.x, T = blockDim.x;
+  if (fast_done && fast_done[doc]) return;  // merged by k_doc_fast (am_doc_fast.h)
   const am_doc_desc dd = docs[doc];
   uint8_t* const wsg = ws_base + ws_off[doc];  // global (derived from the kernel argument)
   if (t == 0) {

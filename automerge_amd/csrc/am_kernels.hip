@@ -411,6 +411,7 @@ namespace glb_mode {
 constexpr bool kHotLds = false;
 #include "am_doc_impl.h"
 }  // namespace glb_mode
+#include "am_doc_fast.h"
 
 // ------------------------------------------------------------------------------------------
 // k_compact: workgroup per document copies its merged chunk into the dense output arena
@@ -472,7 +473,9 @@ static_assert(sizeof(ChgHdr) <= AM_SZ_CHGHDR, "ChgHdr");
 
 size_t am_scan_tmp_elems(uint32_t n) { return (n + SCAN_T - 1) / SCAN_T + 1; }
 
-__global__ void __launch_bounds__(256) k_max_hot(const DocBounds* __restrict__ bounds, uint32_t ndocs, uint64_t* __restrict__ max_hot) {
+// max_hot[0]: largest k_doc hot working set; max_hot[1]: largest k_doc_fast LDS slice (0: none)
+__global__ void __launch_bounds__(256) k_max_hot(const DocBounds* __restrict__ bounds, const am_doc_desc* __restrict__ docs,
+                                                 uint32_t ndocs, uint64_t* __restrict__ max_hot) {
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= ndocs) return;
   const DocBounds b = bounds[d];
@@ -480,6 +483,9 @@ __global__ void __launch_bounds__(256) k_max_hot(const DocBounds* __restrict__ b
   // a scattered document needs the global-mode launch: report a hot set above any LDS budget
   const uint64_t h = doc_scattered(b) ? (1ull << 40) : L.hot_total;
   atomicMax(reinterpret_cast<unsigned long long*>(max_hot), (unsigned long long)h);
+  const am_doc_desc dd = docs[d];
+  if (fast_eligible(b, dd))
+    atomicMax(reinterpret_cast<unsigned long long*>(max_hot + 1), (unsigned long long)fast_layout(b, dd.known_count).total);
 }
 
 void am_launch_chunks(const BatchDev& b, hipStream_t s) {
@@ -488,10 +494,10 @@ void am_launch_chunks(const BatchDev& b, hipStream_t s) {
 }
 void am_launch_bounds(const BatchDev& b, hipStream_t s) {
   if (!b.ndocs) return;
-  (void)hipMemsetAsync(b.max_hot, 0, sizeof(uint64_t), s);
+  (void)hipMemsetAsync(b.max_hot, 0, 2 * sizeof(uint64_t), s);
   hipLaunchKernelGGL(k_bounds, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, b.docs, b.ndocs, b.chunks, b.info, b.bounds,
                      b.ws_bytes);
-  hipLaunchKernelGGL(k_max_hot, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, b.bounds, b.ndocs, b.max_hot);
+  hipLaunchKernelGGL(k_max_hot, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, b.bounds, b.docs, b.ndocs, b.max_hot);
   uint32_t nblk = (b.ndocs + SCAN_T - 1) / SCAN_T;
   hipLaunchKernelGGL(k_scan_blocks, dim3(nblk), dim3(SCAN_T), 0, s, b.ws_bytes, b.ws_off, b.scan_tmp, b.ndocs);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, b.scan_tmp, nblk, b.ws_total);
@@ -501,11 +507,23 @@ void am_launch_doc(const BatchDev& b, hipStream_t s) {
   if (!b.ndocs) return;
   // documents whose hot working set fits the LDS allocation run from LDS; the rest (if any)
   // from their global workspace
-  hipLaunchKernelGGL(lds_mode::k_doc, dim3(b.ndocs), dim3(DOC_T), b.lds_bytes, s, b.arena, b.chunks, b.docs, b.known,
-                     b.info, b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state);
-  if (b.max_hot_host > b.lds_bytes)
-    hipLaunchKernelGGL(glb_mode::k_doc, dim3(b.ndocs), dim3(DOC_T), 0, s, b.arena, b.chunks, b.docs, b.known, b.info,
-                       b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state);
+  // small documents first: k_doc_fast merges every document in its envelope (one wave each,
+  // four per workgroup) and marks it; k_doc then takes the rest and exits at once for the marked
+  const uint8_t* fd = nullptr;
+  if (b.fast_lds && b.fast_done) {
+    (void)hipMemsetAsync(b.fast_done, 0, b.ndocs, s);
+    hipLaunchKernelGGL(k_doc_fast, dim3((b.ndocs + FD_DOCS_PER_WG - 1) / FD_DOCS_PER_WG), dim3(64 * FD_DOCS_PER_WG),
+                       FD_DOCS_PER_WG * b.fast_lds, s, b.arena, b.chunks, b.docs, b.known, b.info, b.bounds, b.ws_off, b.ws,
+                       b.ws_cap, b.fast_lds, b.ndocs, b.results, b.chg_state, b.fast_done);
+    fd = b.fast_done;
+  }
+  if (!b.fast_only) {
+    hipLaunchKernelGGL(lds_mode::k_doc, dim3(b.ndocs), dim3(DOC_T), b.lds_bytes, s, b.arena, b.chunks, b.docs, b.known,
+                       b.info, b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd);
+    if (b.max_hot_host > b.lds_bytes)
+      hipLaunchKernelGGL(glb_mode::k_doc, dim3(b.ndocs), dim3(DOC_T), 0, s, b.arena, b.chunks, b.docs, b.known, b.info,
+                         b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd);
+  }
 }
 __global__ void __launch_bounds__(256) k_out_hash_ws(am_doc_result* __restrict__ res, uint32_t ndocs, uint8_t* __restrict__ ws,
                                                      const DocBounds* __restrict__ bounds) {

@@ -19,6 +19,9 @@ struct BatchDev {
   uint64_t* max_hot;       // 1 value: largest hot working set of the batch
   uint32_t lds_bytes;      // dynamic LDS per document workgroup
   uint64_t max_hot_host;   // host copy of *max_hot
+  uint32_t fast_lds;       // k_doc_fast LDS slice per document (0: no document in its envelope / disabled)
+  uint8_t* fast_done;      // per doc: 1 = merged by k_doc_fast
+  bool fast_only;          // every document is in the fast envelope: skip the k_doc launches
   uint8_t* ws;
   uint64_t ws_cap;
   am_doc_result* results;

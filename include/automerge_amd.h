@@ -164,6 +164,9 @@ int am_batch_stage_times(am_batch *b, float *ms4);
  * container (columnar.js:659-686) and mix64 is the splitmix64 finalizer. Host restatement:
  * automerge_amd/shard.py doc_digest. */
 int am_batch_digest(am_batch *b, uint64_t first_doc, uint64_t *digest);
+/* Per document of the last run: 1 when the small-document kernel (k_doc_fast) merged it, 0 when
+ * the general kernel did (documents outside its envelope, errors, getPatch requests). */
+int am_batch_fast_flags(am_batch *b, uint8_t *flags);
 /* Device pointer + size of the staged arena / merged outputs (for bench byte accounting). */
 uint64_t am_batch_workspace_bytes(am_batch *b);
 

@@ -190,3 +190,58 @@ def test_workload_batch_matches_oracle_and_digest(kind, first, n):
         assert b.doc_output(i, r[i]) == want, i
         terms.append(shard.doc_digest(first + i, 0, want))
     assert b.digest(first) == shard.combine(terms)
+
+
+def test_fast_and_general_kernels_agree(docs):
+    """Every single-apply golden scenario and a C4/C2 sample merged twice in one process: with the
+    small-document kernel (k_doc_fast) and with it disabled (AM_FAST=0 at stage time, k_doc only).
+    Outputs, heads and results must be identical, and the fast kernel must take the C4/C2 documents."""
+    import os
+    from automerge_amd import workload
+    from automerge_amd.batch import Batch
+    items = []
+    for sc in docs:
+        steps = sc["steps"]
+        if len(steps) == 1 and steps[0]["op"] == "apply":
+            items.append((None, [bytes.fromhex(c) for c in steps[0]["changes"]]))
+        elif len(steps) == 2 and steps[0]["op"] == "load":
+            items.append((bytes.fromhex(steps[0]["bytes"]), [bytes.fromhex(c) for c in steps[1]["changes"]]))
+    for kind in ("c4", "c2"):
+        arena, chunks, dd, _ = getattr(workload, kind)(5, 300)
+        items += [workload.doc_chunks(arena, chunks, dd, i) for i in range(300)]
+
+    def run(fast):
+        old = os.environ.get("AM_FAST")
+        os.environ["AM_FAST"] = "1" if fast else "0"
+        try:
+            b = Batch()
+            b.stage_docs(items)
+        finally:
+            if old is None:
+                del os.environ["AM_FAST"]
+            else:
+                os.environ["AM_FAST"] = old
+        b.run()
+        b.sync()
+        r = b.results()
+        outs = [b.doc_output(i, r[i]) if r[i]["status"] == 0 else b"" for i in range(len(items))]
+        heads = [b.doc_heads(i, int(r[i]["nheads"])) if r[i]["status"] == 0 else [] for i in range(len(items))]
+        return r, outs, heads, b.fast_flags()
+
+    rf, of, hf, flags = run(True)
+    rg, og, hg, gflags = run(False)
+    assert not gflags.any()
+    nfast = int(flags.sum())
+    assert flags[-600:].all(), "C4/C2 documents must take the fast kernel"
+    bad = []
+    for i in range(len(items)):
+        for k in ("status", "err_change", "arg0", "arg1", "napplied", "nqueued", "nheads", "nops", "nchanges", "max_op",
+                  "out_len"):
+            if rf[i][k] != rg[i][k]:
+                bad.append((i, k, int(rf[i][k]), int(rg[i][k]), bool(flags[i])))
+        if of[i] != og[i]:
+            bad.append((i, "bytes", bool(flags[i])))
+        if hf[i] != hg[i]:
+            bad.append((i, "heads", bool(flags[i])))
+    assert not bad, (nfast, bad[:10])
+    print("fast kernel merged %d of %d documents" % (nfast, len(items)))
