@@ -139,3 +139,9 @@ class Batch:
 
     def workspace_bytes(self):
         return N.lib.am_batch_workspace_bytes(self._b)
+
+    def kernel_info(self):
+        """{k_doc LDS bytes, k_doc_fast LDS bytes per document, largest k_doc hot set} of the staged batch."""
+        out = np.zeros(3, np.uint64)
+        N.lib.am_batch_kernel_info(self._b, out.ctypes.data)
+        return {"k_doc_lds": int(out[0]), "k_doc_fast_lds_per_doc": int(out[1]), "k_doc_max_hot": int(out[2])}

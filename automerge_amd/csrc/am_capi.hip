@@ -536,6 +536,14 @@ extern "C" int am_batch_fast_flags(am_batch* b, uint8_t* flags) {
 }
 
 extern "C" uint64_t am_batch_workspace_bytes(am_batch* b) { return b->ws_need; }
+// launch shape of the document kernels of the staged batch: [0] k_doc dynamic LDS bytes, [1] the
+// k_doc_fast LDS slice per document (0: no document in its envelope), [2] largest k_doc hot set
+extern "C" int am_batch_kernel_info(am_batch* b, uint64_t* out3) {
+  out3[0] = b->lds_bytes;
+  out3[1] = b->fast_lds;
+  out3[2] = b->max_hot_v;
+  return 0;
+}
 
 // =============================================================================================
 // per-document backend state (backend/backend.js + BackendDoc over the batch path, n = 1)

@@ -394,7 +394,7 @@ __device__ static uint32_t rle_count_sum(const uint8_t* p, uint64_t n, bool is_s
 }
 
 // UTF-8 well-formedness (WHATWG decoder would substitute U+FFFD otherwise)
-__device__ static bool utf8_valid_dev(const uint8_t* s, uint32_t n) {
+__device__ __forceinline__ static bool utf8_valid_dev(const uint8_t* s, uint32_t n) {
   uint32_t i = 0;
   while (i < n) {
     uint8_t b = s[i];

@@ -22,6 +22,25 @@
 //   cells   decoded column values (4 B per value); reused as the output image afterwards
 #pragma once
 
+// Probe builds (-DAM_PHASE_CLOCK, tools/build_probe.sh): lane 0 of every 16th document adds the
+// s_memtime delta of each phase to am_phase_cycles[16 + k]
+#ifdef AM_PHASE_CLOCK
+#define FPH(k)                                                                        \
+  do {                                                                                \
+    if (l == 0 && (doc & 15) == 0) {                                                  \
+      const uint64_t now_ = clock64();                                                \
+      atomicAdd(&am_phase_cycles[16 + (k)], (unsigned long long)(now_ - ph_last));    \
+      ph_last = now_;                                                                 \
+    }                                                                                 \
+  } while (0)
+#else
+#define FPH(k) \
+  do {         \
+  } while (0)
+#endif
+
+#include "am_wave.h"
+
 #define FD_MAX 64
 #define FD_SPAN_MAX 8192
 #define FD_LDS_CAP (24 * 1024)
@@ -105,7 +124,6 @@ __host__ __device__ inline bool fast_eligible(const DocBounds& b, const am_doc_d
 }
 
 namespace fastdoc {
-using lds_mode::kOpColDec;
 using lds_mode::kEncKind;
 using lds_mode::EK_U;
 using lds_mode::EK_D;
@@ -125,54 +143,11 @@ __device__ __forceinline__ uint64_t lt_mask() {
   return l ? (~0ull >> (64 - l)) : 0ull;
 }
 __device__ __forceinline__ uint32_t ctz64(uint64_t m) { return m ? (uint32_t)__builtin_ctzll(m) : 64u; }
-__device__ __forceinline__ uint32_t excl_add(uint32_t v, uint32_t& total) {
-  const uint32_t l = lane();
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (l >= (uint32_t)d) x += y;
-  }
-  total = __shfl(x, 63, 64);
-  return x - v;
-}
-__device__ __forceinline__ int32_t incl_max(int32_t v) {
-  const uint32_t l = lane();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int32_t y = __shfl_up(v, d, 64);
-    if (l >= (uint32_t)d && y > v) v = y;
-  }
-  return v;
-}
-__device__ __forceinline__ int64_t max_all(int64_t v) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) {
-    const int64_t y = __shfl_xor(v, d, 64);
-    v = y > v ? y : v;
-  }
-  return v;
-}
-__device__ __forceinline__ uint32_t sum_all(uint32_t v) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
-  return v;
-}
-// ascending bitonic sort of one u64 per lane (padding lanes hold ~0)
-__device__ __forceinline__ uint64_t sort64(uint64_t v) {
-  const uint32_t l = lane();
-#pragma unroll
-  for (uint32_t k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      const uint64_t p = __shfl_xor(v, (int)j, 64);
-      const bool up = (l & k) == 0, lo = (l & j) == 0;
-      const uint64_t mn = v < p ? v : p, mx = v < p ? p : v;
-      v = (lo == up) ? mn : mx;
-    }
-  }
-  return v;
-}
+using wave::excl_add;
+using wave::incl_max;
+using wave::max_all;
+using wave::sum_all;
+using wave::sort64;
 __device__ __forceinline__ bool words_eq(const uint32_t* a, const uint32_t* b) {
   const uint4 a0 = reinterpret_cast<const uint4*>(a)[0], a1 = reinterpret_cast<const uint4*>(a)[1];
   const uint4 b0 = reinterpret_cast<const uint4*>(b)[0], b1 = reinterpret_cast<const uint4*>(b)[1];
@@ -187,6 +162,158 @@ __device__ __forceinline__ void load32(const uint8_t* p, uint32_t w[8]) {
 }
 __device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
 
+// ---- 32-bit column stream decoder (RLEDecoder / DeltaDecoder / BooleanDecoder,
+// encoding.js:789-1207) specialised by column type at compile time. Every lane of a decode round
+// runs the same type, so the wave executes one record state machine instead of the union of
+// four. Anything the fast envelope does not cover -- a value outside 31 bits, a non-canonical
+// record, a truncated stream -- only raises `bad`: the document then goes to k_doc, which
+// reports the reference's exact error. ----
+struct Dec32 {
+  uint32_t off, end;  // byte offsets into the staged input
+  int32_t count;      // values left in the current record
+  int32_t last;       // repeated / last literal value (utf8: offset << 8 | length)
+  int64_t abs;        // delta running value
+  uint8_t state;      // 0 none, 1 repetition, 2 literal, 3 nulls
+  bool has_last, last_null;
+};
+__device__ __forceinline__ void d32_init(Dec32& d, uint32_t off, uint32_t len) {
+  d.off = off; d.end = off + len; d.count = 0; d.last = 0; d.abs = 0;
+  d.state = 0; d.has_last = false; d.last_null = false;
+}
+// unsigned LEB128 < 2^31 (anything else is outside the envelope)
+__device__ __forceinline__ uint32_t d32_uleb(const uint8_t* in, Dec32& d, bool& bad) {
+  uint32_t v = 0;
+  for (uint32_t sh = 0; sh < 35; sh += 7) {
+    if (d.off >= d.end) { bad = true; return 0; }
+    const uint32_t b = in[d.off++];
+    v |= (b & 0x7f) << sh;
+    if (!(b & 0x80)) {
+      if (sh == 28 && (b & 0x78)) bad = true;  // >= 2^31
+      if (b == 0 && sh) bad = true;            // over-long: let k_doc judge it
+      return v;
+    }
+  }
+  bad = true;
+  return 0;
+}
+// signed LEB128 in (-2^31, 2^31)
+__device__ __forceinline__ int32_t d32_sleb(const uint8_t* in, Dec32& d, bool& bad) {
+  uint32_t v = 0;
+  for (uint32_t sh = 0; sh < 35; sh += 7) {
+    if (d.off >= d.end) { bad = true; return 0; }
+    const uint32_t b = in[d.off++];
+    v |= (b & 0x7f) << sh;
+    if (!(b & 0x80)) {
+      const uint32_t used = sh + 7;
+      if (used < 32 && (b & 0x40)) v |= ~0u << used;
+      if (sh == 28) {
+        // the fifth byte carries bits 28..34: in range iff they all equal the sign bit
+        if ((b & 0x78) != 0 && (b & 0x78) != 0x78) bad = true;
+      }
+      if ((int32_t)v == INT32_MIN) bad = true;
+      return (int32_t)v;
+    }
+  }
+  bad = true;
+  return 0;
+}
+template <uint8_t T>
+__device__ __forceinline__ int32_t d32_raw(const uint8_t* in, Dec32& d, bool& bad) {
+  if constexpr (T == DT_UTF8) {
+    const uint32_t len = d32_uleb(in, d, bad);
+    const uint32_t at = d.off;
+    if (len > 255 || d.off + len > d.end) { bad = true; return 0; }
+    d.off += len;
+    return (int32_t)((at << 8) | len);
+  } else if constexpr (T == DT_UINT) {
+    return (int32_t)d32_uleb(in, d, bad);
+  } else {
+    return d32_sleb(in, d, bad);
+  }
+}
+template <uint8_t T>
+__device__ __forceinline__ bool d32_eq(const uint8_t* in, int32_t a, int32_t b) {
+  if constexpr (T == DT_UTF8) {
+    const uint32_t al = (uint32_t)a & 255, bl = (uint32_t)b & 255;
+    if (al != bl) return false;
+    const uint32_t ao = (uint32_t)a >> 8, bo = (uint32_t)b >> 8;
+    for (uint32_t q = 0; q < al; q++)
+      if (in[ao + q] != in[bo + q]) return false;
+    return true;
+  } else {
+    return a == b;
+  }
+}
+// next value of an RLE stream: FD_NULL for nulls (and past the end, RLEDecoder.readValue)
+template <uint8_t T>
+__device__ __forceinline__ int32_t d32_next(const uint8_t* in, Dec32& d, bool& bad) {
+  if (d.count == 0) {
+    if (d.off == d.end) return FD_NULL;
+    const int32_t c = d32_sleb(in, d, bad);
+    if (c > 1) {
+      const int32_t v = d32_raw<T>(in, d, bad);
+      if ((d.state == 1 || d.state == 2) && d.has_last && !d.last_null && d32_eq<T>(in, v, d.last)) bad = true;
+      d.state = 1; d.last = v; d.has_last = true; d.last_null = false; d.count = c;
+    } else if (c < 0) {
+      if (d.state == 2) bad = true;
+      d.state = 2; d.count = -c;
+    } else if (c == 0) {
+      if (d.state == 3) bad = true;
+      const uint32_t z = d32_uleb(in, d, bad);
+      if (z == 0) bad = true;
+      d.state = 3; d.has_last = true; d.last_null = true; d.count = (int32_t)z;
+    } else {
+      bad = true;  // a repetition of one
+    }
+    if (bad) { d.count = 0; d.off = d.end; return FD_NULL; }
+  }
+  d.count--;
+  if (d.state == 2) {
+    const int32_t v = d32_raw<T>(in, d, bad);
+    if (d.has_last && !d.last_null && d32_eq<T>(in, v, d.last)) bad = true;
+    d.last = v; d.has_last = true; d.last_null = false;
+    return v;
+  }
+  return d.last_null ? FD_NULL : d.last;
+}
+// one op-column stream [off, off + len) -> n cells
+template <uint8_t T>
+__device__ __forceinline__ void d32_stream(const uint8_t* in, uint32_t off, uint32_t len, uint32_t n, int32_t* dst,
+                                           bool& bad) {
+  Dec32 d;
+  d32_init(d, off, len);
+  if constexpr (T == DT_BOOL) {
+    bool cur = true, first = true;
+    for (uint32_t i = 0; i < n; i++) {
+      if (d.count == 0 && d.off == d.end) { dst[i] = 0; continue; }  // past the end: false
+      while (d.count == 0) {
+        const uint32_t c = d32_uleb(in, d, bad);
+        cur = !cur;
+        if (c == 0 && !first) bad = true;
+        first = false;
+        d.count = (int32_t)c;
+        if (bad) break;
+      }
+      if (bad) return;
+      d.count--;
+      dst[i] = cur ? 1 : 0;
+    }
+  } else {
+    for (uint32_t i = 0; i < n; i++) {
+      const int32_t v = d32_next<T>(in, d, bad);
+      if (bad) return;
+      if (v == FD_NULL) { dst[i] = FD_NULL; continue; }
+      if constexpr (T == DT_DELTA) {
+        d.abs += v;
+        if (d.abs <= -0x7fffffffLL || d.abs > 0x7fffffffLL) { bad = true; return; }
+        dst[i] = (int32_t)d.abs;
+      } else {
+        dst[i] = v;
+      }
+    }
+  }
+}
+
 // Canonical column encoder over the values of lanes [0, n) (one value per lane, wave-parallel):
 // runs of equal adjacent values -> repetition / null / literal records (RLEEncoder,
 // encoding.js:558-783), deltas against the previous non-null value (DeltaEncoder :932-951),
@@ -194,7 +321,7 @@ __device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap
 // the column at `out` and returns its length, or ~0u when it would exceed `cap`.
 //   v: value (U / D / B), isnull; S: string bytes at in + soff (len slen), eqs = equal to the
 //   previous lane's string; W: raw bytes at in + soff (len slen).
-__device__ uint32_t enc_col(uint8_t kind, uint32_t n, int64_t v, bool isnull, uint32_t soff, uint32_t slen, bool eqs,
+__device__ __forceinline__ uint32_t enc_col(uint8_t kind, uint32_t n, int64_t v, bool isnull, uint32_t soff, uint32_t slen, bool eqs,
                             const uint8_t* in, uint8_t* out, uint32_t cap) {
   if (n == 0) return 0;
   const uint32_t l = lane();
@@ -202,13 +329,13 @@ __device__ uint32_t enc_col(uint8_t kind, uint32_t n, int64_t v, bool isnull, ui
   const bool nul = act && isnull && kind != EK_W && kind != EK_B;
   if (kind == EK_D) {
     const int32_t pi = incl_max(act && !nul ? (int32_t)l : -1);
-    int32_t prev = __shfl_up(pi, 1, 64);
+    int32_t prev = wave::up1(pi, -1);
     if (l == 0) prev = -1;
     const int64_t pv = __shfl(v, prev < 0 ? 0 : prev, 64);
     if (act && !nul) v -= prev < 0 ? 0 : pv;
   }
-  const int64_t pv = __shfl_up(v, 1, 64);
-  const int32_t pn = __shfl_up((int32_t)nul, 1, 64);
+  const int64_t pv = wave::up1(v, (int64_t)0);
+  const int32_t pn = wave::up1((int32_t)nul, 0);
   bool same = false;
   if (act && l > 0 && kind != EK_W) {
     if (nul) same = pn != 0;
@@ -270,7 +397,13 @@ __device__ uint32_t enc_col(uint8_t kind, uint32_t n, int64_t v, bool isnull, ui
 
 }  // namespace fastdoc
 
-__global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
+// probe builds may ask the register allocator for more waves per SIMD (-DAM_FAST_WAVES=n)
+#ifdef AM_FAST_WAVES
+#define FD_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(AM_FAST_WAVES, 8)))
+#else
+#define FD_WAVES_ATTR
+#endif
+__global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     k_doc_fast(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks, const am_doc_desc* __restrict__ docs,
                const am_known_hash* __restrict__ known, const ChunkInfo* __restrict__ info,
                const DocBounds* __restrict__ bounds, const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base,
@@ -280,6 +413,9 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   const uint32_t l = lane();
   const uint32_t doc = blockIdx.x * FD_DOCS_PER_WG + (threadIdx.x >> 6);
   if (doc >= ndocs) return;
+#ifdef AM_PHASE_CLOCK
+  uint64_t ph_last = clock64();
+#endif
   const am_doc_desc dd = docs[doc];
   const DocBounds b = bounds[doc];
   if (!fast_eligible(b, dd)) return;
@@ -328,17 +464,24 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   }
   const uint8_t* const IN = S + F.input;  // IN[off - a0] = arena[off]
   wsync();
+  FPH(0);
 
   // ---- headers: the base document (lane 0) and one change per lane ----
   DocHdr* dh = reinterpret_cast<DocHdr*>(M + FM_DH);
   ChgHdr* chh = reinterpret_cast<ChgHdr*>(S + F.chg);
   if (l == 0) {
-    if (has_base) bad |= parse_doc_hdr(IN + (base_data - a0), base_len, base_data, *dh) != AM_OK;
+    if (has_base) {
+      uint32_t st;
+      [[clang::always_inline]] st = parse_doc_hdr(IN + (base_data - a0), base_len, base_data, *dh);  // ds_* reads
+      bad |= st != AM_OK;
+    }
     else { dh->nactors = 0; dh->nheads = 0; dh->has_hidx = 0; dh->extra_len = 0; dh->base = 0; }
   }
   if (l < N) {
     const uint64_t cdat = chunks[dd.chg_begin + l].off + info[dd.chg_begin + l].data_off;
-    bad |= parse_change_hdr(IN + (cdat - a0), info[dd.chg_begin + l].data_len, cdat, chh[l]) != AM_OK;
+    uint32_t st;
+    [[clang::always_inline]] st = parse_change_hdr(IN + (cdat - a0), info[dd.chg_begin + l].data_len, cdat, chh[l]);
+    bad |= st != AM_OK;
   }
   wsync();
   FD_CHECK();
@@ -426,13 +569,18 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
     const uint32_t off = RO[2 * l];
     r_len = RO[2 * l + 1];
     bad |= r_len > 32;
-    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t q = 0; q < r_len && q < 32; q++) w[q >> 2] |= (uint32_t)IN[off + q] << (24 - 8 * (q & 3));
 #pragma unroll
-    for (int k = 0; k < 8; k++) RW[8 * l + k] = w[k];
+    for (int k = 0; k < 8; k++) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if ((uint32_t)(4 * k + q) < r_len) w |= (uint32_t)IN[off + 4 * k + q] << (24 - 8 * q);
+      RW[8 * l + k] = w;
+    }
   }
   wsync();
   FD_CHECK();
+  FPH(1);
   // canonical ref (first equal id) and rank of the canonical ids (hex order = bytewise, shorter
   // prefix first: actor_cmp_dev)
   uint8_t* CANON = M + FM_CANON;
@@ -497,6 +645,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   const uint8_t* DPC = M + FM_DPC;
   const uint8_t* RANKDP = M + FM_RANKDP;
 
+  FPH(2);
   // ---- base document change rows (DOCUMENT_COLUMNS, lane per column), then lane per row ----
   int64_t* DCC = reinterpret_cast<int64_t*>(S + F.cells);  // [9][nbc] (+ deps at [9*nbc])
   if (has_base && l < DC_NCOLS) {
@@ -557,7 +706,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
     // clock: seq must count 1, 2, ... per actor in row order (new.js:1654-1660)
     uint32_t before = 0;
     for (uint32_t j = 0; j < nbc; j++) {
-      const uint32_t aj = __shfl(bc_actor, j, 64);
+      const uint32_t aj = wave::bcast(bc_actor, (int)j);
       if (j < l && aj == bc_actor) before++;
     }
     uint32_t* CLK = reinterpret_cast<uint32_t*>(M + FM_CLOCK);
@@ -571,10 +720,11 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   wsync();
   FD_CHECK();
 
+  FPH(3);
   // ---- causal queue, first pass (applyChanges, new.js:1550-1597): every change must be new,
   // ready in list order and carry the next seq of its author ----
   uint32_t prior = 0;  // earlier changes of this call by the same author
-  for (uint32_t j = 0; j < N; j++) prior += (__shfl(a_dp, j, 64) == a_dp && j < l) ? 1u : 0u;
+  for (uint32_t j = 0; j < N; j++) prior += (wave::bcast(a_dp, (int)j) == a_dp && j < l) ? 1u : 0u;
   if (l < N) {
     uint32_t mine[8];
 #pragma unroll
@@ -631,8 +781,8 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
     const uint64_t pre = l < ncand ? bswap64(((uint64_t)HT[8 * l + 1] << 32) | HT[8 * l]) : 0;
     uint32_t pos = 0;
     for (uint32_t y = 0; y < ncand; y++) {
-      const uint64_t py = __shfl(pre, y, 64);
-      const int32_t hy = __shfl((int32_t)ishead, y, 64);
+      const uint64_t py = wave::bcast(pre, (int)y);
+      const int32_t hy = wave::bcast((int32_t)ishead, (int)y);
       if (hy && y != l) {
         if (py < pre) pos++;
         else if (py == pre) bad = true;  // equal 8-byte prefixes: k_doc sorts full hashes
@@ -653,6 +803,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   }
   FD_CHECK();
 
+  FPH(4);
   // ---- op columns: lane per (source, column) stream into 4-byte cells (readOperation,
   // new.js:570-611) ----
   const uint32_t nsrc = (has_base ? 1u : 0u) + N;
@@ -685,51 +836,42 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   if (l < nsrc && s_ne) SRCE[s_ent0] = (int32_t)l;
   FD_CHECK();
   int32_t* CELL = reinterpret_cast<int32_t*>(S + F.cells);
-  for (uint32_t it = l; it < nsrc * 15; it += 64) {
-    const uint32_t s = it / 15, j = it % 15;
-    const uint32_t col = j < OC_VAL_RAW ? j : j + 1;
+  // stream (source s, op column col) -> its cells: rows [ROW0[s], ROW0[s+1]) of cell column j
+  // (j < 13), or entries [ENT0[s], ENT0[s+1]) of entry column j - 13
+  auto stream = [&](uint32_t s, uint32_t col, uint32_t& off, uint32_t& len, uint32_t& n, int32_t*& dst) -> bool {
     const bool chg_src = !(has_base && s == 0);
-    if (chg_src && (col == OC_ID_ACTOR || col == OC_ID_CTR)) continue;  // ids from the header
+    if (chg_src && (col == OC_ID_ACTOR || col == OC_ID_CTR)) return false;  // ids from the header
     const uint32_t c = has_base ? s - 1 : s;
     const uint64_t cbase = chg_src ? chh[c].base : dh->base;
-    const uint32_t coff = chg_src ? chh[c].col_off[col] : dh->ocol_off[col];
-    const uint32_t clen = chg_src ? chh[c].col_len[col] : dh->ocol_len[col];
+    off = (uint32_t)(cbase - a0) + (chg_src ? chh[c].col_off[col] : dh->ocol_off[col]);
+    len = chg_src ? chh[c].col_len[col] : dh->ocol_len[col];
+    const uint32_t j = col < OC_VAL_RAW ? col : col - 1;
     const uint32_t r0 = ROW0[s], e0 = ENT0[s];
-    const uint32_t n = j < 13 ? ROW0[s + 1] - r0 : ENT0[s + 1] - e0;
-    int32_t* dst = j < 13 ? CELL + j * R + r0 : CELL + 13 * R + (j - 13) * E + e0;
-    const uint8_t type = kOpColDec[col];
-    ColDec d;
-    cd_init(d, type, IN + (cbase + coff - a0), clen);
-    for (uint32_t i = 0; i < n; i++) {
-      int32_t cv;
-      uint32_t e;
-      if (type == DT_BOOL) {
-        bool bv;
-        e = cd_next_bool(d, bv);
-        cv = bv ? 1 : 0;
-      } else {
-        bool isnull;
-        uint32_t sl;
-        int64_t x;
-        e = cd_next(d, x, isnull, sl);
-        if (isnull) cv = FD_NULL;
-        else if (type == DT_UTF8) {
-          const uint64_t so = cbase + coff + (uint64_t)x - a0;
-          if (sl > 255) bad = true;
-          cv = (int32_t)((so << 8) | (sl & 255));
-        } else {
-          if (type == DT_DELTA) x = (d.absolute += x);
-          if (x <= -0x7fffffffLL || x > 0x7fffffffLL) bad = true;
-          cv = (int32_t)x;
-        }
-      }
-      if (e) { bad = true; break; }
-      dst[i] = cv;
+    n = j < 13 ? ROW0[s + 1] - r0 : ENT0[s + 1] - e0;
+    dst = j < 13 ? CELL + j * R + r0 : CELL + 13 * R + (j - 13) * E + e0;
+    return true;
+  };
+  // type-uniform rounds: lanes take (source, column) pairs of one decoder type at a time
+  {
+    constexpr uint8_t kU[9] = {OC_OBJ_ACTOR, OC_OBJ_CTR, OC_KEY_ACTOR, OC_ID_ACTOR, OC_ACTION, OC_VAL_LEN,
+                               OC_CHLD_ACTOR, OC_GRP_NUM, OC_GRP_ACTOR};
+    constexpr uint8_t kD[4] = {OC_KEY_CTR, OC_ID_CTR, OC_CHLD_CTR, OC_GRP_CTR};
+    uint32_t off, len, n;
+    int32_t* dst;
+    for (uint32_t it = l; it < nsrc * 9; it += 64)
+      if (stream(it / 9, kU[it % 9], off, len, n, dst)) d32_stream<DT_UINT>(IN, off, len, n, dst, bad);
+    for (uint32_t it = l; it < nsrc * 4; it += 64)
+      if (stream(it / 4, kD[it % 4], off, len, n, dst)) d32_stream<DT_DELTA>(IN, off, len, n, dst, bad);
+    for (uint32_t it = l; it < nsrc * 2; it += 64) {
+      const uint32_t s2 = it >> 1;
+      if (it & 1) { if (stream(s2, OC_INSERT, off, len, n, dst)) d32_stream<DT_BOOL>(IN, off, len, n, dst, bad); }
+      else if (stream(s2, OC_KEY_STR, off, len, n, dst)) d32_stream<DT_UTF8>(IN, off, len, n, dst, bad);
     }
   }
   wsync();
   FD_CHECK();
 
+  FPH(5);
   // ---- rows: lane per op row (gather_row) ----
   const int32_t r_src = incl_max(l < R ? SRCR[l] : -1);
   const bool isrow = l < R;
@@ -830,6 +972,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   if (isrow) bad |= r_idc < 0 || (r_objc != FD_NULL && r_objc < 0);
   FD_CHECK();
 
+  FPH(6);
   // ---- opId order: (counter, actor rank) (new.js:1197-1224) ----
   const uint32_t r_rank = isrow ? RANKDP[r_ida] : 0;
   uint64_t* IDT = reinterpret_cast<uint64_t*>(M + FM_IDT);
@@ -837,7 +980,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   {
     const uint64_t key = isrow ? ((uint64_t)(uint32_t)r_idc << 12) | (r_rank << 6) | l : ~0ull;
     const uint64_t s = sort64(key);
-    const uint64_t prev = __shfl_up(s, 1, 64);
+    const uint64_t prev = wave::up1(s, ~0ull);
     if (l > 0 && l < R && (prev >> 6) == (s >> 6)) bad = true;  // duplicate operation ID
     IDT[l] = s;
     if (l < R) M[FM_OPR + (s & 63)] = (uint8_t)l;
@@ -872,8 +1015,8 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
     while (km) {
       const uint32_t j = (uint32_t)__builtin_ctzll(km);
       km &= km - 1;
-      const uint64_t pj = __shfl(pre, j, 64);
-      const uint32_t kj = (uint32_t)__shfl(r_key, j, 64);
+      const uint64_t pj = wave::bcast(pre, (int)j);
+      const uint32_t kj = (uint32_t)wave::bcast(r_key, (int)j);
       if (!keyed || j == l) continue;
       bool less = pj < pre;
       if (pj == pre) {
@@ -887,6 +1030,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   }
   FD_CHECK();
 
+  FPH(7);
   // ---- preds -> target rows (new.js:1173-1188, 1254-1258) ----
   uint8_t* OWN = M + FM_OWN;
   if (r_chg)
@@ -963,6 +1107,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   const uint64_t r_objkey = (!isrow || r_objc == FD_NULL) ? 0ull
                                                           : (((uint64_t)(uint32_t)r_objc + 1) << 6) | (r_obja < 0 ? 0u : RANKDP[r_obja]);
 
+  FPH(8);
   // ---- RGA order: preorder of the reference-element tree, children by descending opId
   // (new.js:145-163); Euler tour + pointer jumping gives each element its suffix count ----
   int8_t* FC = reinterpret_cast<int8_t*>(M + FM_FC);
@@ -974,7 +1119,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   {
     const uint64_t key = is_el ? (r_objkey << 19) | ((uint64_t)(r_parent + 1) << 12) | ((uint64_t)(63 - r_opr) << 6) | l : ~0ull;
     const uint64_t s = sort64(key);
-    const uint64_t nx = __shfl_down(s, 1, 64), pv = __shfl_up(s, 1, 64);
+    const uint64_t nx = wave::down1(s, ~0ull), pv = wave::up1(s, ~0ull);
     if (s != ~0ull) {
       const uint32_t row = (uint32_t)(s & 63);
       if (l < 63 && nx != ~0ull && (nx >> 12) == (s >> 12)) NS[row] = (int8_t)(nx & 63);
@@ -1016,6 +1161,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   }
   FD_CHECK();
 
+  FPH(9);
   // ---- document order: object, then key (UTF-16) | list position, then opId ----
   const bool isout = isrow && !r_del;
   const uint32_t NOUT = __popcll(__ballot(isout));
@@ -1040,7 +1186,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
     const uint64_t key = e_new ? ((uint64_t)e_tr << 37) | ((uint64_t)e_octr << 6) | e_orank : ~0ull;
     const uint64_t s = sort64(key);
     NSORT[l] = s;
-    const uint64_t pv = __shfl_up(s, 1, 64);
+    const uint64_t pv = wave::up1(s, ~0ull);
     if (s != ~0ull) {
       const uint32_t tg = (uint32_t)(s >> 37);
       if (l == 0 || (pv >> 37) != tg) LON[tg] = (uint8_t)l;
@@ -1086,6 +1232,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   wsync();
   FD_CHECK();
 
+  FPH(10);
   // ---- canonical re-encode into the output image (cells are dead) ----
   uint8_t* const OB = S + F.cells;
   uint32_t* COLLEN = reinterpret_cast<uint32_t*>(M + FM_COLLEN);
@@ -1122,7 +1269,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
       x_len = h.has_extra ? h.extra_len : 0u;
     }
     // message equality with the previous row (S column run detection)
-    const uint32_t pm_off = __shfl_up(m_off, 1, 64), pm_len = __shfl_up(m_len, 1, 64);
+    const uint32_t pm_off = wave::up1(m_off, 0u), pm_len = wave::up1(m_len, 0u);
     bool meq = !m_null && l > 0 && pm_len == m_len;
     for (uint32_t q = 0; meq && q < m_len; q++) meq = IN[pm_off + q] == IN[m_off + q];
     const int64_t dep_new = __shfl(dep_idx, (l - nbd) & 63, 64);
@@ -1150,6 +1297,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
       cur += len;
     }
   }
+  FPH(11);
   FD_CHECK();
   {
     const uint32_t r = k_row;
@@ -1159,7 +1307,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
     const int32_t ida = __shfl(r_ida, r, 64), ins = __shfl((int32_t)r_ins, r, 64), act = __shfl(r_act, r, 64);
     const int32_t vlen = __shfl(r_vlen, r, 64), chc = __shfl(r_chc, r, 64), cha = __shfl(r_cha, r, 64);
     const uint32_t voff = __shfl(r_voff, r, 64), vb = __shfl(r_vb, r, 64), kr = __shfl(r_krank, r, 64);
-    const uint32_t pkr = __shfl_up(kr, 1, 64);
+    const uint32_t pkr = wave::up1(kr, ~0u);
     const uint32_t succ_a = OUTA[l], succ_c = (uint32_t)OUTC[l];
     auto nv = [](int32_t x) -> int64_t { return x == FD_NULL ? AM_NULL64 : (int64_t)x; };
     auto av = [](int32_t x) -> int64_t { return x < 0 ? AM_NULL64 : (int64_t)x; };
@@ -1195,6 +1343,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   }
   wsync();
   FD_CHECK();
+  FPH(12);
   // trailer: heads indexes (all known here) and the base document's extra bytes
   const uint32_t cols_end = cur;
   const uint32_t xlen = has_base ? dh->extra_len : 0u;
@@ -1266,6 +1415,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
       dst[q >> 2] = w;
     }
   }
+  FPH(13);
   if (l < N) chg_state[dd.chg_begin + l] = (int32_t)l;
   if (l == 0) {
     am_doc_result r;
@@ -1289,3 +1439,4 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG)
   }
 #undef FD_CHECK
 }
+#undef FPH

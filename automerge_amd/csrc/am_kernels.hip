@@ -332,7 +332,7 @@ struct NewEnt { int64_t ctr; int32_t target; int32_t actor; int32_t rank; int32_
 // Optional per-phase cycle counters (probe builds only: -DAM_PHASE_CLOCK). Every 64th document
 // adds the s_memtime delta of each phase; read back with amx_phase_cycles().
 #ifdef AM_PHASE_CLOCK
-__device__ unsigned long long am_phase_cycles[16];
+__device__ unsigned long long am_phase_cycles[32];
 #define PH(k)                                                                  \
   do {                                                                         \
     __syncthreads();                                                           \
@@ -578,11 +578,49 @@ void am_launch_sha256(const uint8_t* arena, const am_chunk_desc* msgs, uint32_t 
   hipLaunchKernelGGL(k_sha256, dim3((n + 255) / 256), dim3(256), 0, s, arena, msgs, n, out);
 }
 
+// Self-test of the DPP / permlane primitives (am_wave.h) on the device: one wave, the lane values
+// in[64] -> 16 result rows of 64 lanes (tests/test_gpu_wave.py checks them against numpy)
+__global__ void __launch_bounds__(64) k_wave_selftest(const uint64_t* __restrict__ in, uint64_t* __restrict__ out) {
+  const uint32_t l = threadIdx.x;
+  const uint64_t v = in[l];
+  const uint32_t v32 = (uint32_t)v;
+  uint32_t tot = 0;
+  out[0 * 64 + l] = wave::incl_add(v32);
+  out[1 * 64 + l] = wave::excl_add(v32, tot);
+  out[2 * 64 + l] = tot;
+  out[3 * 64 + l] = (uint64_t)(int64_t)wave::incl_max((int32_t)v32);
+  out[4 * 64 + l] = (uint64_t)wave::max_all((int64_t)v);
+  out[5 * 64 + l] = wave::xor_lane<1>(v);
+  out[6 * 64 + l] = wave::xor_lane<2>(v);
+  out[7 * 64 + l] = wave::xor_lane<4>(v);
+  out[8 * 64 + l] = wave::xor_lane<8>(v);
+  out[9 * 64 + l] = wave::xor_lane<16>(v);
+  out[10 * 64 + l] = wave::xor_lane<32>(v);
+  out[11 * 64 + l] = wave::sort64(v);
+  out[12 * 64 + l] = wave::up1(v, 7ull);
+  out[13 * 64 + l] = wave::down1(v, 9ull);
+  out[14 * 64 + l] = wave::bcast(v, 37);
+  out[15 * 64 + l] = wave::sum_all(v32);
+}
+extern "C" int amx_wave_selftest(const uint64_t* in_host, uint64_t* out_host) {
+  uint64_t *din = nullptr, *dout = nullptr;
+  if (hipMalloc(&din, 64 * 8) != hipSuccess) return 1;
+  if (hipMalloc(&dout, 16 * 64 * 8) != hipSuccess) { (void)hipFree(din); return 1; }
+  int rc = hipMemcpy(din, in_host, 64 * 8, hipMemcpyHostToDevice) != hipSuccess;
+  if (!rc) {
+    hipLaunchKernelGGL(k_wave_selftest, dim3(1), dim3(64), 0, 0, din, dout);
+    rc = hipDeviceSynchronize() != hipSuccess || hipMemcpy(out_host, dout, 16 * 64 * 8, hipMemcpyDeviceToHost) != hipSuccess;
+  }
+  (void)hipFree(din);
+  (void)hipFree(dout);
+  return rc;
+}
+
 #ifdef AM_PHASE_CLOCK
 extern "C" int amx_phase_cycles(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(am_phase_cycles), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(am_phase_cycles), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[16] = {0};
+    unsigned long long z[32] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(am_phase_cycles), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;

@@ -148,6 +148,7 @@ def main():
         "docs_per_sec": tot[0] / (elapsed / k),
         "errors": tot[2], "verified_docs": checked, "input_bytes_per_gpu": in_bytes, "output_bytes_per_gpu": out_bytes,
         "workspace_bytes_per_gpu": int(b.workspace_bytes()), "gen_s": t_gen,
+        "kernel_info": b.kernel_info(),
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))

@@ -169,6 +169,10 @@ int am_batch_digest(am_batch *b, uint64_t first_doc, uint64_t *digest);
 int am_batch_fast_flags(am_batch *b, uint8_t *flags);
 /* Device pointer + size of the staged arena / merged outputs (for bench byte accounting). */
 uint64_t am_batch_workspace_bytes(am_batch *b);
+/* Launch shape of the staged batch's document kernels: out3[0] = k_doc dynamic LDS bytes,
+ * out3[1] = k_doc_fast LDS slice per document (0: none in its envelope), out3[2] = largest k_doc
+ * hot working set. Not part of the reference interface (bench/profiling only). */
+int am_batch_kernel_info(am_batch *b, uint64_t *out3);
 
 /* ---- per-document backend state (mirrors backend/backend.js over the batch path, n = 1) ---- */
 am_doc *am_doc_init(am_engine *eng);

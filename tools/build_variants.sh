@@ -1,0 +1,14 @@
+#!/bin/bash
+# Probe variants of libautomerge_amd.so for A/B runs on the GPU (never shipped):
+#   tools/probe/libam_<name>.so built with extra flags. Usage: tools/build_variants.sh name "-DFOO=1" [...]
+set -e
+cd "$(dirname "$0")/../automerge_amd/csrc"
+F="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -munsafe-fp-atomics"
+mkdir -p ../../tools/probe
+make -s am_capi.o am_workload.o am_sync.o
+while [ $# -ge 2 ]; do
+  name=$1; flags=$2; shift 2
+  /opt/rocm/bin/hipcc $F $flags -c am_kernels.hip -o /tmp/am_kernels_$name.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared -o ../../tools/probe/libam_$name.so /tmp/am_kernels_$name.o am_capi.o am_sync.o am_workload.o -lz -lpthread
+  echo built tools/probe/libam_$name.so
+done

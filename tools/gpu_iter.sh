@@ -1,12 +1,12 @@
-# GPU iteration: parity tests, phase-clock profile, 1-GPU bench (each step time-limited)
+#!/bin/bash
+# One GPU iteration: wave + parity tests, phase clock of the probe build, bench (no CPU baseline).
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-timeout -k 10 400 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/gpu_tests.log
-[ $rc -ne 0 ] && exit $rc
-AM_LIB_PATH=tools/probe/libam_clock.so timeout -k 10 300 python tools/phase_clock.py --docs 65536 > gpurun_out/phase.log 2>&1
-rc=$?; cat gpurun_out/phase.log
-[ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python bench.py --docs 262144 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench.log 2>&1
-rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log
-exit $rc
+mkdir -p gpurun_out/it
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/it/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -30 gpurun_out/it/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/it/gpu_tests.log
+if [ -f tools/probe/libam_clock.so ]; then
+  AM_LIB_PATH=tools/probe/libam_clock.so timeout -k 10 200 python tools/phase_clock.py --docs 131072 > gpurun_out/it/phase.log 2>&1 || { echo "phase failed"; tail -5 gpurun_out/it/phase.log; exit 1; }
+  tail -16 gpurun_out/it/phase.log
+fi
+timeout -k 10 200 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/it/bench.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/it/bench.log; exit 1; }
+python -c "import json; d=json.loads(open('gpurun_out/it/bench.log').read().strip().splitlines()[-1]); print(d['value'], d['stage_ms'])"

@@ -14,6 +14,10 @@ sys.path.insert(0, ROOT)
 NAMES = ["P0 stage input", "P1 headers", "P2a lookups", "P2b plan (serial)", "P4 decode streams+ranks",
          "P4 gather+place", "P5a-c checks+id sort", "P5d-e preds+elements", "P5f RGA", "P5g row sort",
          "P5h succ merge", "P6 encode", "header+copy"]
+FAST = ["F0 status+stage input", "F1 headers+hashes+refs", "F2 canon+actor table", "F3 base change rows",
+        "F4 queue+deps+heads", "F5 op column decode", "F6 rows+entries+checks", "F7 id sort+key rank",
+        "F8 preds+elements", "F9 RGA", "F10 doc order+succ", "F11 encode change cols", "F12 encode op cols",
+        "F13 trailer+header+copy"]
 
 
 def main():
@@ -29,7 +33,7 @@ def main():
     b = Batch(device=0)
     b.stage(arena, chunks, docs)
     b.run(); b.sync()
-    buf = (ctypes.c_ulonglong * 16)()
+    buf = (ctypes.c_ulonglong * 32)()
     f(buf, 1)
     b.run(); b.sync()
     f(buf, 1)
@@ -40,6 +44,14 @@ def main():
         tot += c
         print("%-26s %10.0f cycles/doc" % (n, c))
     print("%-26s %10.0f cycles/doc   k_doc stage ms: %s" % ("total", tot, b.stage_times()))
+    # k_doc_fast: lane 0 of every 16th document
+    sampled = (args.docs + 15) // 16
+    tot = 0
+    for i, n in enumerate(FAST):
+        c = buf[16 + i] / sampled
+        tot += c
+        print("%-26s %10.0f cycles/doc" % (n, c))
+    print("%-26s %10.0f cycles/doc (k_doc_fast)" % ("total", tot))
 
 
 if __name__ == "__main__":
