@@ -280,6 +280,7 @@ struct am_batch {
   DevBuf<am_doc_desc> docs;
   DevBuf<am_known_hash> known;
   DevBuf<ChunkInfo> info;
+  DevBuf<HdrSlot> hdr;
   DevBuf<DocBounds> bounds;
   DevBuf<uint64_t> ws_bytes, ws_off, scan_tmp, ws_total, max_hot;
   DevBuf<uint8_t> fast_done;
@@ -296,7 +297,7 @@ struct am_batch {
 
   BatchDev dev() {
     BatchDev b;
-    b.arena = arena.p; b.chunks = chunks.p; b.docs = docs.p; b.known = known.p; b.info = info.p; b.bounds = bounds.p;
+    b.arena = arena.p; b.chunks = chunks.p; b.docs = docs.p; b.known = known.p; b.info = info.p; b.hdr = hdr.p; b.bounds = bounds.p;
     b.ws_bytes = ws_bytes.p; b.ws_off = ws_off.p; b.scan_tmp = scan_tmp.p; b.ws_total = ws_total.p; b.max_hot = max_hot.p; b.lds_bytes = lds_bytes; b.max_hot_host = max_hot_v; b.ws = ws.p;
     b.fast_lds = fast_lds; b.fast_done = fast_done.p; b.fast_only = fast_only;
     b.ws_cap = ws.cap; b.results = results.p; b.chg_state = chg_state.p; b.nchunks = nchunks; b.ndocs = ndocs;
@@ -360,7 +361,7 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   hipStream_t s = e->stream;
   // 64 bytes of slack: k_doc_fast stages whole 16-byte words of a document's span
   if (!b->arena.ensure(arena_len + 64) || !b->chunks.ensure(nchunks) || !b->docs.ensure(ndocs) || !b->known.ensure(nknown) ||
-      !b->info.ensure(nchunks) || !b->bounds.ensure(ndocs) || !b->ws_bytes.ensure(ndocs) || !b->ws_off.ensure(ndocs) ||
+      !b->info.ensure(nchunks) || !b->hdr.ensure(nchunks) || !b->bounds.ensure(ndocs) || !b->ws_bytes.ensure(ndocs) || !b->ws_off.ensure(ndocs) ||
       !b->scan_tmp.ensure(am_scan_tmp_elems(ndocs)) || !b->ws_total.ensure(1) || !b->max_hot.ensure(2) ||
       !b->fast_done.ensure(ndocs) || !b->results.ensure(ndocs) ||
       !b->chg_state.ensure(nchunks))

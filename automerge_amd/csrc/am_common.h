@@ -29,6 +29,13 @@ enum : int {
 #include "../../include/automerge_amd.h"
 
 // ---- per-chunk summary written by k_chunks (96 bytes) ----
+// Compact parsed header of one chunk (128 B slot per chunk, written by k_chunks when the chunk
+// data is shorter than 64 KiB; read by k_doc_fast instead of re-parsing). Typed views:
+// ChgHdrC / DocHdrC in am_kernels.hip.
+struct alignas(16) HdrSlot {
+  uint8_t b[128];
+};
+
 struct ChunkInfo {
   uint8_t hash[32];
   uint32_t status;          // AM_* code

@@ -49,7 +49,7 @@
 
 // misc region (byte offsets)
 enum : uint32_t {
-  FM_DH = 0,                      // DocHdr (240 B)
+  FM_DH = 0,                      // DocHdrC (128 B)
   FM_BHIDX = 256,                 // int64 [64] base head -> changeIndexByHash index
   FM_KIDX = FM_BHIDX + 512,       // int64 [64] known hash -> index
   FM_IDT = FM_KIDX + 512,         // uint64 [64] sorted op ids (ctr << 12 | rank << 6 | row)
@@ -97,7 +97,7 @@ __host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t n
   F.hashes = take(32 * (b.N + nbh + nknown));
   F.refs = take(40 * nrefs);  // 32 B padded id words + (off, len)
   F.misc = take(FM_TOTAL);
-  F.chg = take((uint32_t)sizeof(ChgHdr) * b.N);
+  F.chg = take((uint32_t)sizeof(ChgHdrC) * b.N);
   const uint32_t nbc = b.C - b.N, nbd = b.D - b.ND;
   uint32_t cells = 4 * (13 * b.R + 2 * b.E);
   const uint32_t dcc = 8 * (9 * nbc + nbd);
@@ -406,7 +406,7 @@ __device__ __forceinline__ uint32_t enc_col(uint8_t kind, uint32_t n, int64_t v,
 __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     k_doc_fast(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks, const am_doc_desc* __restrict__ docs,
                const am_known_hash* __restrict__ known, const ChunkInfo* __restrict__ info,
-               const DocBounds* __restrict__ bounds, const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base,
+               const HdrSlot* __restrict__ hdr, const DocBounds* __restrict__ bounds, const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base,
                uint64_t ws_cap, uint32_t lds_per_doc, uint32_t ndocs, am_doc_result* __restrict__ results,
                int32_t* __restrict__ chg_state, uint8_t* __restrict__ fast_done) {
   using namespace fastdoc;
@@ -443,14 +443,10 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     c_nops = ci.nops; c_nents = ci.nents; c_ndeps = ci.ndeps; c_nact = ci.nactors;
   }
   uint32_t nb = 0, nbe = 0, nbc = 0, nbd = 0;
-  uint64_t base_data = 0;
-  uint32_t base_len = 0;
   if (has_base) {
     const ChunkInfo& ci = info[dd.base_chunk];
     bad |= ci.status != AM_OK || ci.type != 0;
     nb = ci.nops; nbe = ci.nents; nbc = ci.nchg; nbd = ci.ndeps;
-    base_data = chunks[dd.base_chunk].off + ci.data_off;
-    base_len = ci.data_len;
   }
   FD_CHECK();
 
@@ -467,21 +463,18 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   FPH(0);
 
   // ---- headers: the base document (lane 0) and one change per lane ----
-  DocHdr* dh = reinterpret_cast<DocHdr*>(M + FM_DH);
-  ChgHdr* chh = reinterpret_cast<ChgHdr*>(S + F.chg);
-  if (l == 0) {
-    if (has_base) {
-      uint32_t st;
-      [[clang::always_inline]] st = parse_doc_hdr(IN + (base_data - a0), base_len, base_data, *dh);  // ds_* reads
-      bad |= st != AM_OK;
+  DocHdrC* dh = reinterpret_cast<DocHdrC*>(M + FM_DH);
+  ChgHdrC* chh = reinterpret_cast<ChgHdrC*>(S + F.chg);
+  // parsed by k_chunks (compact slots): 8 x 16 B per header, base document first
+  {
+    const uint32_t hb = has_base ? 1u : 0u;
+    const uint4* src_b = reinterpret_cast<const uint4*>(hdr + (has_base ? dd.base_chunk : 0));
+    const uint4* src_c = reinterpret_cast<const uint4*>(hdr + dd.chg_begin);
+    for (uint32_t v = l; v < 8 * (hb + N); v += 64) {
+      if (v < 8 * hb) reinterpret_cast<uint4*>(dh)[v] = src_b[v];
+      else reinterpret_cast<uint4*>(chh)[v - 8 * hb] = src_c[v - 8 * hb];
     }
-    else { dh->nactors = 0; dh->nheads = 0; dh->has_hidx = 0; dh->extra_len = 0; dh->base = 0; }
-  }
-  if (l < N) {
-    const uint64_t cdat = chunks[dd.chg_begin + l].off + info[dd.chg_begin + l].data_off;
-    uint32_t st;
-    [[clang::always_inline]] st = parse_change_hdr(IN + (cdat - a0), info[dd.chg_begin + l].data_len, cdat, chh[l]);
-    bad |= st != AM_OK;
+    if (!has_base && l == 0) { dh->nactors = 0; dh->nheads = 0; dh->has_hidx = 0; dh->extra_len = 0; dh->base = 0; }
   }
   wsync();
   FD_CHECK();
@@ -548,7 +541,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     }
   }
   if (l < N) {
-    const ChgHdr& h = chh[l];
+    const ChgHdrC& h = chh[l];
     const uint32_t r0 = NB + ambase;
     RO[2 * r0] = (uint32_t)(h.base + h.actor_off - a0);
     RO[2 * r0 + 1] = h.actor_len;
@@ -753,7 +746,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   const uint32_t dep_b = __shfl(dbase, dep_c, 64);
   if (l < nd_total) {
     const uint32_t c = dep_c;
-    const ChgHdr& h = chh[c];
+    const ChgHdrC& h = chh[c];
     uint32_t w[8];
     load32(IN + (h.base + h.deps_off + 32 * (l - dep_b) - a0), w);
     int32_t hit = -1;
@@ -1248,7 +1241,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   {
     const uint32_t c = l >= nbc ? l - nbc : 0;
     const uint32_t cs = c & 63;
-    const ChgHdr& h = chh[cs < N ? cs : 0];
+    const ChgHdrC& h = chh[cs < N ? cs : 0];
     const uint32_t n_adp = __shfl(a_dp, cs, 64), n_nd = __shfl(c_ndeps, cs, 64), n_nops = __shfl(c_nops, cs, 64);
     const bool isnew = l >= nbc && l < NC;
     int64_t v_act = bc_actor, v_seq = bc_seq, v_max = bc_max, v_time = bc_time, v_xlen = bc_xlen;

@@ -39,6 +39,25 @@ struct ChgHdr {              // decodeChangeHeader + column info (columnar.js:63
   uint32_t col_off[OC_NCOLS];
   uint32_t col_len[OC_NCOLS];
 };
+// compact forms (u16 offsets/lengths, chunk data < 64 KiB) kept per chunk in HdrSlot
+struct alignas(16) ChgHdrC {
+  uint64_t base;
+  int64_t seq, start_op, time;
+  uint16_t actor_off, actors_off, deps_off, msg_off, extra_off;
+  uint16_t actor_len, nactors, ndeps, msg_len, extra_len, has_extra, pad;
+  uint16_t col_off[OC_NCOLS];
+  uint16_t col_len[OC_NCOLS];
+};
+struct alignas(16) DocHdrC {
+  uint64_t base;
+  uint16_t actors_off, heads_off, hidx_off, extra_off;
+  uint16_t nactors, nheads, has_hidx, extra_len;
+  uint16_t ccol_off[DC_NCOLS];
+  uint16_t ccol_len[DC_NCOLS];
+  uint16_t ocol_off[OC_NCOLS];
+  uint16_t ocol_len[OC_NCOLS];
+};
+static_assert(sizeof(ChgHdrC) <= sizeof(HdrSlot) && sizeof(DocHdrC) <= sizeof(HdrSlot), "HdrSlot");
 struct DocHdr {              // decodeDocumentHeader (columnar.js:1006-1038)
   uint64_t base;
   uint32_t actors_off, heads_off, hidx_off, extra_off;
@@ -152,7 +171,8 @@ __device__ static uint32_t parse_doc_hdr(const uint8_t* data, uint64_t n, uint64
 // k_chunks: one thread per chunk
 // ------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_chunks(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
-                                                uint32_t nchunks, ChunkInfo* __restrict__ info) {
+                                                uint32_t nchunks, ChunkInfo* __restrict__ info,
+                                                HdrSlot* __restrict__ hdr) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nchunks) return;
   am_chunk_desc cd = chunks[i];
@@ -185,6 +205,16 @@ __global__ void __launch_bounds__(256) k_chunks(const uint8_t* __restrict__ aren
       if (r.off != cd.len) { st = AM_E_CHANGE_TRAILING; break; }
       ChgHdr hh;
       if ((st = parse_change_hdr(data, len, cd.off + at, hh))) break;
+      if (len < 65536) {
+        ChgHdrC c;
+        c.base = hh.base; c.seq = hh.seq; c.start_op = hh.start_op; c.time = hh.time;
+        c.actor_off = hh.actor_off; c.actors_off = hh.actors_off; c.deps_off = hh.deps_off; c.msg_off = hh.msg_off;
+        c.extra_off = hh.extra_off; c.actor_len = hh.actor_len; c.nactors = hh.nactors; c.ndeps = hh.ndeps;
+        c.msg_len = hh.msg_len; c.extra_len = hh.extra_len; c.has_extra = hh.has_extra; c.pad = 0;
+#pragma unroll
+        for (int k = 0; k < OC_NCOLS; k++) { c.col_off[k] = hh.col_off[k]; c.col_len[k] = hh.col_len[k]; }
+        *reinterpret_cast<ChgHdrC*>(hdr + i) = c;
+      }
       ci.ndeps = hh.ndeps;
       ci.nactors = hh.nactors;
       uint64_t cnt, sum;
@@ -201,6 +231,17 @@ __global__ void __launch_bounds__(256) k_chunks(const uint8_t* __restrict__ aren
       if (r.off != cd.len) { st = AM_E_DOC_TRAILING; break; }
       DocHdr dh;
       if ((st = parse_doc_hdr(data, len, cd.off + at, dh))) break;
+      if (len < 65536) {
+        DocHdrC c;
+        c.base = dh.base; c.actors_off = dh.actors_off; c.heads_off = dh.heads_off; c.hidx_off = dh.hidx_off;
+        c.extra_off = dh.extra_off; c.nactors = dh.nactors; c.nheads = dh.nheads; c.has_hidx = dh.has_hidx;
+        c.extra_len = dh.extra_len;
+#pragma unroll
+        for (int k = 0; k < DC_NCOLS; k++) { c.ccol_off[k] = dh.ccol_off[k]; c.ccol_len[k] = dh.ccol_len[k]; }
+#pragma unroll
+        for (int k = 0; k < OC_NCOLS; k++) { c.ocol_off[k] = dh.ocol_off[k]; c.ocol_len[k] = dh.ocol_len[k]; }
+        *reinterpret_cast<DocHdrC*>(hdr + i) = c;
+      }
       ci.nactors = dh.nactors;
       ci.nheads = dh.nheads;
       uint64_t cnt, sum;
@@ -490,7 +531,7 @@ __global__ void __launch_bounds__(256) k_max_hot(const DocBounds* __restrict__ b
 
 void am_launch_chunks(const BatchDev& b, hipStream_t s) {
   if (!b.nchunks) return;
-  hipLaunchKernelGGL(k_chunks, dim3((b.nchunks + 255) / 256), dim3(256), 0, s, b.arena, b.chunks, b.nchunks, b.info);
+  hipLaunchKernelGGL(k_chunks, dim3((b.nchunks + 255) / 256), dim3(256), 0, s, b.arena, b.chunks, b.nchunks, b.info, b.hdr);
 }
 void am_launch_bounds(const BatchDev& b, hipStream_t s) {
   if (!b.ndocs) return;
@@ -513,7 +554,7 @@ void am_launch_doc(const BatchDev& b, hipStream_t s) {
   if (b.fast_lds && b.fast_done) {
     (void)hipMemsetAsync(b.fast_done, 0, b.ndocs, s);
     hipLaunchKernelGGL(k_doc_fast, dim3((b.ndocs + FD_DOCS_PER_WG - 1) / FD_DOCS_PER_WG), dim3(64 * FD_DOCS_PER_WG),
-                       FD_DOCS_PER_WG * b.fast_lds, s, b.arena, b.chunks, b.docs, b.known, b.info, b.bounds, b.ws_off, b.ws,
+                       FD_DOCS_PER_WG * b.fast_lds, s, b.arena, b.chunks, b.docs, b.known, b.info, b.hdr, b.bounds, b.ws_off, b.ws,
                        b.ws_cap, b.fast_lds, b.ndocs, b.results, b.chg_state, b.fast_done);
     fd = b.fast_done;
   }

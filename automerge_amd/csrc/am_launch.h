@@ -11,6 +11,7 @@ struct BatchDev {
   const am_doc_desc* docs;
   const am_known_hash* known;
   ChunkInfo* info;
+  HdrSlot* hdr;            // per chunk: compact parsed header (k_chunks)
   DocBounds* bounds;
   uint64_t* ws_bytes;      // per doc
   uint64_t* ws_off;        // per doc (exclusive scan)
