@@ -395,6 +395,115 @@ __device__ __forceinline__ uint32_t enc_col(uint8_t kind, uint32_t n, int64_t v,
   return total;
 }
 
+// LEB128 lengths in closed form (32-bit): ceil(significant bits / 7), bits / 7 as (x * 37) >> 8
+__device__ __forceinline__ uint32_t uleb_len32(uint32_t v) { return ((32u - __clz(v | 1u) + 6u) * 37u) >> 8; }
+__device__ __forceinline__ uint32_t sleb_len32(int32_t v) {
+  return ((33u - __clz((uint32_t)(v ^ (v >> 31))) + 6u) * 37u) >> 8;
+}
+__device__ __forceinline__ uint8_t* put_uleb32(uint8_t* o, uint32_t v) {
+  const uint32_t n = uleb_len32(v);
+  for (uint32_t k = 0; k + 1 < n; k++) o[k] = (uint8_t)(((v >> (7 * k)) & 0x7f) | 0x80);
+  o[n - 1] = (uint8_t)(v >> (7 * (n - 1)));
+  return o + n;
+}
+__device__ __forceinline__ uint8_t* put_sleb32(uint8_t* o, int32_t v) {
+  const uint32_t n = sleb_len32(v);
+  for (uint32_t k = 0; k + 1 < n; k++) o[k] = (uint8_t)(((v >> (7 * k)) & 0x7f) | 0x80);
+  o[n - 1] = (uint8_t)((v >> (7 * (n - 1))) & 0x7f);
+  return o + n;
+}
+// enc_col for 31-bit values with the column kind fixed at compile time (op columns and every
+// document change column but time). Unsigned / delta inputs must be >= 0 (else `bad`).
+template <uint8_t K>
+__device__ __forceinline__ uint32_t enc32(uint32_t n, int32_t v, bool isnull, uint32_t soff, uint32_t slen, bool eqs,
+                                          const uint8_t* in, uint8_t* out, uint32_t cap, bool& bad) {
+  if (n == 0) return 0;
+  const uint32_t l = lane();
+  const bool act = l < n;
+  const bool nul = (K == EK_W || K == EK_B) ? false : (act && isnull);
+  if constexpr (K == EK_U || K == EK_D) {
+    if (act && !nul && v < 0) bad = true;
+  }
+  if constexpr (K == EK_D) {
+    const int32_t pi = incl_max(act && !nul ? (int32_t)l : -1);
+    const int32_t prev = wave::up1(pi, -1);
+    const int32_t pv = __shfl(v, prev < 0 ? 0 : prev, 64);
+    if (act && !nul) v -= prev < 0 ? 0 : pv;
+  }
+  const int32_t pv = wave::up1(v, 0);
+  const uint32_t pn = wave::up1((uint32_t)nul, 0u);
+  bool same = false;
+  if (K != EK_W && act && l > 0) {
+    if (nul) same = pn != 0;
+    else if (pn) same = false;
+    else if constexpr (K == EK_S) same = eqs;
+    else same = pv == v;
+  }
+  const bool st = act && !same;
+  const uint64_t M = __ballot(st);
+  const uint64_t above = l == 63 ? 0ull : (M >> (l + 1));
+  const uint32_t rl = (above ? l + 1 + ctz64(above) : n) - l;
+  uint32_t bytes = 0, gcnt = 0;
+  bool gs = false;
+  if constexpr (K == EK_W) {
+    bytes = act ? slen : 0;
+  } else if constexpr (K == EK_B) {
+    bytes = st ? uleb_len32(rl) + ((l == 0 && v) ? 1u : 0u) : 0u;
+  } else {
+    if (!__any(act && !nul)) return 0;  // nulls only: nothing is written (RLEEncoder.finish)
+    const bool single = st && !nul && rl == 1;
+    const uint64_t SM = __ballot(single);
+    gs = single && !(l > 0 && ((SM >> (l - 1)) & 1));
+    gcnt = gs ? ctz64(~(SM >> l)) : 0;
+    uint32_t vs;
+    if constexpr (K == EK_U) vs = uleb_len32((uint32_t)v);
+    else if constexpr (K == EK_D) vs = sleb_len32(v);
+    else vs = uleb_len32(slen) + slen;
+    if (st) {
+      if (nul) bytes = 1 + uleb_len32(rl);
+      else if (rl >= 2) bytes = sleb_len32((int32_t)rl) + vs;
+      else bytes = vs + (gs ? sleb_len32(-(int32_t)gcnt) : 0u);
+    }
+  }
+  uint32_t total;
+  const uint32_t off = excl_add(bytes, total);
+  if (total > cap) return ~0u;
+  if (bytes) {
+    uint8_t* o = out + off;
+    if constexpr (K == EK_W) {
+      for (uint32_t q = 0; q < slen; q++) o[q] = in[soff + q];
+    } else if constexpr (K == EK_B) {
+      if (l == 0 && v) *o++ = 0;
+      put_uleb32(o, rl);
+    } else {
+      if (nul) {
+        *o++ = 0;
+        put_uleb32(o, rl);
+      } else {
+        if (rl >= 2) o = put_sleb32(o, (int32_t)rl);
+        else if (gs) o = put_sleb32(o, -(int32_t)gcnt);
+        if constexpr (K == EK_U) put_uleb32(o, (uint32_t)v);
+        else if constexpr (K == EK_D) put_sleb32(o, v);
+        else {
+          o = put_uleb32(o, slen);
+          for (uint32_t q = 0; q < slen; q++) o[q] = in[soff + q];
+        }
+      }
+    }
+  }
+  return total;
+}
+__device__ __forceinline__ uint32_t enc32k(uint8_t kind, uint32_t n, int32_t v, bool isnull, uint32_t soff, uint32_t slen,
+                                           bool eqs, const uint8_t* in, uint8_t* out, uint32_t cap, bool& bad) {
+  switch (kind) {
+    case EK_U: return enc32<EK_U>(n, v, isnull, soff, slen, eqs, in, out, cap, bad);
+    case EK_D: return enc32<EK_D>(n, v, isnull, soff, slen, eqs, in, out, cap, bad);
+    case EK_S: return enc32<EK_S>(n, v, isnull, soff, slen, eqs, in, out, cap, bad);
+    case EK_B: return enc32<EK_B>(n, v, isnull, soff, slen, eqs, in, out, cap, bad);
+    default: return enc32<EK_W>(n, v, isnull, soff, slen, eqs, in, out, cap, bad);
+  }
+}
+
 }  // namespace fastdoc
 
 // probe builds may ask the register allocator for more waves per SIMD (-DAM_FAST_WAVES=n)
@@ -1267,24 +1376,32 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     for (uint32_t q = 0; meq && q < m_len; q++) meq = IN[pm_off + q] == IN[m_off + q];
     const int64_t dep_new = __shfl(dep_idx, (l - nbd) & 63, 64);
     const int64_t v_deps = l < nbd ? bc_dep : dep_new;
+    // 31-bit values go through enc32; time keeps the 64-bit encoder
+    const bool act = l < NC;
+    bad |= act && (v_act < 0 || v_act > 0x7fffffff || v_seq < 0 || v_seq > 0x7fffffff || v_max < 0 || v_max > 0x7fffffff ||
+                   (v_xlen != AM_NULL64 && (v_xlen < 0 || v_xlen > 0x7fffffff)));
+    bad |= l < ND && (v_deps < 0 || v_deps > 0x7fffffff);
 #pragma unroll 1
     for (int col = 0; col < DC_NCOLS; col++) {
-      int64_t v = 0;
-      bool nul = false;
-      uint32_t so = 0, sl = 0, n = NC;
-      switch (col) {
-        case DC_ACTOR: v = v_act; break;
-        case DC_SEQ: v = v_seq; break;
-        case DC_MAXOP: v = v_max; break;
-        case DC_TIME: v = v_time; break;
-        case DC_MESSAGE: nul = m_null; so = m_off; sl = m_len; break;
-        case DC_DEPS_NUM: v = v_nd; break;
-        case DC_DEPS_INDEX: v = v_deps; n = ND; break;
-        case DC_EXTRA_LEN: v = v_xlen; break;
-        default: so = x_off; sl = x_len; break;
+      uint32_t len;
+      if (col == DC_TIME) {
+        len = enc_col(EK_D, NC, v_time, v_time == AM_NULL64, 0, 0, false, IN, OB + cur, F.cells_cap - cur);
+      } else {
+        int32_t v = 0;
+        bool nul = false;
+        uint32_t so = 0, sl = 0, n = NC;
+        switch (col) {
+          case DC_ACTOR: v = (int32_t)v_act; break;
+          case DC_SEQ: v = (int32_t)v_seq; break;
+          case DC_MAXOP: v = (int32_t)v_max; break;
+          case DC_MESSAGE: nul = m_null; so = m_off; sl = m_len; break;
+          case DC_DEPS_NUM: v = (int32_t)v_nd; break;
+          case DC_DEPS_INDEX: v = (int32_t)v_deps; n = ND; break;
+          case DC_EXTRA_LEN: nul = v_xlen == AM_NULL64; v = (int32_t)v_xlen; break;
+          default: so = x_off; sl = x_len; break;
+        }
+        len = enc32k(kEncKind[OC_NCOLS + col], n, v, nul, so, sl, meq, IN, OB + cur, F.cells_cap - cur, bad);
       }
-      if (v == AM_NULL64) nul = true;
-      const uint32_t len = enc_col(kEncKind[OC_NCOLS + col], n, v, nul, so, sl, meq, IN, OB + cur, F.cells_cap - cur);
       if (len == ~0u) { bad = true; break; }
       if (l == 0) COLLEN[OC_NCOLS + col] = len;
       cur += len;
@@ -1302,33 +1419,31 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     const uint32_t voff = __shfl(r_voff, r, 64), vb = __shfl(r_vb, r, 64), kr = __shfl(r_krank, r, 64);
     const uint32_t pkr = wave::up1(kr, ~0u);
     const uint32_t succ_a = OUTA[l], succ_c = (uint32_t)OUTC[l];
-    auto nv = [](int32_t x) -> int64_t { return x == FD_NULL ? AM_NULL64 : (int64_t)x; };
-    auto av = [](int32_t x) -> int64_t { return x < 0 ? AM_NULL64 : (int64_t)x; };
 #pragma unroll 1
     for (int col = 0; col < OC_NCOLS; col++) {
-      int64_t v = 0;
+      int32_t v = 0;
+      bool nul = false;
       uint32_t so = 0, sl = 0, n = NOUT;
       switch (col) {
-        case OC_OBJ_ACTOR: v = av(obja); break;
-        case OC_OBJ_CTR: v = nv(objc); break;
-        case OC_KEY_ACTOR: v = av(keya); break;
-        case OC_KEY_CTR: v = nv(keyc); break;
-        case OC_KEY_STR: v = key == FD_NULL ? AM_NULL64 : 0; so = (uint32_t)key >> 8; sl = (uint32_t)key & 255; break;
+        case OC_OBJ_ACTOR: v = obja; nul = obja < 0; break;
+        case OC_OBJ_CTR: v = objc; nul = objc == FD_NULL; break;
+        case OC_KEY_ACTOR: v = keya; nul = keya < 0; break;
+        case OC_KEY_CTR: v = keyc; nul = keyc == FD_NULL; break;
+        case OC_KEY_STR: nul = key == FD_NULL; so = (uint32_t)key >> 8; sl = (uint32_t)key & 255; break;
         case OC_ID_ACTOR: v = ida; break;
         case OC_ID_CTR: v = idc; break;
         case OC_INSERT: v = ins; break;
         case OC_ACTION: v = act; break;
-        case OC_VAL_LEN: v = nv(vlen); break;
+        case OC_VAL_LEN: v = vlen; nul = vlen == FD_NULL; break;
         case OC_VAL_RAW: so = voff; sl = vb; break;
-        case OC_CHLD_ACTOR: v = av(cha); break;
-        case OC_CHLD_CTR: v = nv(chc); break;
-        case OC_GRP_NUM: v = sc_k; break;
-        case OC_GRP_ACTOR: v = succ_a; n = NSUCC; break;
-        default: v = succ_c; n = NSUCC; break;
+        case OC_CHLD_ACTOR: v = cha; nul = cha < 0; break;
+        case OC_CHLD_CTR: v = chc; nul = chc == FD_NULL; break;
+        case OC_GRP_NUM: v = (int32_t)sc_k; break;
+        case OC_GRP_ACTOR: v = (int32_t)succ_a; n = NSUCC; break;
+        default: v = (int32_t)succ_c; n = NSUCC; break;
       }
-      const bool nul = out && v == AM_NULL64;
       const bool eqs = col == OC_KEY_STR && key != FD_NULL && pkr == kr;
-      const uint32_t len = enc_col(kEncKind[col], n, v, nul, so, sl, eqs, IN, OB + cur, F.cells_cap - cur);
+      const uint32_t len = enc32k(kEncKind[col], n, v, nul && out, so, sl, eqs, IN, OB + cur, F.cells_cap - cur, bad);
       if (len == ~0u) { bad = true; break; }
       if (l == 0) COLLEN[col] = len;
       cur += len;
