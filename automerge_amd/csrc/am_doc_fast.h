@@ -47,21 +47,25 @@
 #define FD_DOCS_PER_WG 4
 #define FD_NULL ((int32_t)0x80000000)
 
-// misc region (byte offsets)
+// misc region (byte offsets). Tables whose phases never overlap share a union slot:
+//   U1: {BHIDX, KIDX} (headers .. heads) | {IDT} (opId sort .. list elements) | {NSORT, BENT} (succ)
+//   U2: {CLOCK, FIRST} (actor table .. queue) | {SRCR, SRCE} (decode .. rows) | {CNTN} (succ)
 enum : uint32_t {
   FM_DH = 0,                      // DocHdrC (128 B)
-  FM_BHIDX = 256,                 // int64 [64] base head -> changeIndexByHash index
-  FM_KIDX = FM_BHIDX + 512,       // int64 [64] known hash -> index
-  FM_IDT = FM_KIDX + 512,         // uint64 [64] sorted op ids (ctr << 12 | rank << 6 | row)
-  FM_NSORT = FM_IDT + 512,        // uint64 [64] sorted new succ entries
-  FM_BENT = FM_NSORT + 512,       // uint64 [64] base entries (ctr << 6 | rank)
-  FM_OUTC = FM_BENT + 512,        // int32 [64] output succ ctr
-  FM_SRCR = FM_OUTC + 256,        // int32 [64] row -> source marks
-  FM_SRCE = FM_SRCR + 256,        // int32 [64] entry -> source marks
-  FM_CNTN = FM_SRCE + 256,        // uint32 [64] new succs per target row
-  FM_CLOCK = FM_CNTN + 256,       // uint32 [64] base clock per doc actor
-  FM_FIRST = FM_CLOCK + 256,      // uint32 [64] first change authored by a canonical ref
-  FM_ROW0 = FM_FIRST + 256,       // uint32 [65] first row of each source
+  FM_U1 = 128,                    // 1024 B union
+  FM_BHIDX = FM_U1,               //   int64 [64] base head -> changeIndexByHash index
+  FM_KIDX = FM_U1 + 512,          //   int64 [64] known hash -> index
+  FM_IDT = FM_U1,                 //   uint64 [64] sorted op ids (ctr << 12 | rank << 6 | row)
+  FM_NSORT = FM_U1,               //   uint64 [64] sorted new succ entries
+  FM_BENT = FM_U1 + 512,          //   uint64 [64] base entries (ctr << 6 | rank)
+  FM_U2 = FM_U1 + 1024,           // 512 B union
+  FM_CLOCK = FM_U2,               //   uint32 [64] base clock per doc actor
+  FM_FIRST = FM_U2 + 256,         //   uint32 [64] first change authored by a canonical ref
+  FM_SRCR = FM_U2,                //   int32 [64] row -> source marks
+  FM_SRCE = FM_U2 + 256,          //   int32 [64] entry -> source marks
+  FM_CNTN = FM_U2,                //   uint32 [64] new succs per target row
+  FM_OUTC = FM_U2 + 512,          // int32 [64] output succ ctr
+  FM_ROW0 = FM_OUTC + 256,        // uint32 [65] first row of each source
   FM_ENT0 = FM_ROW0 + 272,        // uint32 [65] first entry of each source
   FM_COLLEN = FM_ENT0 + 272,      // uint32 [32] encoded column lengths
   FM_OWN = FM_COLLEN + 128,       // uint8 [64] owner row of each entry
@@ -77,8 +81,8 @@ enum : uint32_t {
   FM_DEPD = FM_LON + 64,          // uint8 [128] hash candidate is depended on
   FM_OUTA = FM_DEPD + 128,        // uint8 [64] output succ actor
   FM_DOWN = FM_OUTA + 64,         // uint8 [64] owner change of each dep slot
-  FM_HOUT = FM_DOWN + 64,         // uint8 [64 * 32] sorted heads
-  FM_HIDX = FM_HOUT + 2048,       // int64 [64] sorted heads' indexes
+  FM_HSEL = FM_DOWN + 64,         // uint8 [64] hash-table slot of each sorted head
+  FM_HIDX = FM_HSEL + 64,         // int64 [64] sorted heads' indexes
   FM_TOTAL = FM_HIDX + 512
 };
 
@@ -103,7 +107,8 @@ __host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t n
   const uint32_t dcc = 8 * (9 * nbc + nbd);
   if (dcc > cells) cells = dcc;
   // output image: header (actors, heads, column table) + columns + heads indexes + extra bytes
-  const uint32_t out = 64 + 40 * b.A + 42 * b.H + 25 * 12 + span + 1024;
+  // (a larger image fails the encoder's capacity check: the document then goes to k_doc)
+  const uint32_t out = 64 + 40 * b.A + 42 * b.H + 25 * 12 + span;
   if (out > cells) cells = out;
   F.cells = take(cells);
   F.cells_cap = cells;
@@ -506,12 +511,12 @@ __device__ __forceinline__ uint32_t enc32k(uint8_t kind, uint32_t n, int32_t v, 
 
 }  // namespace fastdoc
 
-// probe builds may ask the register allocator for more waves per SIMD (-DAM_FAST_WAVES=n)
-#ifdef AM_FAST_WAVES
-#define FD_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(AM_FAST_WAVES, 8)))
-#else
-#define FD_WAVES_ATTR
+// registers for three waves per SIMD (<= 168 VGPRs): with the LDS slice of a C4 document (~13 KB)
+// three 4-document workgroups fit a CU. Probe builds may ask for another count (-DAM_FAST_WAVES=n).
+#ifndef AM_FAST_WAVES
+#define AM_FAST_WAVES 3
 #endif
+#define FD_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(AM_FAST_WAVES, 8)))
 __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     k_doc_fast(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks, const am_doc_desc* __restrict__ docs,
                const am_known_hash* __restrict__ known, const ChunkInfo* __restrict__ info,
@@ -895,9 +900,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
       const int64_t hidx = l < N ? (int64_t)nbc + l : reinterpret_cast<const int64_t*>(M + FM_BHIDX)[l - N];
       bad |= hidx < 0;
       reinterpret_cast<int64_t*>(M + FM_HIDX)[pos] = hidx;
-      uint4* ho = reinterpret_cast<uint4*>(M + FM_HOUT + 32 * pos);
-      ho[0] = reinterpret_cast<const uint4*>(HT + 8 * l)[0];
-      ho[1] = reinterpret_cast<const uint4*>(HT + 8 * l)[1];
+      M[FM_HSEL + pos] = (uint8_t)l;
       uint4* hg = reinterpret_cast<uint4*>(wsg + L.heads + 32 * pos);
       hg[0] = reinterpret_cast<const uint4*>(HT + 8 * l)[0];
       hg[1] = reinterpret_cast<const uint4*>(HT + 8 * l)[1];
@@ -1491,7 +1494,8 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
       for (uint32_t q = 0; q < a_len; q++) o[q] = IN[src + q];
     }
     const uint32_t hbytes0 = heads0 + uleb_len(NH);
-    for (uint32_t q = l; q < 32 * NH; q += 64) OB[hbytes0 + q] = M[FM_HOUT + q];
+    for (uint32_t q = l; q < 32 * NH; q += 64)
+      OB[hbytes0 + q] = reinterpret_cast<const uint8_t*>(HT + 8 * M[FM_HSEL + (q >> 5)])[q & 31];
     if (l == 0) {
       uint8_t* o = OB + start;
       for (int k = 0; k < 4; k++) *o++ = kMagic[k];
