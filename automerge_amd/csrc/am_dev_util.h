@@ -46,40 +46,59 @@ __device__ __forceinline__ void sha256_compress(uint32_t h[8], uint32_t w[16]) {
   h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
 }
 
-// Hash of p[0..len). Reads whole big-endian words where possible.
-__device__ static void sha256_dev(const uint8_t* p, uint64_t len, uint8_t out[32]) {
-  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+// Hash of p[0..len): message words come from aligned 32-bit loads funnel-shifted by the
+// message's byte misalignment (v_alignbyte, shift in bytes), 17 loads per 64-byte block instead of 64 byte
+// loads. Reads up to 4 bytes past the last message byte's word: every caller's buffer has slack
+// (the arena and the staging slices carry >= 16 bytes of it).
+__device__ __forceinline__ void sha256_words(const uint8_t* p, uint64_t len, uint32_t h[8]) {
+  h[0] = 0x6a09e667; h[1] = 0xbb67ae85; h[2] = 0x3c6ef372; h[3] = 0xa54ff53a;
+  h[4] = 0x510e527f; h[5] = 0x9b05688c; h[6] = 0x1f83d9ab; h[7] = 0x5be0cd19;
+  const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+  const uint32_t* w0 = reinterpret_cast<const uint32_t*>(p - sh);
+  // little-endian word of message bytes [4k, 4k + 4)
+  auto word_le = [&](uint64_t k) -> uint32_t {
+    const uint32_t lo = w0[k], hi = w0[k + 1];
+    return sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+  };
   uint32_t w[16];
-  uint64_t nfull = len / 64;
+  const uint64_t nfull = len / 64;
   for (uint64_t blk = 0; blk < nfull; blk++) {
-    const uint8_t* q = p + blk * 64;
-#pragma unroll
-    for (int i = 0; i < 16; i++)
-      w[i] = (uint32_t)q[4 * i] << 24 | (uint32_t)q[4 * i + 1] << 16 | (uint32_t)q[4 * i + 2] << 8 | q[4 * i + 3];
-    sha256_compress(h, w);
-  }
-  uint32_t rem = (uint32_t)(len - nfull * 64);
-  const uint8_t* q = p + nfull * 64;
-  int nblk = (rem + 9 <= 64) ? 1 : 2;
-  uint64_t bits = len * 8;
-  for (int b = 0; b < nblk; b++) {
+    uint32_t lo = w0[16 * blk];
 #pragma unroll
     for (int i = 0; i < 16; i++) {
-      uint32_t word = 0;
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        uint32_t pos = b * 64 + 4 * i + k;
-        uint32_t byte;
-        if (pos < rem) byte = q[pos];
-        else if (pos == rem) byte = 0x80;
-        else if (b == nblk - 1 && 4 * i + k >= 56) byte = (uint32_t)(bits >> (8 * (63 - (4 * i + k)))) & 0xff;
-        else byte = 0;
-        word = (word << 8) | byte;
-      }
-      w[i] = word;
+      const uint32_t hi = w0[16 * blk + i + 1];
+      w[i] = __builtin_bswap32(sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo);
+      lo = hi;
     }
     sha256_compress(h, w);
   }
+  const uint32_t rem = (uint32_t)(len - nfull * 64);
+  const uint64_t kt = 16 * nfull;  // first word of the tail
+  const int nblk = (rem + 9 <= 64) ? 1 : 2;
+  const uint64_t bits = len * 8;
+  for (int b = 0; b < nblk; b++) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const uint32_t pos = 64 * b + 4 * i;  // tail byte position of this word
+      uint32_t le = 0;
+      if (pos < rem) {
+        le = word_le(kt + 16 * b + i);
+        const uint32_t cnt = rem - pos;
+        if (cnt < 4) le = (le & ((1u << (8 * cnt)) - 1)) | (0x80u << (8 * cnt));
+      } else if (pos == rem) {
+        le = 0x80;
+      }
+      uint32_t be = __builtin_bswap32(le);
+      if (b == nblk - 1 && i == 14) be = (uint32_t)(bits >> 32);
+      if (b == nblk - 1 && i == 15) be = (uint32_t)bits;
+      w[i] = be;
+    }
+    sha256_compress(h, w);
+  }
+}
+__device__ static void sha256_dev(const uint8_t* p, uint64_t len, uint8_t out[32]) {
+  uint32_t h[8];
+  sha256_words(p, len, h);
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     out[4 * k] = h[k] >> 24; out[4 * k + 1] = h[k] >> 16; out[4 * k + 2] = h[k] >> 8; out[4 * k + 3] = h[k];
@@ -391,6 +410,13 @@ __device__ static uint32_t rle_count_sum(const uint8_t* p, uint64_t n, bool is_s
     }
   }
   return AM_OK;
+}
+
+__device__ __forceinline__ uint32_t rle_count_sum_i(const uint8_t* p, uint64_t n, bool is_str, uint64_t& count, uint64_t& sum,
+                                                int sum_shift, bool is_signed = false) {
+  uint32_t st;
+  [[clang::always_inline]] st = rle_count_sum(p, n, is_str, count, sum, sum_shift, is_signed);
+  return st;
 }
 
 // UTF-8 well-formedness (WHATWG decoder would substitute U+FFFD otherwise)

@@ -70,11 +70,15 @@ struct DocHdr {              // decodeDocumentHeader (columnar.js:1006-1038)
 
 // Column table (decodeColumnInfo, columnar.js:609) -> spec slots; the data follows in table
 // order, i.e. ascending id order, so a second pass assigns offsets in spec order.
-__device__ static uint32_t parse_cols(Rd& r, const uint8_t* spec, int nspec, uint32_t* len, bool is_change) {
+// NSPEC is a compile-time constant so the slot writes are predicated register moves rather than
+// a dynamically indexed (scratch) array
+template <int NSPEC>
+__device__ __forceinline__ uint32_t parse_cols(Rd& r, const uint8_t* spec, uint32_t* len, bool is_change) {
   int64_t num;
   TRY(rd_u53(r, num));
   int64_t last = -1;
-  for (int i = 0; i < nspec; i++) len[i] = 0;
+#pragma unroll
+  for (int i = 0; i < NSPEC; i++) len[i] = 0;
   for (int64_t i = 0; i < num; i++) {
     int64_t id, l;
     TRY(rd_u53(r, id));
@@ -83,16 +87,19 @@ __device__ static uint32_t parse_cols(Rd& r, const uint8_t* spec, int nspec, uin
     last = id;
     if (is_change && (id & COL_DEFLATE)) return AM_E_CHANGE_DEFLATED_COL;
     if (id & COL_DEFLATE) return AM_U_VALUE;  // the host stage inflates document columns
-    int k = -1;
-    for (int j = 0; j < nspec; j++) if (spec[j] == id) k = j;
-    if (k < 0) return AM_U_UNKNOWN_COLUMN;
     if (l > 0x7fffffff) return AM_E_SUBARRAY;
-    len[k] = (uint32_t)l;
+    bool found = false;
+#pragma unroll
+    for (int j = 0; j < NSPEC; j++)
+      if (spec[j] == id) { len[j] = (uint32_t)l; found = true; }
+    if (!found) return AM_U_UNKNOWN_COLUMN;
   }
   return AM_OK;
 }
-__device__ static uint32_t place_cols(Rd& r, int nspec, uint32_t* off, const uint32_t* len) {
-  for (int k = 0; k < nspec; k++) {
+template <int NSPEC>
+__device__ __forceinline__ uint32_t place_cols(Rd& r, uint32_t* off, const uint32_t* len) {
+#pragma unroll
+  for (int k = 0; k < NSPEC; k++) {
     uint64_t at;
     TRY(rd_raw(r, len[k], at));
     off[k] = (uint32_t)at;
@@ -100,7 +107,7 @@ __device__ static uint32_t place_cols(Rd& r, int nspec, uint32_t* off, const uin
   return AM_OK;
 }
 
-__device__ static uint32_t parse_change_hdr(const uint8_t* data, uint64_t n, uint64_t abs, ChgHdr& h) {
+__device__ __forceinline__ uint32_t parse_change_hdr(const uint8_t* data, uint64_t n, uint64_t abs, ChgHdr& h) {
   Rd r{data, n, 0};
   int64_t v;
   uint64_t at;
@@ -128,15 +135,15 @@ __device__ static uint32_t parse_change_hdr(const uint8_t* data, uint64_t n, uin
     TRY(rd_u53(r, l));
     TRY(rd_raw(r, (uint64_t)l, at));
   }
-  TRY(parse_cols(r, kChangeColIds, OC_NCOLS, h.col_len, true));
-  TRY(place_cols(r, OC_NCOLS, h.col_off, h.col_len));
+  TRY(parse_cols<OC_NCOLS>(r, kChangeColIds, h.col_len, true));
+  TRY(place_cols<OC_NCOLS>(r, h.col_off, h.col_len));
   h.has_extra = r.off < r.n;
   h.extra_off = (uint32_t)r.off;
   h.extra_len = (uint32_t)(r.n - r.off);
   return AM_OK;
 }
 
-__device__ static uint32_t parse_doc_hdr(const uint8_t* data, uint64_t n, uint64_t abs, DocHdr& h) {
+__device__ __forceinline__ uint32_t parse_doc_hdr(const uint8_t* data, uint64_t n, uint64_t abs, DocHdr& h) {
   Rd r{data, n, 0};
   int64_t v;
   uint64_t at;
@@ -153,10 +160,10 @@ __device__ static uint32_t parse_doc_hdr(const uint8_t* data, uint64_t n, uint64
   h.nheads = (uint32_t)v;
   TRY(rd_raw(r, (uint64_t)v * 32, at));
   h.heads_off = (uint32_t)at;
-  TRY(parse_cols(r, kDocChgColIds, DC_NCOLS, h.ccol_len, false));
-  TRY(parse_cols(r, kDocOpColIds, OC_NCOLS, h.ocol_len, false));
-  TRY(place_cols(r, DC_NCOLS, h.ccol_off, h.ccol_len));
-  TRY(place_cols(r, OC_NCOLS, h.ocol_off, h.ocol_len));
+  TRY(parse_cols<DC_NCOLS>(r, kDocChgColIds, h.ccol_len, false));
+  TRY(parse_cols<OC_NCOLS>(r, kDocOpColIds, h.ocol_len, false));
+  TRY(place_cols<DC_NCOLS>(r, h.ccol_off, h.ccol_len));
+  TRY(place_cols<OC_NCOLS>(r, h.ocol_off, h.ocol_len));
   h.has_hidx = r.off < r.n;
   h.hidx_off = (uint32_t)r.off;
   if (h.has_hidx) {
@@ -170,15 +177,14 @@ __device__ static uint32_t parse_doc_hdr(const uint8_t* data, uint64_t n, uint64
 // ------------------------------------------------------------------------------------------
 // k_chunks: one thread per chunk
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_chunks(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
-                                                uint32_t nchunks, ChunkInfo* __restrict__ info,
-                                                HdrSlot* __restrict__ hdr) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nchunks) return;
-  am_chunk_desc cd = chunks[i];
-  const uint8_t* p = arena + cd.off;
+// Per chunk: container header, SHA-256 (hash + checksum), change/document header parse into the
+// compact slot, row/entry/string counts. `p` is the chunk start: a staged LDS copy or the arena.
+__device__ __forceinline__ void chunk_body(const uint8_t* p, const am_chunk_desc cd, uint32_t i, ChunkInfo* __restrict__ info,
+                                           HdrSlot* __restrict__ hdr) {
   ChunkInfo ci;
-  for (int k = 0; k < 32; k++) ci.hash[k] = 0;
+  uint32_t* hw = reinterpret_cast<uint32_t*>(ci.hash);
+#pragma unroll
+  for (int k = 0; k < 8; k++) hw[k] = 0;
   ci.status = AM_OK; ci.type = 0xff; ci.data_off = 0; ci.data_len = 0; ci.nops = 0; ci.nents = 0; ci.nchg = 0;
   ci.ndeps = 0; ci.nactors = 0; ci.strbytes = 0; ci.nheads = 0; ci.arg0 = 0;
   uint32_t st = AM_OK;
@@ -196,10 +202,14 @@ __global__ void __launch_bounds__(256) k_chunks(const uint8_t* __restrict__ aren
     if ((st = rd_raw(r, (uint64_t)len, at))) break;
     ci.data_off = (uint32_t)at;
     ci.data_len = (uint32_t)len;
-    uint8_t h[32];
-    sha256_dev(p + 8, r.off - 8, h);
-    for (int k = 0; k < 32; k++) ci.hash[k] = h[k];
-    if (!(cd.flags & 1) && (h[0] != p[4] || h[1] != p[5] || h[2] != p[6] || h[3] != p[7])) { st = AM_E_CHECKSUM; break; }
+    uint32_t h[8];
+    sha256_words(p + 8, r.off - 8, h);
+#pragma unroll
+    for (int k = 0; k < 8; k++) hw[k] = __builtin_bswap32(h[k]);
+    if (!(cd.flags & 1) && ((uint32_t)p[4] << 24 | (uint32_t)p[5] << 16 | (uint32_t)p[6] << 8 | p[7]) != h[0]) {
+      st = AM_E_CHECKSUM;
+      break;
+    }
     const uint8_t* data = p + at;
     if (ci.type == 1) {
       if (r.off != cd.len) { st = AM_E_CHANGE_TRAILING; break; }
@@ -219,13 +229,13 @@ __global__ void __launch_bounds__(256) k_chunks(const uint8_t* __restrict__ aren
       ci.nactors = hh.nactors;
       uint64_t cnt, sum;
       // rows: values in the action column (new.js:701)
-      if ((st = rle_count_sum(data + hh.col_off[OC_ACTION], hh.col_len[OC_ACTION], false, cnt, sum, 0))) break;
+      if ((st = rle_count_sum_i(data + hh.col_off[OC_ACTION], hh.col_len[OC_ACTION], false, cnt, sum, 0))) break;
       ci.nops = (uint32_t)cnt;
-      if ((st = rle_count_sum(data + hh.col_off[OC_GRP_NUM], hh.col_len[OC_GRP_NUM], false, cnt, sum, 0))) break;
+      if ((st = rle_count_sum_i(data + hh.col_off[OC_GRP_NUM], hh.col_len[OC_GRP_NUM], false, cnt, sum, 0))) break;
       ci.nents = (uint32_t)sum;
       // key string bytes summed over rows (bounds the re-encoded keyStr column)
       uint64_t scnt, ssum;
-      if ((st = rle_count_sum(data + hh.col_off[OC_KEY_STR], hh.col_len[OC_KEY_STR], true, scnt, ssum, 0))) break;
+      if ((st = rle_count_sum_i(data + hh.col_off[OC_KEY_STR], hh.col_len[OC_KEY_STR], true, scnt, ssum, 0))) break;
       ci.strbytes = (uint32_t)ssum + hh.msg_len;
     } else if (ci.type == 0) {
       if (r.off != cd.len) { st = AM_E_DOC_TRAILING; break; }
@@ -245,18 +255,18 @@ __global__ void __launch_bounds__(256) k_chunks(const uint8_t* __restrict__ aren
       ci.nactors = dh.nactors;
       ci.nheads = dh.nheads;
       uint64_t cnt, sum;
-      if ((st = rle_count_sum(data + dh.ccol_off[DC_ACTOR], dh.ccol_len[DC_ACTOR], false, cnt, sum, 0))) break;
+      if ((st = rle_count_sum_i(data + dh.ccol_off[DC_ACTOR], dh.ccol_len[DC_ACTOR], false, cnt, sum, 0))) break;
       ci.nchg = (uint32_t)cnt;
-      if ((st = rle_count_sum(data + dh.ccol_off[DC_DEPS_NUM], dh.ccol_len[DC_DEPS_NUM], false, cnt, sum, 0))) break;
+      if ((st = rle_count_sum_i(data + dh.ccol_off[DC_DEPS_NUM], dh.ccol_len[DC_DEPS_NUM], false, cnt, sum, 0))) break;
       ci.ndeps = (uint32_t)sum;
       // doc rows: values in the idCtr column (updateBlockMetadata, new.js:386)
-      if ((st = rle_count_sum(data + dh.ocol_off[OC_ID_CTR], dh.ocol_len[OC_ID_CTR], false, cnt, sum, 0, true))) break;
+      if ((st = rle_count_sum_i(data + dh.ocol_off[OC_ID_CTR], dh.ocol_len[OC_ID_CTR], false, cnt, sum, 0, true))) break;
       ci.nops = (uint32_t)cnt;
-      if ((st = rle_count_sum(data + dh.ocol_off[OC_GRP_NUM], dh.ocol_len[OC_GRP_NUM], false, cnt, sum, 0))) break;
+      if ((st = rle_count_sum_i(data + dh.ocol_off[OC_GRP_NUM], dh.ocol_len[OC_GRP_NUM], false, cnt, sum, 0))) break;
       ci.nents = (uint32_t)sum;
       uint64_t s1, s2;
-      if ((st = rle_count_sum(data + dh.ocol_off[OC_KEY_STR], dh.ocol_len[OC_KEY_STR], true, cnt, s1, 0))) break;
-      if ((st = rle_count_sum(data + dh.ccol_off[DC_MESSAGE], dh.ccol_len[DC_MESSAGE], true, cnt, s2, 0))) break;
+      if ((st = rle_count_sum_i(data + dh.ocol_off[OC_KEY_STR], dh.ocol_len[OC_KEY_STR], true, cnt, s1, 0))) break;
+      if ((st = rle_count_sum_i(data + dh.ccol_off[DC_MESSAGE], dh.ccol_len[DC_MESSAGE], true, cnt, s2, 0))) break;
       ci.strbytes = (uint32_t)(s1 + s2);
     } else {
       st = AM_E_CHUNK_TYPE;
@@ -265,6 +275,43 @@ __global__ void __launch_bounds__(256) k_chunks(const uint8_t* __restrict__ aren
   } while (0);
   ci.status = st;
   info[i] = ci;
+}
+
+#define KC_STAGE 12288  // bytes of LDS per wave for its 64 chunks
+// k_chunks: thread per chunk. Each wave first stages the byte span of its 64 chunks (adjacent in
+// the arena for staged batches) into LDS with 16-byte loads, so the SHA-256 rounds and the
+// dependent LEB128 reads of the header parse hit LDS; a wave whose span does not fit reads the
+// arena directly.
+__global__ void __launch_bounds__(256) k_chunks(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
+                                                uint32_t nchunks, ChunkInfo* __restrict__ info,
+                                                HdrSlot* __restrict__ hdr) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[4][KC_STAGE + 16];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const bool valid = i < nchunks;
+  am_chunk_desc cd;
+  cd.off = 0; cd.len = 0; cd.flags = 0;
+  if (valid) cd = chunks[i];
+  // span of the wave's chunks
+  uint64_t lo = valid ? cd.off : ~0ull, hi = valid ? cd.off + cd.len : 0ull;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    const uint64_t a = __shfl_xor(lo, d, 64), b2 = __shfl_xor(hi, d, 64);
+    lo = a < lo ? a : lo;
+    hi = b2 > hi ? b2 : hi;
+  }
+  const uint64_t lo16 = lo & ~15ull;
+  const bool staged = hi > lo && hi - lo16 <= KC_STAGE;
+  if (staged) {
+    const uint32_t nv = (uint32_t)((hi - lo16 + 15) >> 4);
+    uint4* dst = reinterpret_cast<uint4*>(stage[w]);
+    const uint4* src = reinterpret_cast<const uint4*>(arena + lo16);
+    for (uint32_t v = l; v < nv; v += 64) dst[v] = src[v];
+  }
+  __syncthreads();
+  if (!valid) return;
+  if (staged) chunk_body(stage[w] + (cd.off - lo16), cd, i, info, hdr);
+  else chunk_body(arena + cd.off, cd, i, info, hdr);
 }
 
 // ------------------------------------------------------------------------------------------
