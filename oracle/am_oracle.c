@@ -1063,6 +1063,11 @@ typedef struct { const uint8_t *a; uint32_t n; int64_t seq; } clock_t_;
 
 static void encode_doc(ctx_t *c, const docst_t *st, int deflate, bbuf *out);
 
+/* applyChanges patch replay (am_apply_patch_oracle.inc): set while oc_doc_apply_patch runs */
+typedef struct apatch apatch;
+static apatch *g_ap = NULL;
+static void ap_pass(ctx_t *c, apatch *ap, change_t **applied, size_t na);
+
 static void apply_changes(ctx_t *c, oc_doc *doc, docst_t *st, const uint8_t *const *bufs, const size_t *lens, size_t n) {
   /* decode all given changes first (new.js:1798), then append the old queue (new.js:1814) */
   size_t total = n + doc->nqueue;
@@ -1155,6 +1160,7 @@ static void apply_changes(ctx_t *c, oc_doc *doc, docst_t *st, const uint8_t *con
       }
     }
     if (reuse_abort) { na = 0; ne = nq; memcpy(enq, queue, sizeof(change_t *) * nq); }
+    if (na > 0 && g_ap) ap_pass(c, g_ap, applied, na);
     if (na > 0) {
       /* readNextChangeOp / applyOps over all ops of the applied changes (new.js:1589-1591) */
       for (size_t ai = 0; ai < na; ai++) {
@@ -1691,3 +1697,4 @@ int oc_col_decode(int type, const uint8_t *buf, size_t len, size_t maxn, size_t 
 }
 
 #include "am_patch_oracle.inc"
+#include "am_apply_patch_oracle.inc"

@@ -72,6 +72,11 @@ void oc_free(void *p);
 
 /* Backend.getPatch(doc) as JSON text (malloc'd, free with oc_free); NULL on error (message in err) */
 char *oc_doc_patch(const oc_doc *doc, char *err, size_t errcap);
+/* Backend.applyChanges(doc, changes): applies like oc_doc_apply and returns the patch the
+ * reference returns (maxOp, clock, deps, pendingChanges, diffs) as JSON text (malloc'd, free with
+ * oc_free); NULL on error (message in err). am_apply_patch_oracle.inc. */
+char *oc_doc_apply_patch(oc_doc *doc, const uint8_t *const *bufs, const size_t *lens, size_t n, char *err,
+                         size_t errcap);
 
 /* Flat export of a decoded (saved) document: ops in document order -- for host checks of the
  * engine's patch scan. Nulls: obj/key ctr and actor -1, key_len -1, action -1, val_len 0. */

@@ -43,6 +43,8 @@ def lib():
         L.oc_free.argtypes = [P]
         L.oc_doc_patch.restype = C.c_void_p
         L.oc_doc_patch.argtypes = [P, C.c_char_p, S]
+        L.oc_doc_apply_patch.restype = C.c_void_p
+        L.oc_doc_apply_patch.argtypes = [P, C.POINTER(C.c_char_p), C.POINTER(S), S, C.c_char_p, S]
         L.oc_bloom_build.restype = S
         L.oc_bloom_build.argtypes = [C.c_char_p, S, C.c_char_p, S]
         L.oc_bloom_contains.restype = C.c_int
@@ -178,6 +180,20 @@ class Doc:
         rc = lib().oc_doc_apply(self._p, arr, lens, n, err, 512)
         if rc:
             raise OracleError(err.value.decode(), rc)
+
+    def apply_patch(self, changes):
+        """Backend.applyChanges(doc, changes): applies and returns the patch as a dict."""
+        import json
+        n = len(changes)
+        arr = (C.c_char_p * max(n, 1))(*changes)
+        lens = (C.c_size_t * max(n, 1))(*[len(c) for c in changes])
+        err = C.create_string_buffer(512)
+        p = lib().oc_doc_apply_patch(self._p, arr, lens, n, err, 512)
+        if not p:
+            raise OracleError(err.value.decode())
+        txt = C.string_at(p).decode("utf-8")
+        lib().oc_free(p)
+        return json.loads(txt)
 
     def patch(self):
         """Backend.getPatch(doc) as a dict (JSON from the C restatement)."""
