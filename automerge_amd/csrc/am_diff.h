@@ -1,0 +1,989 @@
+// am_diff.h -- the patch Backend.applyChanges returns as a patch log, written by
+// lane 0 of k_doc (phase P8) after the parallel merge.
+//
+// Reference: applyChanges / applyOps / mergeDocChangeOps (new.js:1550-1597, 1304-1380,
+// 1052-1290), seekWithinBlock (:50-192), updatePatchProperty (:884-1040), appendEdit /
+// appendUpdate / convertInsertToUpdate (:747-869), setupPatches (:1461-1528), and the objectMeta
+// that documentPatch leaves at load (:1604-1635, 1748).
+//
+// The reference merges the applied change ops into the document one applyOps call at a time.
+// Here the merged document is already known (document order F from the parallel merge), and every
+// intermediate document is F restricted to the rows present at that point: base rows, and change
+// rows whose op precedes the current position in the applied op stream. A row's succ list at
+// stream position p is likewise its final succ list restricted to the entries whose op precedes
+// p. So the replay walks F under those filters -- the seek (with the reference's per-column
+// decoder positions), the merge loop and updatePatchProperty -- and never rebuilds a document.
+//
+// The patch tree (objectMeta, object patches, props, edits) lives in index-linked pools; the
+// object patches are written out at the end as PR_OBJ sections of the am_patch.h log (PR_OBJ
+// carries the object type, so the host stage can create any object on first sight). Pools are
+// sized from the row and entry counts; running out reports PATCH_U_CAPACITY, never a wrong patch.
+#pragma once
+#include "am_patch.h"
+
+// ---- pools ----
+struct DVal { uint32_t vtag, dt; int64_t v0, v1; };  // a patch value as the log stores it
+struct DObj {                                        // objectMeta entry + patches[objectId]
+  int64_t ctr; int32_t actor; int32_t type;          // actor -1: _root; type 0 map 1 list 2 text 3 table
+  int32_t parent;                                    // objectMeta.parentObj (DObj index), -1: none
+  int32_t pk_row;                                    // the make op: its elemId is parentKey
+  int32_t kids;                                      // children: first DKid
+  int32_t has_patch;
+  int32_t edit_tail;                                 // last DEdit of the object's edits, -1
+  int32_t prop_head, prop_tail;                      // DProp list
+  int32_t pad;
+};
+struct DKid { int32_t elem_row; int32_t head; int32_t n; int32_t next; };  // children[elemId]
+struct DKV { int64_t ctr; int32_t actor; int32_t kind; int32_t ref; int32_t next; };  // 1: set row, 2: DObj
+struct DProp { int32_t key_row; int32_t head, tail; int32_t next; };
+struct DPE { int64_t ctr; int32_t actor; int32_t next; DVal v; };
+struct DEdit {
+  uint32_t action;  // PR_INSERT / PR_MULTI / PR_UPDATE / PR_REMOVE
+  int32_t prev;
+  int64_t index, ec, oc, count;
+  int32_t ea, oa;
+  DVal v;
+  int32_t mv_tail;
+  uint32_t nmv, mdt;
+  int32_t pad;
+};
+struct DMV { DVal v; int32_t prev; int32_t pad; };
+struct DPst { int32_t elem_row; int32_t vis_head, vis_tail; int32_t has_child; int32_t action; int32_t cs_head; int32_t cm_head; int32_t next; };
+struct DVis { int32_t row; int32_t next; };
+struct DCs { int64_t op_ctr; int64_t value; int32_t op_actor; int32_t nleft; int32_t next; int32_t pad; };
+struct DCm { int64_t ctr; int32_t actor; int32_t state; int32_t next; int32_t pad; };
+
+struct DiffScratch {
+  DObj* obj; uint32_t nobj, cap_obj;
+  DKid* kid; uint32_t nkid, cap_kid;
+  DKV* kv; uint32_t nkv, cap_kv;
+  DProp* prop; uint32_t nprop, cap_prop;
+  DPE* pe; uint32_t npe, cap_pe;
+  DEdit* ed; uint32_t ned, cap_ed;
+  DMV* mv; uint32_t nmv, cap_mv;
+  DPst* pst; uint32_t npst, cap_pst;  // reset at each mergeDocChangeOps call
+  DVis* vis; uint32_t nvis, cap_vis;
+  DCs* cs; uint32_t ncs, cap_cs;
+  DCm* cm; uint32_t ncm, cap_cm;
+  int32_t* fpos;                      // row -> position in F (-1: deletion)
+  int32_t* oids; uint32_t noid, cap_oid;  // objectIds (Set, insertion order)
+  int32_t* tmp;                       // emission order of one object's edits / popped edits
+  int32_t* cops; uint8_t* seen;       // changeOps (rows) and predSeen flags
+  uint32_t* seen_off;
+  uint32_t cap_cops, cap_seen;
+};
+
+// sizes of the pools for R rows and E pred/succ entries (host and device agree)
+AM_PHD inline void diff_caps(uint64_t R, uint64_t E, uint64_t caps[16]) {
+  caps[0] = R + 2;          // obj
+  caps[1] = R + 2;          // kid
+  caps[2] = 4 * R + 64;     // kv
+  caps[3] = R + 2;          // prop
+  caps[4] = 4 * R + 64;     // pe
+  caps[5] = 4 * R + 64;     // ed
+  caps[6] = 4 * R + 64;     // mv
+  caps[7] = R + 2;          // pst
+  caps[8] = 2 * R + 4;      // vis
+  caps[9] = R + 2;          // cs
+  caps[10] = E + 2;         // cm
+  caps[11] = R + 2;         // fpos
+  caps[12] = R + 2;         // oids
+  caps[13] = 8 * R + 128;   // tmp
+  caps[14] = R + 2;         // cops (+ seen_off)
+  caps[15] = E + 2;         // seen
+}
+AM_PHD inline uint64_t diff_scratch_bytes(uint64_t R, uint64_t E) {
+  uint64_t c[16];
+  diff_caps(R, E, c);
+  const uint64_t sz[16] = {sizeof(DObj), sizeof(DKid), sizeof(DKV), sizeof(DProp), sizeof(DPE), sizeof(DEdit), sizeof(DMV),
+                           sizeof(DPst), sizeof(DVis), sizeof(DCs), sizeof(DCm), 4, 4, 4, 8, 1};
+  uint64_t t = 0;
+  for (int i = 0; i < 16; i++) t += (c[i] * sz[i] + 15) & ~(uint64_t)15;
+  return t;
+}
+AM_PHD inline void diff_scratch_bind(uint8_t* p, uint64_t R, uint64_t E, DiffScratch& w) {
+  uint64_t c[16];
+  diff_caps(R, E, c);
+  uint64_t o = 0;
+  auto take = [&](uint64_t bytes) { uint8_t* at = p + o; o += (bytes + 15) & ~(uint64_t)15; return at; };
+  w.obj = reinterpret_cast<DObj*>(take(c[0] * sizeof(DObj))); w.cap_obj = (uint32_t)c[0];
+  w.kid = reinterpret_cast<DKid*>(take(c[1] * sizeof(DKid))); w.cap_kid = (uint32_t)c[1];
+  w.kv = reinterpret_cast<DKV*>(take(c[2] * sizeof(DKV))); w.cap_kv = (uint32_t)c[2];
+  w.prop = reinterpret_cast<DProp*>(take(c[3] * sizeof(DProp))); w.cap_prop = (uint32_t)c[3];
+  w.pe = reinterpret_cast<DPE*>(take(c[4] * sizeof(DPE))); w.cap_pe = (uint32_t)c[4];
+  w.ed = reinterpret_cast<DEdit*>(take(c[5] * sizeof(DEdit))); w.cap_ed = (uint32_t)c[5];
+  w.mv = reinterpret_cast<DMV*>(take(c[6] * sizeof(DMV))); w.cap_mv = (uint32_t)c[6];
+  w.pst = reinterpret_cast<DPst*>(take(c[7] * sizeof(DPst))); w.cap_pst = (uint32_t)c[7];
+  w.vis = reinterpret_cast<DVis*>(take(c[8] * sizeof(DVis))); w.cap_vis = (uint32_t)c[8];
+  w.cs = reinterpret_cast<DCs*>(take(c[9] * sizeof(DCs))); w.cap_cs = (uint32_t)c[9];
+  w.cm = reinterpret_cast<DCm*>(take(c[10] * sizeof(DCm))); w.cap_cm = (uint32_t)c[10];
+  w.fpos = reinterpret_cast<int32_t*>(take(c[11] * 4));
+  w.oids = reinterpret_cast<int32_t*>(take(c[12] * 4)); w.cap_oid = (uint32_t)c[12];
+  w.tmp = reinterpret_cast<int32_t*>(take(c[13] * 4));
+  w.cops = reinterpret_cast<int32_t*>(take(c[14] * 4));
+  w.seen_off = reinterpret_cast<uint32_t*>(take(c[14] * 4));
+  w.cap_cops = (uint32_t)c[14];
+  w.seen = take(c[15]);
+  w.cap_seen = (uint32_t)c[15];
+  w.nobj = w.nkid = w.nkv = w.nprop = w.npe = w.ned = w.nmv = w.npst = w.nvis = w.ncs = w.ncm = w.noid = 0;
+}
+
+// ---- the replay ----
+// Src interface (row indexes: base rows [0, nb()) in document order, then the applied change ops
+// in application order, deletions included):
+//   nb(); nrows(); nout(); frow(f); f_nsucc(f); f_succ_ctr(f, k); f_succ_actor(f, k);
+//   f_succ_time(f, k) (-1: base entry, else the stream index of the succ op);
+//   obj_ctr(i) / obj_actor(i) (-1: root); key_ctr(i) (-1: null) / key_actor(i) (-1: null);
+//   has_key(i) (key string not null); key_len(i); key_cmp(i, j) (UTF-16 order); key_eq(i, j);
+//   copy_key(i, dst); id_ctr(i); id_actor(i); insert(i); action(i); npred(i); pred_ctr(i, k);
+//   pred_actor(i, k); rank(a); patch_value's val_len / copy_value / value_int / value_f64_bits;
+//   nactors(); actor_len(a); copy_actor(a, dst); nchg(); chg_actor(c); chg_seq(c); npass();
+//   pass_end(p) (stream index where pass p ends)
+template <class Src>
+struct Diff {
+  const Src& s;
+  DiffScratch& w;
+  PatchOut& o;
+  bool ok;
+  AM_PHD Diff(const Src& src, DiffScratch& ws, PatchOut& out) : s(src), w(ws), o(out), ok(true) {}
+
+  AM_PHD bool fail(uint32_t st, int64_t a0 = 0, int64_t a1 = 0) {
+    if (ok) { o.status = st; o.arg0 = a0; o.arg1 = a1; }
+    ok = false;
+    return false;
+  }
+  AM_PHD int64_t rtime(int32_t row) const { return row >= (int32_t)s.nb() ? (int64_t)row - s.nb() : -1; }
+  // actor string order through the ranks; -1 (null / undefined) compares false
+  AM_PHD bool act_lt(int32_t a, int32_t b) const { return a >= 0 && b >= 0 && s.rank(a) < s.rank(b); }
+  // succ count of the row at F position f when the stream has reached position lim
+  AM_PHD uint32_t nsucc_at(int32_t f, int64_t lim) const {
+    uint32_t n = 0;
+    for (uint32_t k = 0; k < s.f_nsucc(f); k++) n += s.f_succ_time(f, k) < lim ? 1u : 0u;
+    return n;
+  }
+  // elemId of an op (new.js:888-890): the key string when truthy, else the element id
+  AM_PHD bool elem_str(int32_t i) const { return s.has_key(i) && s.key_len(i) > 0; }
+  AM_PHD int64_t elem_ctr(int32_t i) const { return s.insert(i) ? s.id_ctr(i) : s.key_ctr(i); }
+  AM_PHD int32_t elem_actor(int32_t i) const { return s.insert(i) ? s.id_actor(i) : s.key_actor(i); }
+  AM_PHD bool elem_eq(int32_t i, int32_t j) const {
+    if (elem_str(i) != elem_str(j)) return false;
+    if (elem_str(i)) return s.key_eq(i, j);
+    return elem_ctr(i) == elem_ctr(j) && elem_actor(i) == elem_actor(j);
+  }
+  AM_PHD static uint32_t obj_type_of_action(int64_t a) { return a == 2 ? 1u : a == 4 ? 2u : a == 6 ? 3u : 0u; }
+
+  // ---- objectMeta / patches ----
+  AM_PHD int32_t obj_find(int64_t ctr, int32_t actor) const {
+    for (uint32_t k = 0; k < w.nobj; k++) if (w.obj[k].ctr == ctr && w.obj[k].actor == actor) return (int32_t)k;
+    return -1;
+  }
+  AM_PHD int32_t obj_new(int64_t ctr, int32_t actor, uint32_t type) {
+    if (w.nobj >= w.cap_obj) { fail(PATCH_U_CAPACITY); return -1; }
+    DObj& d = w.obj[w.nobj];
+    d.ctr = ctr; d.actor = actor; d.type = (int32_t)type; d.parent = -1; d.pk_row = -1; d.kids = -1;
+    d.has_patch = 0; d.edit_tail = -1; d.prop_head = d.prop_tail = -1; d.pad = 0;
+    return (int32_t)w.nobj++;
+  }
+  AM_PHD int32_t kid_find(int32_t ob, int32_t row, bool create) {
+    int32_t* link = &w.obj[ob].kids;
+    while (*link >= 0) {
+      if (elem_eq(w.kid[*link].elem_row, row)) return *link;
+      link = &w.kid[*link].next;
+    }
+    if (!create) return -1;
+    if (w.nkid >= w.cap_kid) { fail(PATCH_U_CAPACITY); return -1; }
+    DKid& d = w.kid[w.nkid];
+    d.elem_row = row; d.head = -1; d.n = 0; d.next = -1;
+    *link = (int32_t)w.nkid;  // appended: JS object key order
+    return (int32_t)w.nkid++;
+  }
+  // children[elemId][opId] = value (an existing opId keeps its position)
+  AM_PHD bool kv_set(int32_t kd, int64_t ctr, int32_t actor, int32_t kind, int32_t ref) {
+    int32_t* link = &w.kid[kd].head;
+    while (*link >= 0) {
+      DKV& e = w.kv[*link];
+      if (e.ctr == ctr && e.actor == actor) { e.kind = kind; e.ref = ref; return true; }
+      link = &e.next;
+    }
+    if (w.nkv >= w.cap_kv) return fail(PATCH_U_CAPACITY);
+    DKV& e = w.kv[w.nkv];
+    e.ctr = ctr; e.actor = actor; e.kind = kind; e.ref = ref; e.next = -1;
+    *link = (int32_t)w.nkv++;
+    w.kid[kd].n++;
+    return true;
+  }
+  AM_PHD void patch_on(int32_t ob) { w.obj[ob].has_patch = 1; }
+  AM_PHD DVal child_val(int32_t ob) const {
+    DVal v;
+    v.vtag = PV_CHILD; v.dt = (uint32_t)w.obj[ob].type; v.v0 = w.obj[ob].ctr; v.v1 = w.obj[ob].actor;
+    return v;
+  }
+  AM_PHD bool row_val(int32_t row, DVal& v) {
+    if (!patch_value(s, (uint32_t)row, o, v.vtag, v.dt, v.v0, v.v1)) {
+      ok = false;
+      return false;
+    }
+    return true;
+  }
+
+  // ---- edits (appendEdit / appendUpdate / convertInsertToUpdate, new.js:747-869) ----
+  AM_PHD bool mv_push(DEdit& e, const DVal& v) {
+    if (w.nmv >= w.cap_mv) return fail(PATCH_U_CAPACITY);
+    DMV& m = w.mv[w.nmv];
+    m.v = v; m.prev = e.mv_tail; m.pad = 0;
+    e.mv_tail = (int32_t)w.nmv++;
+    e.nmv++;
+    return true;
+  }
+  AM_PHD const DVal& mv_first(const DEdit& e) const {
+    int32_t k = e.mv_tail;
+    for (uint32_t q = 1; q < e.nmv; q++) k = w.mv[k].prev;
+    return w.mv[k].v;
+  }
+  AM_PHD bool edit_push(int32_t ob, const DEdit& ne) {
+    if (w.ned >= w.cap_ed) return fail(PATCH_U_CAPACITY);
+    DEdit& e = w.ed[w.ned];
+    e = ne;
+    e.prev = w.obj[ob].edit_tail;
+    e.mv_tail = -1; e.nmv = 0;
+    w.obj[ob].edit_tail = (int32_t)w.ned++;
+    return true;
+  }
+  AM_PHD void edit_pop(int32_t ob) { w.obj[ob].edit_tail = w.ed[w.obj[ob].edit_tail].prev; }
+  AM_PHD bool append_edit(int32_t ob, const DEdit& ne) {
+    const int32_t lt = w.obj[ob].edit_tail;
+    if (lt >= 0) {
+      DEdit& last = w.ed[lt];
+      if (last.action == PR_INSERT && ne.action == PR_INSERT && last.index == ne.index - 1 && last.v.vtag != PV_CHILD &&
+          ne.v.vtag != PV_CHILD && last.ec == last.oc && last.ea == last.oa && ne.ec == ne.oc && ne.ea == ne.oa &&
+          last.ea == ne.ea && last.ec + 1 == ne.ec) {
+        const uint32_t da = pv_dtcode(last.v.vtag, last.v.dt), db = pv_dtcode(ne.v.vtag, ne.v.dt);
+        if (da == db && pv_typeof(last.v.vtag) == pv_typeof(ne.v.vtag)) {
+          const DVal first = last.v;
+          last.action = PR_MULTI;
+          last.mdt = pv_dt_truthy(db) ? db : 0;  // lastEdit.datatype set only when truthy
+          last.mv_tail = -1; last.nmv = 0;
+          return mv_push(last, first) && mv_push(last, ne.v);
+        }
+      }
+      if (last.action == PR_MULTI && ne.action == PR_INSERT && last.index + (int64_t)last.nmv == ne.index &&
+          ne.v.vtag != PV_CHILD && ne.ec == ne.oc && ne.ea == ne.oa && last.ea == ne.ea &&
+          last.ec + (int64_t)last.nmv == ne.ec) {
+        const uint32_t db = pv_dtcode(ne.v.vtag, ne.v.dt);
+        if (last.mdt == db && pv_typeof(mv_first(last).vtag) == pv_typeof(ne.v.vtag)) return mv_push(last, ne.v);
+      }
+      if (last.action == PR_REMOVE && ne.action == PR_REMOVE && last.index == ne.index) {
+        last.count += ne.count;
+        return true;
+      }
+    }
+    return edit_push(ob, ne);
+  }
+  AM_PHD bool append_update(int32_t ob, int64_t index, int64_t ec, int32_t ea, int64_t oc, int32_t oa, const DVal& v,
+                            bool first) {
+    bool ins = false;
+    if (first) {
+      while (!ins && w.obj[ob].edit_tail >= 0) {
+        DEdit& last = w.ed[w.obj[ob].edit_tail];
+        if ((last.action == PR_INSERT || last.action == PR_UPDATE) && last.index == index) {
+          ins = last.action == PR_INSERT;
+          edit_pop(ob);
+        } else if (last.action == PR_MULTI && last.index + (int64_t)last.nmv - 1 == index) {
+          last.mv_tail = w.mv[last.mv_tail].prev;  // values.pop()
+          last.nmv--;
+          ins = true;
+        } else {
+          break;
+        }
+      }
+    }
+    DEdit e = {};
+    e.index = index; e.oc = oc; e.oa = oa; e.v = v;
+    if (ins) { e.action = PR_INSERT; e.ec = ec; e.ea = ea; }
+    else e.action = PR_UPDATE;
+    return append_edit(ob, e);
+  }
+  AM_PHD bool convert_insert_to_update(int32_t ob, int64_t index, int64_t ec, int32_t ea) {
+    // pop the suffix (updates, then the insert, at `index`) into tmp
+    uint32_t nu = 0;
+    while (w.obj[ob].edit_tail >= 0) {
+      const int32_t k = w.obj[ob].edit_tail;
+      const uint32_t act = w.ed[k].action;
+      if (act == PR_INSERT || act == PR_UPDATE) {
+        if (w.ed[k].index != index) return fail(PATCH_U_VALUE);  // 'last edit has unexpected index'
+        w.tmp[nu++] = k;
+        edit_pop(ob);
+        if (act == PR_INSERT) break;
+      } else {
+        return fail(PATCH_U_VALUE);  // 'last edit has unexpected action'
+      }
+    }
+    for (uint32_t q = 0; q < nu; q++) {
+      const DEdit u = w.ed[w.tmp[nu - 1 - q]];
+      if (!append_update(ob, index, ec, ea, u.oc, u.oa, u.v, q == 0)) return false;
+    }
+    return true;
+  }
+
+  // ---- props (map objects) ----
+  AM_PHD int32_t prop_get(int32_t ob, int32_t row, bool reset) {
+    for (int32_t k = w.obj[ob].prop_head; k >= 0; k = w.prop[k].next)
+      if (s.key_eq(w.prop[k].key_row, row)) {
+        if (reset) w.prop[k].head = w.prop[k].tail = -1;
+        return k;
+      }
+    if (w.nprop >= w.cap_prop) { fail(PATCH_U_CAPACITY); return -1; }
+    DProp& p = w.prop[w.nprop];
+    p.key_row = row; p.head = p.tail = -1; p.next = -1;
+    if (w.obj[ob].prop_tail >= 0) w.prop[w.obj[ob].prop_tail].next = (int32_t)w.nprop;
+    else w.obj[ob].prop_head = (int32_t)w.nprop;
+    w.obj[ob].prop_tail = (int32_t)w.nprop;
+    return (int32_t)w.nprop++;
+  }
+  // props[key][opId] = v; with `existed`, an existing opId is left alone and reported
+  AM_PHD bool prop_set(int32_t pr, int64_t ctr, int32_t actor, const DVal& v, bool* existed = nullptr) {
+    for (int32_t k = w.prop[pr].head; k >= 0; k = w.pe[k].next)
+      if (w.pe[k].ctr == ctr && w.pe[k].actor == actor) {
+        if (existed) { *existed = true; return true; }
+        w.pe[k].v = v;
+        return true;
+      }
+    if (existed) *existed = false;
+    if (w.npe >= w.cap_pe) return fail(PATCH_U_CAPACITY);
+    DPE& e = w.pe[w.npe];
+    e.ctr = ctr; e.actor = actor; e.v = v; e.next = -1;
+    if (w.prop[pr].tail >= 0) w.pe[w.prop[pr].tail].next = (int32_t)w.npe;
+    else w.prop[pr].head = (int32_t)w.npe;
+    w.prop[pr].tail = (int32_t)w.npe++;
+    return true;
+  }
+
+  // ---- propState ----
+  AM_PHD int32_t pst_get(int32_t row) const {
+    for (uint32_t k = 0; k < w.npst; k++) if (elem_eq(w.pst[k].elem_row, row)) return (int32_t)k;
+    return -1;
+  }
+
+  // updatePatchProperty (new.js:884-1040). f: F position of a document op (its succ list as of
+  // stream position lim), -1 for a change op (has_old = false, oldSuccNum undefined).
+  AM_PHD bool update_property(int32_t ob, int32_t row, int32_t f, int64_t lim, int64_t list_index, bool has_old,
+                              uint32_t old_succ, bool whole_doc) {
+    const int64_t action = s.action(row);
+    if (action < 0 || action >= 8) return fail(PATCH_U_VALUE);
+    const int64_t idc = s.id_ctr(row);
+    const int32_t ida = s.id_actor(row);
+    const uint32_t cur_succ = has_old ? nsucc_at(f, lim) : 0u;
+    // a new make* op: objectMeta[opId] and children[elemId][opId] (new.js:894-897)
+    if (action % 2 == 0 && obj_find(idc, ida) < 0) {
+      const int32_t nm = obj_new(idc, ida, obj_type_of_action(action));
+      if (nm < 0) return false;
+      w.obj[nm].parent = ob;
+      w.obj[nm].pk_row = row;
+      const int32_t kd = kid_find(ob, row, true);
+      if (kd < 0 || !kv_set(kd, idc, ida, 2, nm)) return false;
+    }
+    int32_t ps = pst_get(row);
+    const bool first_op = ps < 0;
+    if (ps < 0) {
+      if (w.npst >= w.cap_pst) return fail(PATCH_U_CAPACITY);
+      DPst& p = w.pst[w.npst];
+      p.elem_row = row; p.vis_head = p.vis_tail = -1; p.has_child = 0; p.action = 0; p.cs_head = -1; p.cm_head = -1; p.next = -1;
+      ps = (int32_t)w.npst++;
+    }
+    const bool overwritten = has_old && cur_succ > 0;
+    if (!overwritten) {
+      if (w.nvis >= w.cap_vis) return fail(PATCH_U_CAPACITY);
+      w.vis[w.nvis].row = row;
+      w.vis[w.nvis].next = -1;
+      if (w.pst[ps].vis_tail >= 0) w.vis[w.pst[ps].vis_tail].next = (int32_t)w.nvis;
+      else w.pst[ps].vis_head = (int32_t)w.nvis;
+      w.pst[ps].vis_tail = (int32_t)w.nvis++;
+      if (action % 2 == 0) w.pst[ps].has_child = 1;
+    }
+    const int32_t prev = kid_find(ob, row, false);
+    if (w.pst[ps].has_child || (prev >= 0 && w.kid[prev].n > 0)) {
+      const int32_t kd = kid_find(ob, row, true);
+      if (kd < 0) return false;
+      w.kid[kd].head = -1;  // children[elemId] = values
+      w.kid[kd].n = 0;
+      for (int32_t v = w.pst[ps].vis_head; v >= 0; v = w.vis[v].next) {
+        const int32_t vr = w.vis[v].row;
+        const int64_t va = s.action(vr);
+        if (va == 1) {
+          if (!kv_set(kd, s.id_ctr(vr), s.id_actor(vr), 1, vr)) return false;
+        } else if (va >= 0 && va < 8 && va % 2 == 0) {
+          const int32_t co = obj_find(s.id_ctr(vr), s.id_actor(vr));
+          if (co < 0) return fail(PATCH_U_VALUE);
+          if (!kv_set(kd, s.id_ctr(vr), s.id_actor(vr), 2, co)) return false;
+        }
+      }
+    }
+    if (whole_doc) return true;  // documentPatch at load: only objectMeta is kept
+    // patchKey / patchValue (new.js:933-977)
+    bool have_pv = false;
+    DVal pv = {};
+    int64_t pk_c = 0;
+    int32_t pk_a = 0;
+    const int64_t tag = s.val_len(row);
+    if (overwritten && action == 1 && (tag & 0x0f) == 8) {
+      if (w.ncs >= w.cap_cs) return fail(PATCH_U_CAPACITY);
+      int64_t cv;
+      if (!s.value_int((uint32_t)row, false, cv)) return fail(PATCH_U_VALUE);
+      const int32_t st = (int32_t)w.ncs++;
+      DCs& c = w.cs[st];
+      c.op_ctr = idc; c.op_actor = ida; c.value = cv; c.nleft = 0; c.next = -1; c.pad = 0;
+      for (uint32_t k = 0; k < s.f_nsucc(f); k++) {
+        if (s.f_succ_time(f, k) >= lim) continue;
+        const int64_t sc = s.f_succ_ctr(f, k);
+        const int32_t sa = s.f_succ_actor(f, k);
+        int32_t q = w.pst[ps].cm_head;
+        while (q >= 0 && !(w.cm[q].ctr == sc && w.cm[q].actor == sa)) q = w.cm[q].next;
+        if (q < 0) {
+          if (w.ncm >= w.cap_cm) return fail(PATCH_U_CAPACITY);
+          q = (int32_t)w.ncm++;
+          w.cm[q].ctr = sc; w.cm[q].actor = sa; w.cm[q].next = w.pst[ps].cm_head; w.cm[q].pad = 0;
+          w.pst[ps].cm_head = q;
+          c.nleft++;
+        } else if (w.cm[q].state != st) {
+          c.nleft++;  // counterStates[succOp] rebound to this counter; counted once per counter
+        }
+        w.cm[q].state = st;
+      }
+    } else if (action == 5) {
+      int32_t q = w.pst[ps].cm_head;
+      while (q >= 0 && !(w.cm[q].ctr == idc && w.cm[q].actor == ida)) q = w.cm[q].next;
+      if (q < 0) return fail(PATCH_E_UNKNOWN_COUNTER, idc, ida);
+      DCs& c = w.cs[w.cm[q].state];
+      const uint32_t t15 = (uint32_t)(tag & 15);
+      int64_t iv;
+      if (tag < 16 || !(t15 == 3 || t15 == 4 || t15 == 8 || t15 == 9) || !s.value_int((uint32_t)row, t15 == 3, iv))
+        return fail(PATCH_U_VALUE);
+      c.value += iv;
+      c.nleft--;  // delete counterState.succs[opId]
+      if (c.nleft == 0) {
+        have_pv = true;
+        pv.vtag = PV_COUNTER; pv.dt = 0; pv.v0 = c.value; pv.v1 = 0;
+        pk_c = c.op_ctr; pk_a = c.op_actor;
+      }
+    } else if (!overwritten) {
+      if (action == 1) {
+        if (!row_val(row, pv)) return false;
+        have_pv = true;
+        pk_c = idc; pk_a = ida;
+      } else if (action % 2 == 0) {
+        const int32_t co = obj_find(idc, ida);
+        if (co < 0) return fail(PATCH_U_VALUE);
+        patch_on(co);
+        pv = child_val(co);
+        have_pv = true;
+        pk_c = idc; pk_a = ida;
+      }
+    }
+    patch_on(ob);
+    if (!s.has_key(row)) {
+      // list / text object (new.js:983-1033)
+      const int64_t ec = elem_ctr(row);
+      const int32_t ea = elem_actor(row);
+      if (has_old && old_succ == 0 && w.pst[ps].action == 1) {
+        w.pst[ps].action = 2;
+        if (!convert_insert_to_update(ob, list_index, ec, ea)) return false;
+      }
+      if (have_pv) {
+        if (!w.pst[ps].action && !has_old) {
+          w.pst[ps].action = 1;
+          DEdit e = {};
+          e.action = PR_INSERT; e.index = list_index; e.ec = ec; e.ea = ea; e.oc = pk_c; e.oa = pk_a; e.v = pv;
+          return append_edit(ob, e);
+        } else if (w.pst[ps].action == 3) {
+          const int32_t lt = w.obj[ob].edit_tail;
+          if (lt < 0 || w.ed[lt].action != PR_REMOVE) return fail(PATCH_U_VALUE);  // 'last edit has unexpected type'
+          if (w.ed[lt].count > 1) w.ed[lt].count--;
+          else edit_pop(ob);
+          w.pst[ps].action = 2;
+          return append_update(ob, list_index, ec, ea, pk_c, pk_a, pv, true);
+        } else {
+          const bool fst = !w.pst[ps].action;
+          if (!w.pst[ps].action) w.pst[ps].action = 2;
+          return append_update(ob, list_index, ec, ea, pk_c, pk_a, pv, fst);
+        }
+      } else if (has_old && old_succ == 0 && !w.pst[ps].action) {
+        w.pst[ps].action = 3;
+        DEdit e = {};
+        e.action = PR_REMOVE; e.index = list_index; e.count = 1;
+        return append_edit(ob, e);
+      }
+      return true;
+    }
+    // map / table object (new.js:1035-1039)
+    const int32_t pr = prop_get(ob, row, first_op);
+    if (pr < 0) return false;
+    if (have_pv) return prop_set(pr, pk_c, pk_a, pv);
+    return true;
+  }
+
+  // ---- seekWithinBlock over the rows present before stream position W (new.js:50-192) ----
+  struct Cur { int32_t f; };
+  AM_PHD void cur_norm(Cur& c, int64_t W) const {
+    while (c.f < (int32_t)s.nout() && rtime(s.frow(c.f)) >= W) c.f++;
+  }
+  AM_PHD int32_t cur_read(Cur& c, int64_t W) const {  // row, or -1 past the end (readValue -> null)
+    cur_norm(c, W);
+    if (c.f >= (int32_t)s.nout()) return -1;
+    return s.frow(c.f++);
+  }
+  AM_PHD bool cur_done(Cur& c, int64_t W) const {
+    cur_norm(c, W);
+    return c.f >= (int32_t)s.nout();
+  }
+  AM_PHD void cur_skip(Cur& c, uint32_t k, int64_t W) const {
+    for (uint32_t q = 0; q < k; q++)
+      if (cur_read(c, W) < 0) break;
+  }
+  // (row, current succ count) of the next present row
+  AM_PHD int32_t cur_read_succ(Cur& c, int64_t W, int64_t& nsucc) const {
+    cur_norm(c, W);
+    if (c.f >= (int32_t)s.nout()) { nsucc = -1; return -1; }
+    nsucc = (int64_t)nsucc_at(c.f, W);
+    return s.frow(c.f++);
+  }
+
+  // The seek of an op with object (q_oc, q_oa), key row `qrow` (or element (q_kc, q_ka) when
+  // key_row < 0), insert flag and id. Returns false for 'Reference element not found'.
+  AM_PHD bool seek(int64_t q_oc, int32_t q_oa, int32_t qrow, int64_t q_kc, int32_t q_ka, bool q_ins, int64_t q_idc,
+                   int32_t q_ida, int64_t W, uint32_t& skip, int64_t& vis) const {
+    Cur objA{0}, objC{0}, keyS{0}, idA{0}, idC{0}, ins{0}, act{0}, succ{0};
+    skip = 0;
+    vis = 0;
+    bool elem_visible = false;
+    int64_t n_oc = -1;
+    int32_t n_oa = -1;
+    if (q_oc >= 0) {
+      while (!cur_done(objC, W) || !cur_done(objA, W) || !cur_done(act, W)) {
+        const int32_t a = cur_read(objC, W), b = cur_read(objA, W);
+        n_oc = a >= 0 ? s.obj_ctr(a) : -1;
+        n_oa = b >= 0 ? s.obj_actor(b) : -1;
+        cur_read(act, W);
+        if (n_oc < 0 || n_oa < 0 || n_oc < q_oc || (n_oc == q_oc && act_lt(n_oa, q_oa))) skip++;
+        else break;
+      }
+    }
+    if (n_oc != q_oc || n_oa != q_oa) return true;
+    if (qrow >= 0 && s.has_key(qrow)) {
+      cur_skip(keyS, skip, W);
+      while (!cur_done(keyS, W)) {
+        const int32_t a = cur_read(objA, W), b = cur_read(objC, W), k = cur_read(keyS, W);
+        const int32_t noa = a >= 0 ? s.obj_actor(a) : -1;
+        const int64_t noc = b >= 0 ? s.obj_ctr(b) : -1;
+        if (s.has_key(k) && s.key_cmp(k, qrow) < 0 && noc == q_oc && noa == q_oa) skip++;
+        else break;
+      }
+      return true;
+    }
+    cur_skip(idC, skip, W); cur_skip(idA, skip, W); cur_skip(ins, skip, W); cur_skip(succ, skip, W);
+    int64_t n_idc = -1;
+    int32_t n_ida = -1;
+    bool n_ins = false;
+    int64_t n_succ = -1;  // -1: null
+    auto rd_id = [&]() {
+      const int32_t a = cur_read(idC, W), b = cur_read(idA, W);
+      n_idc = a >= 0 ? s.id_ctr(a) : -1;
+      n_ida = b >= 0 ? s.id_actor(b) : -1;
+    };
+    auto rd_obj = [&]() {
+      const int32_t a = cur_read(objC, W), b = cur_read(objA, W);
+      n_oc = a >= 0 ? s.obj_ctr(a) : -1;
+      n_oa = b >= 0 ? s.obj_actor(b) : -1;
+    };
+    auto rd_ins_succ = [&]() {
+      const int32_t a = cur_read(ins, W);
+      n_ins = a >= 0 ? s.insert(a) : false;
+      cur_read_succ(succ, W, n_succ);
+    };
+    auto visit = [&]() {
+      if (n_ins) elem_visible = false;
+      if (n_succ == 0 && !elem_visible) { vis++; elem_visible = true; }
+    };
+    rd_id();
+    rd_ins_succ();
+    if (q_ins) {
+      if (q_kc > 0 && q_ka >= 0) {
+        skip++;
+        while (!cur_done(idC, W) && !cur_done(idA, W) && (n_idc != q_kc || n_ida != q_ka)) {
+          visit();
+          rd_id();
+          rd_obj();
+          rd_ins_succ();
+          if (n_oc == q_oc && n_oa == q_oa) skip++;
+          else break;
+        }
+        if (n_oc != q_oc || n_oa != q_oa || n_idc != q_kc || n_ida != q_ka || !n_ins) return false;
+        visit();
+        if (cur_done(idC, W) || cur_done(idA, W)) return true;
+        rd_id();
+        rd_obj();
+        rd_ins_succ();
+      }
+      for (;;) {
+        const bool greater = n_idc >= 0 && (n_idc > q_idc || (n_idc == q_idc && act_lt(q_ida, n_ida)));
+        if (!((!n_ins || greater) && n_oc == q_oc && n_oa == q_oa)) break;
+        skip++;
+        visit();
+        if (!cur_done(idC, W) && !cur_done(idA, W)) {
+          rd_id();
+          rd_obj();
+          rd_ins_succ();
+        } else {
+          break;
+        }
+      }
+    } else if (q_kc > 0 && q_ka >= 0) {
+      while ((!n_ins || n_idc != q_kc || n_ida != q_ka) && n_oc == q_oc && n_oa == q_oa) {
+        skip++;
+        visit();
+        if (!cur_done(idC, W) && !cur_done(idA, W)) {
+          rd_id();
+          rd_obj();
+          rd_ins_succ();
+        } else {
+          break;
+        }
+      }
+      if (n_oc != q_oc || n_oa != q_oa || n_idc != q_kc || n_ida != q_ka || !n_ins) return false;
+    }
+    return true;
+  }
+
+  // ---- mergeDocChangeOps (new.js:1052-1290) for the window starting at stream index `pos` ----
+  AM_PHD bool oid_add(int32_t ob) {
+    for (uint32_t k = 0; k < w.noid; k++) if (w.oids[k] == ob) return true;
+    if (w.noid >= w.cap_oid) return fail(PATCH_U_CAPACITY);
+    w.oids[w.noid++] = ob;
+    return true;
+  }
+  AM_PHD int32_t srow(uint32_t p) const { return (int32_t)(s.nb() + p); }  // stream index -> row
+
+  AM_PHD bool apply_ops(uint32_t& pos, uint32_t pend) {
+    const int64_t W = pos;  // rows present: time < W
+    const int32_t first = srow(pos);
+    const bool insert = s.insert(first);
+    const int64_t f_oc = s.obj_ctr(first);
+    const int32_t f_oa = s.obj_actor(first);
+    uint32_t skip;
+    int64_t visible;
+    if (!seek(f_oc, f_oa, first, s.key_ctr(first), s.key_actor(first), insert, s.id_ctr(first), s.id_actor(first), W, skip,
+              visible))
+      return fail(PATCH_U_VALUE);  // Reference element not found (the merge reports it first)
+    if (s.has_key(first)) visible = 0;
+    int64_t list_index = visible;
+    const int32_t ob = obj_find(f_oa < 0 ? -1 : f_oc, f_oa);
+    if (ob < 0) return fail(PATCH_U_VALUE);  // objectMeta[objectId] undefined
+    const int32_t author = s.id_actor(first);
+    bool found_list_elem = false, elem_visible = false;
+    w.npst = 0; w.nvis = 0; w.ncs = 0; w.ncm = 0;  // propState = {}
+    // the first doc op: the present row after `skip` present rows
+    Cur dc{0};
+    cur_skip(dc, skip, W);
+    cur_norm(dc, W);
+    int32_t doc_f = dc.f < (int32_t)s.nout() ? dc.f : -1;  // F position of docOp, -1: null
+    if (doc_f >= 0) dc.f++;
+    uint32_t doc_old = doc_f >= 0 ? nsucc_at(doc_f, W) : 0u;
+    uint32_t nc = 0, seen_top = 0;
+    int32_t change_op = -1;
+    bool have_lck = false;
+    int32_t lck_row = -1;
+    if (!oid_add(ob)) return false;
+    for (;;) {
+      if (nc == 0) {
+        found_list_elem = false;
+        seen_top = 0;
+        while (pos < pend) {
+          const int32_t nx = srow(pos);
+          if (!(s.id_actor(nx) == author && s.insert(nx) == insert && s.obj_ctr(nx) == f_oc && s.obj_actor(nx) == f_oa)) break;
+          const int32_t last = nc > 0 ? w.cops[nc - 1] : -1;
+          bool is_overwrite = false;
+          for (uint32_t i = 0; i < s.npred(nx); i++)
+            for (uint32_t k = 0; k < nc; k++)
+              if (s.pred_actor(nx, i) == s.id_actor(w.cops[k]) && s.pred_ctr(nx, i) == s.id_ctr(w.cops[k])) is_overwrite = true;
+          const int32_t dr0 = doc_f >= 0 ? s.frow(doc_f) : -1;
+          bool take = false;
+          if (nx == first) take = true;
+          else if (insert && last >= 0 && !s.has_key(nx) && s.key_actor(nx) == s.id_actor(last) && s.key_ctr(nx) == s.id_ctr(last))
+            take = true;
+          else if (!insert && last >= 0 && s.has_key(nx) && s.has_key(last) && s.key_eq(nx, last) && !is_overwrite)
+            take = true;
+          else if (!insert && last >= 0 && !s.has_key(nx) && !s.has_key(last) && s.key_actor(nx) == s.key_actor(last) &&
+                   s.key_ctr(nx) == s.key_ctr(last) && !is_overwrite)
+            take = true;
+          else if (!insert && last < 0 && !s.has_key(nx) && dr0 >= 0 && s.insert(dr0) && !s.has_key(dr0) &&
+                   s.id_actor(dr0) == s.key_actor(nx) && s.id_ctr(dr0) == s.key_ctr(nx))
+            take = true;
+          else if (!insert && last < 0 && s.has_key(nx) && have_lck && s.key_cmp(lck_row, nx) < 0)
+            take = true;
+          if (!take) break;
+          have_lck = s.has_key(nx);
+          lck_row = nx;
+          if (nc >= w.cap_cops || seen_top + s.npred(nx) > w.cap_seen) return fail(PATCH_U_CAPACITY);
+          w.cops[nc] = nx;
+          w.seen_off[nc] = seen_top;
+          for (uint32_t k = 0; k < s.npred(nx); k++) w.seen[seen_top + k] = 0;
+          seen_top += s.npred(nx);
+          nc++;
+          pos++;  // readNextChangeOp
+        }
+      }
+      if (nc > 0) change_op = w.cops[0];
+      const int32_t dr = doc_f >= 0 ? s.frow(doc_f) : -1;
+      const bool in_obj = dr >= 0 && s.obj_actor(dr) == s.obj_actor(change_op) && s.obj_ctr(dr) == s.obj_ctr(change_op);
+      const bool key_matches = dr >= 0 && s.has_key(dr) && s.has_key(change_op) && s.key_eq(dr, change_op);
+      const bool elem_matches = dr >= 0 && !s.has_key(dr) && !s.has_key(change_op) &&
+                                ((!s.insert(dr) && s.key_actor(dr) == s.key_actor(change_op) && s.key_ctr(dr) == s.key_ctr(change_op)) ||
+                                 (s.insert(dr) && s.id_actor(dr) == s.key_actor(change_op) && s.id_ctr(dr) == s.key_ctr(change_op)));
+      if (nc == 0 && !(in_obj && (key_matches || elem_matches))) break;
+      bool take_doc = false;
+      uint32_t take_chg = 0;
+      if (insert || !in_obj || (!s.has_key(dr) && s.has_key(change_op)) ||
+          (s.has_key(dr) && s.has_key(change_op) && s.key_cmp(change_op, dr) < 0)) {
+        take_chg = nc;
+        if (!in_obj && !found_list_elem && !s.has_key(change_op) && !s.insert(change_op))
+          return fail(PATCH_U_VALUE);  // 'could not find list element with ID'
+      } else if (key_matches || elem_matches || found_list_elem) {
+        // the doc op gains every pulled op whose pred names it (its succ list as of `pos`)
+        for (uint32_t oi = 0; oi < nc; oi++) {
+          const int32_t op = w.cops[oi];
+          for (uint32_t i = 0; i < s.npred(op); i++)
+            if (s.pred_actor(op, i) == s.id_actor(dr) && s.pred_ctr(op, i) == s.id_ctr(dr)) {
+              w.seen[w.seen_off[oi] + i] = 1;
+              break;
+            }
+        }
+        if (elem_matches) found_list_elem = true;
+        if (found_list_elem && !elem_matches) {
+          take_chg = nc;
+        } else if (nc == 0 || s.id_ctr(dr) < s.id_ctr(change_op) ||
+                   (s.id_ctr(dr) == s.id_ctr(change_op) && act_lt(s.id_actor(dr), author))) {
+          take_doc = true;
+          if (!update_property(ob, dr, doc_f, (int64_t)pos, list_index, true, doc_old, false)) return false;
+          // a deletion whose preds have all been seen leaves no row (new.js:1205-1217)
+          for (uint32_t i = nc; i-- > 0;) {
+            const int32_t op = w.cops[i];
+            bool deleted = true;
+            for (uint32_t j = 0; j < s.npred(op); j++) if (!w.seen[w.seen_off[i] + j]) deleted = false;
+            if (s.action(op) == 3 && deleted) {
+              for (uint32_t k = i; k + 1 < nc; k++) { w.cops[k] = w.cops[k + 1]; w.seen_off[k] = w.seen_off[k + 1]; }
+              nc--;
+            }
+          }
+        } else if (s.id_ctr(dr) == s.id_ctr(change_op) && s.id_actor(dr) == author) {
+          return fail(PATCH_U_VALUE);  // duplicate operation ID (the merge reports it first)
+        } else {
+          take_chg = 1;
+        }
+      } else {
+        take_doc = true;
+      }
+      if (take_doc) {
+        if (s.insert(dr) && elem_visible) { elem_visible = false; list_index++; }
+        if (nsucc_at(doc_f, (int64_t)pos) == 0) elem_visible = true;
+        cur_norm(dc, W);
+        doc_f = dc.f < (int32_t)s.nout() ? dc.f : -1;
+        if (doc_f >= 0) { dc.f++; doc_old = nsucc_at(doc_f, W); }
+      }
+      if (take_chg > 0) {
+        for (uint32_t i = 0; i < take_chg; i++) {
+          const int32_t op = w.cops[i];
+          for (uint32_t j = 0; j < s.npred(op); j++)
+            if (!w.seen[w.seen_off[i] + j]) return fail(PATCH_U_VALUE);  // no matching operation for pred
+          if (!update_property(ob, op, -1, (int64_t)pos, list_index, false, 0, false)) return false;
+          if (s.insert(op)) { elem_visible = false; list_index++; }
+          else elem_visible = true;
+        }
+        for (uint32_t k = 0; k + take_chg < nc; k++) { w.cops[k] = w.cops[k + take_chg]; w.seen_off[k] = w.seen_off[k + take_chg]; }
+        nc -= take_chg;
+      }
+    }
+    return true;
+  }
+
+  // ---- objectMeta after documentPatch of the base document (new.js:1604-1635) ----
+  AM_PHD bool build_meta() {
+    if (obj_new(-1, -1, 0) < 0) return false;
+    int64_t last_oc = -2;
+    int32_t last_oa = -2;
+    bool elem_visible = false;
+    int64_t list_index = 0;
+    int32_t ob = 0;
+    w.npst = 0; w.nvis = 0; w.ncs = 0; w.ncm = 0;
+    for (uint32_t i = 0; i < s.nb(); i++) {
+      const int32_t r = (int32_t)i;
+      const int64_t oc = s.obj_ctr(r);
+      const int32_t oa = s.obj_actor(r);
+      if (oc != last_oc || oa != last_oa) {
+        last_oc = oc; last_oa = oa;
+        w.npst = 0; w.nvis = 0; w.ncs = 0; w.ncm = 0;
+        list_index = 0;
+        elem_visible = false;
+        ob = obj_find(oa < 0 ? -1 : oc, oa);
+        if (ob < 0) return fail(PATCH_U_VALUE);
+      }
+      const int32_t f = w.fpos[r];
+      if (f < 0) return fail(PATCH_U_VALUE);
+      const uint32_t ns = nsucc_at(f, 0);
+      if (s.insert(r) && elem_visible) { elem_visible = false; list_index++; }
+      if (ns == 0) elem_visible = true;
+      if (!update_property(ob, r, f, 0, list_index, true, ns, true)) return false;
+    }
+    return true;
+  }
+
+  // ---- setupPatches (new.js:1461-1528) ----
+  AM_PHD bool setup_patches() {
+    for (uint32_t oi = 0; oi < w.noid; oi++) {
+      int32_t ob = w.oids[oi], child = -1;
+      bool exists = false;
+      for (;;) {
+        int32_t kids = -1;
+        bool has_children = false;
+        if (child >= 0) {
+          kids = kid_find(ob, w.obj[child].pk_row, false);
+          if (kids < 0) return fail(PATCH_U_VALUE);
+          has_children = w.kid[kids].n > 0;
+        }
+        patch_on(ob);
+        if (child >= 0 && has_children) {
+          if (w.obj[ob].type == 1 || w.obj[ob].type == 2) {
+            for (int32_t e = w.obj[ob].edit_tail; e >= 0; e = w.ed[e].prev) {
+              const DEdit& ed = w.ed[e];
+              if (ed.action != PR_INSERT && ed.action != PR_UPDATE) continue;  // edit.opId
+              for (int32_t k = w.kid[kids].head; k >= 0; k = w.kv[k].next)
+                if (w.kv[k].ctr == ed.oc && w.kv[k].actor == ed.oa) exists = true;
+            }
+            if (!exists) {
+              // seekToOp of an update of the element (parentKey) over the final document
+              uint32_t skip;
+              int64_t vis;
+              const int32_t pk = w.obj[child].pk_row;
+              if (!seek(w.obj[ob].ctr, w.obj[ob].actor, -1, elem_ctr(pk), elem_actor(pk), false, 0, -1,
+                        (int64_t)s.nrows(), skip, vis))
+                return fail(PATCH_U_VALUE);
+              for (int32_t k = w.kid[kids].head; k >= 0; k = w.kv[k].next) {
+                DVal v;
+                if (w.kv[k].kind == 2) { patch_on(w.kv[k].ref); v = child_val(w.kv[k].ref); }
+                else if (!row_val(w.kv[k].ref, v)) return false;
+                DEdit e = {};
+                e.action = PR_UPDATE; e.index = vis; e.oc = w.kv[k].ctr; e.oa = w.kv[k].actor; e.v = v;
+                if (!append_edit(ob, e)) return false;
+              }
+            }
+          } else {
+            const int32_t pr = prop_get(ob, w.obj[child].pk_row, false);
+            if (pr < 0) return false;
+            for (int32_t k = w.kid[kids].head; k >= 0; k = w.kv[k].next) {
+              DVal v;
+              if (w.kv[k].kind == 2) { patch_on(w.kv[k].ref); v = child_val(w.kv[k].ref); }
+              else if (!row_val(w.kv[k].ref, v)) return false;
+              bool existed = false;
+              if (!prop_set(pr, w.kv[k].ctr, w.kv[k].actor, v, &existed)) return false;
+              if (existed) exists = true;
+            }
+          }
+        }
+        if (exists || w.obj[ob].parent < 0 || (child >= 0 && !has_children)) break;
+        child = ob;
+        ob = w.obj[ob].parent;
+      }
+    }
+    return true;
+  }
+
+  // ---- the log ----
+  AM_PHD bool emit() {
+    for (uint32_t a = 0; a < s.nactors(); a++) {
+      PatchRec r = {};
+      r.tag = PR_ACTOR;
+      const uint32_t l = s.actor_len(a);
+      if (o.nheap + l > o.cap_heap) return fail(PATCH_U_CAPACITY);
+      s.copy_actor(a, o.heap + o.nheap);
+      r.v0 = (int64_t)o.nheap; r.v1 = l; r.a1 = (int32_t)a;
+      o.nheap += l;
+      if (!patch_push(o, r)) { ok = false; return false; }
+    }
+    for (uint32_t c = 0; c < s.nchg(); c++) {  // clock: last seq per actor, first-appearance order
+      bool later = false;
+      for (uint32_t d = c + 1; d < s.nchg() && !later; d++) later = s.chg_actor(d) == s.chg_actor(c);
+      if (later) continue;
+      PatchRec r = {};
+      r.tag = PR_CLOCK; r.a1 = (int32_t)s.chg_actor(c); r.index = s.chg_seq(c);
+      if (!patch_push(o, r)) { ok = false; return false; }
+    }
+    for (uint32_t ob = 0; ob < w.nobj; ob++) {
+      const DObj& d = w.obj[ob];
+      if (!d.has_patch) continue;
+      PatchRec h = {};
+      h.tag = PR_OBJ; h.c1 = d.ctr; h.a1 = d.actor; h.dt = (uint32_t)d.type;
+      if (!patch_push(o, h)) { ok = false; return false; }
+      for (int32_t p = d.prop_head; p >= 0; p = w.prop[p].next) {
+        PatchRec k = {};
+        k.tag = PR_KEY;
+        const uint32_t kl = s.key_len(w.prop[p].key_row);
+        if (o.nheap + kl > o.cap_heap) return fail(PATCH_U_CAPACITY);
+        s.copy_key(w.prop[p].key_row, o.heap + o.nheap);
+        k.v0 = (int64_t)o.nheap; k.v1 = kl;
+        o.nheap += kl;
+        if (!patch_push(o, k)) { ok = false; return false; }
+        for (int32_t e = w.prop[p].head; e >= 0; e = w.pe[e].next) {
+          PatchRec r = {};
+          r.tag = PR_PROP; r.c2 = w.pe[e].ctr; r.a2 = w.pe[e].actor;
+          r.vtag = w.pe[e].v.vtag; r.dt = w.pe[e].v.dt; r.v0 = w.pe[e].v.v0; r.v1 = w.pe[e].v.v1;
+          if (!patch_push(o, r)) { ok = false; return false; }
+        }
+      }
+      uint32_t ne = 0;
+      for (int32_t e = d.edit_tail; e >= 0; e = w.ed[e].prev) w.tmp[ne++] = e;
+      for (uint32_t q = ne; q-- > 0;) {
+        const DEdit& e = w.ed[w.tmp[q]];
+        PatchRec r = {};
+        r.tag = e.action; r.index = e.index;
+        if (e.action == PR_REMOVE) {
+          r.n = (uint32_t)e.count;
+        } else if (e.action == PR_MULTI) {
+          r.c1 = e.ec; r.a1 = e.ea; r.dt = e.mdt; r.n = e.nmv;
+          uint32_t nv = 0;  // values, oldest first
+          for (int32_t m = e.mv_tail; m >= 0 && nv < e.nmv; m = w.mv[m].prev) w.tmp[ne + nv++] = m;
+          for (uint32_t k = nv; k-- > 0;) {
+            const DVal& v = w.mv[w.tmp[ne + k]].v;
+            if (!patch_push_val(o, v.vtag, v.dt, v.v0, v.v1)) { ok = false; return false; }
+          }
+        } else {
+          r.c1 = e.ec; r.a1 = e.ea; r.c2 = e.oc; r.a2 = e.oa;
+          r.vtag = e.v.vtag; r.dt = e.v.dt; r.v0 = e.v.v0; r.v1 = e.v.v1;
+        }
+        if (!patch_push(o, r)) { ok = false; return false; }
+      }
+    }
+    return true;
+  }
+
+  AM_PHD bool run() {
+    for (uint32_t r = 0; r < s.nrows(); r++) w.fpos[r] = -1;
+    for (uint32_t f = 0; f < s.nout(); f++) w.fpos[s.frow((int32_t)f)] = (int32_t)f;
+    if (!build_meta()) return false;
+    uint32_t pos = 0;
+    const uint32_t nstream = s.nrows() - s.nb();
+    for (uint32_t p = 0; p < s.npass() && ok; p++) {
+      const uint32_t pend = s.pass_end(p) < nstream ? s.pass_end(p) : nstream;
+      while (pos < pend && ok)
+        if (!apply_ops(pos, pend)) return false;
+    }
+    if (!setup_patches()) return false;
+    return emit();
+  }
+};
+
+template <class Src>
+AM_PHD inline bool diff_scan(const Src& src, PatchOut& o, DiffScratch& w) {
+  o.nrec = o.nmval = o.nheap = 0;
+  o.status = 0;
+  o.arg0 = o.arg1 = 0;
+  Diff<Src> d(src, w, o);
+  return d.run();
+}

@@ -117,7 +117,7 @@ __host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t n
 }
 
 __host__ __device__ inline bool fast_eligible(const DocBounds& b, const am_doc_desc& dd) {
-  if (dd.flags & AM_DOC_WANT_PATCH) return false;
+  if (dd.flags & (AM_DOC_WANT_PATCH | AM_DOC_WANT_DIFF)) return false;
   if (b.B == 0 || doc_scattered(b)) return false;
   if (dd.base_chunk < 0 && dd.chg_count == 0) return false;
   if (b.span_hi - b.span_lo > FD_SPAN_MAX) return false;

@@ -267,6 +267,8 @@ __device__ static void plan_doc(DocShared& s, const am_doc_desc& dd, const Chunk
       nall++;
       na_pass++;
     }
+    // pass boundaries of the applied op stream (the applyChanges patch replays pass by pass)
+    if (na_pass > 0 && s.b.P == 2) reinterpret_cast<uint32_t*>(s.ws + L.passend)[s.npass++] = nrow - s.nb;
     nq = ne;
     if (nq == 0) break;
     if (na_pass == 0) {
@@ -795,6 +797,85 @@ struct RowSrc {
   __device__ int64_t chg_seq(uint32_t c) const { return chg[c].seq; }
 };
 
+// P8 source (am_diff.h): rows in stream order, F = the merged document order
+struct DiffSrc {
+  const Row* rows;
+  const Ent* ents;       // base succ entries / change preds
+  const SortRec* sr;
+  const uint32_t* soff;  // exclusive scan of succ counts (document order)
+  const Ent* fent;       // final succ entries
+  const int32_t* etime;  // stream time of each final succ entry's op
+  const uint32_t* pend;
+  uint32_t np, nbase, nr, nf, nsucc_total;
+  const ActorRef* actors;
+  uint32_t na;
+  const ChgRow* chg;
+  uint32_t nc;
+  APtr A;
+  __device__ uint32_t nb() const { return nbase; }
+  __device__ uint32_t nrows() const { return nr; }
+  __device__ uint32_t nout() const { return nf; }
+  __device__ int32_t frow(int32_t f) const { return sr[f].row; }
+  __device__ uint32_t f_nsucc(int32_t f) const { return ((uint32_t)f + 1 < nf ? soff[f + 1] : nsucc_total) - soff[f]; }
+  __device__ int64_t f_succ_ctr(int32_t f, uint32_t k) const { return fent[soff[f] + k].ctr; }
+  __device__ int32_t f_succ_actor(int32_t f, uint32_t k) const { return fent[soff[f] + k].actor; }
+  __device__ int64_t f_succ_time(int32_t f, uint32_t k) const { return etime[soff[f] + k]; }
+  __device__ const Row& r(int32_t i) const { return rows[i]; }
+  __device__ int64_t obj_ctr(int32_t i) const { const int64_t v = r(i).obj_ctr; return v == AM_NULL64 ? -1 : v; }
+  __device__ int32_t obj_actor(int32_t i) const { return r(i).obj_actor; }
+  __device__ int64_t key_ctr(int32_t i) const { const int64_t v = r(i).key_ctr; return v == AM_NULL64 ? -1 : v; }
+  __device__ int32_t key_actor(int32_t i) const { return r(i).key_actor; }
+  __device__ bool has_key(int32_t i) const { return r(i).key_len != AM_NOSTR; }
+  __device__ uint32_t key_len(int32_t i) const { return r(i).key_len; }
+  __device__ int key_cmp(int32_t i, int32_t j) const {
+    return utf16_cmp_dev(A + r(i).key_off, r(i).key_len, A + r(j).key_off, r(j).key_len);
+  }
+  __device__ bool key_eq(int32_t i, int32_t j) const {
+    return r(i).key_len == r(j).key_len && bytes_eq(A + r(i).key_off, A + r(j).key_off, r(i).key_len);
+  }
+  __device__ void copy_key(int32_t i, uint8_t* d) const {
+    const uint8_t* p = A + r(i).key_off;
+    for (uint32_t q = 0; q < r(i).key_len; q++) d[q] = p[q];
+  }
+  __device__ int64_t id_ctr(int32_t i) const { return r(i).id_ctr; }
+  __device__ int32_t id_actor(int32_t i) const { return r(i).id_actor; }
+  __device__ bool insert(int32_t i) const { return r(i).insert != 0; }
+  __device__ int64_t action(int32_t i) const { const int64_t v = r(i).action; return v == AM_NULL64 ? -1 : v; }
+  __device__ uint32_t npred(int32_t i) const { return (uint32_t)i >= nbase ? r(i).ps_cnt : 0u; }
+  __device__ int64_t pred_ctr(int32_t i, uint32_t k) const { return ents[r(i).ps_off + k].ctr; }
+  __device__ int32_t pred_actor(int32_t i, uint32_t k) const { return ents[r(i).ps_off + k].actor; }
+  __device__ uint32_t rank(int32_t a) const { return actors[a].rank; }
+  // patch_value source (am_patch.h), by row
+  __device__ int64_t val_len(uint32_t i) const { const int64_t v = rows[i].val_len; return v == AM_NULL64 ? 0 : v; }
+  __device__ uint32_t vbytes(uint32_t i) const { return (uint32_t)((uint64_t)val_len(i) >> 4); }
+  __device__ void copy_value(uint32_t i, uint8_t* d) const {
+    const uint8_t* p = A + rows[i].val_off;
+    const uint32_t nb2 = vbytes(i);
+    for (uint32_t q = 0; q < nb2; q++) d[q] = p[q];
+  }
+  __device__ bool value_int(uint32_t i, bool is_uint, int64_t& out) const {
+    Rd rd{A + rows[i].val_off, vbytes(i), 0};
+    return (is_uint ? rd_u53(rd, out) : rd_i53(rd, out)) == AM_OK;
+  }
+  __device__ int64_t value_f64_bits(uint32_t i) const {
+    const uint8_t* p = A + rows[i].val_off;
+    uint64_t b = 0;
+    for (int q = 7; q >= 0; q--) b = (b << 8) | p[q];
+    return (int64_t)b;
+  }
+  __device__ uint32_t nactors() const { return na; }
+  __device__ uint32_t actor_len(uint32_t a) const { return actors[a].len; }
+  __device__ void copy_actor(uint32_t a, uint8_t* d) const {
+    const uint8_t* p = A + actors[a].off;
+    for (uint32_t q = 0; q < actors[a].len; q++) d[q] = p[q];
+  }
+  __device__ uint32_t nchg() const { return nc; }
+  __device__ int64_t chg_actor(uint32_t c) const { return chg[c].actor; }
+  __device__ int64_t chg_seq(uint32_t c) const { return chg[c].seq; }
+  __device__ uint32_t npass() const { return np; }
+  __device__ uint32_t pass_end(uint32_t p) const { return pend[p]; }
+};
+
 __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
                                                const am_doc_desc* __restrict__ docs, const am_known_hash* __restrict__ known,
                                                const ChunkInfo* __restrict__ info, const DocBounds* __restrict__ bounds,
@@ -817,6 +898,7 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
     s.has_base = dd.base_chunk >= 0;
     s.nb = s.nbe = s.nbc = s.nbd = 0;
     s.napplied = s.nqueued = s.nactors = s.nheads = 0;
+    s.npass = 0;
     s.nrows = s.nents = s.nchg = s.ndeps = s.nout = s.nnew = 0;
     s.max_op = 0;
     s.out_len = 0;
@@ -1256,6 +1338,16 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
     }
     if (t == 0) { s.nout = NOUT; s.nnew = NSUCC; }
     __syncthreads();
+    // applyChanges patch (P8): stream time of every succ entry's op while the id index is alive
+    // (-1: an op of the base document -- rows or deletions it recorded only as succ entries)
+    if (s.b.P == 2) {
+      int32_t* etime = reinterpret_cast<int32_t*>(wsg + L.etime);
+      for (uint32_t j = t; j < NSUCC; j += T) {
+        const int32_t r = id_lookup(idk, R, outent[j].ctr, outent[j].actor);
+        etime[j] = (r >= 0 && (uint32_t)r >= s.nb) ? r - (int32_t)s.nb : -1;
+      }
+    }
+    __syncthreads();
 #if defined(AM_STOP_PHASE) && AM_STOP_PHASE == 5
     goto done;
 #endif
@@ -1412,6 +1504,26 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
       ph->arg0 = po.arg0; ph->arg1 = po.arg1;
       ph->nrec = po.nrec; ph->nmval = po.nmval; ph->nheap = po.nheap;
       ph->max_op = pmax; ph->pad1 = 0;
+    }
+    // P8: the patch applyChanges returns (am_diff.h), lane 0, after the merge
+    if (s.b.P == 2 && t == 0) {
+      uint8_t* pbase = wsg + L.patch;
+      PatchOut po;
+      po.rec = reinterpret_cast<PatchRec*>(pbase + 64);
+      po.mval = reinterpret_cast<PatchVal*>(pbase + 64 + 64 * L.patch_nrec);
+      po.heap = pbase + 64 + 64 * L.patch_nrec + 32 * L.patch_nmval;
+      po.cap_rec = L.patch_nrec; po.cap_mval = L.patch_nmval; po.cap_heap = L.patch_heap;
+      DiffScratch dw;
+      diff_scratch_bind(wsg + L.dscr, s.b.R, s.b.E, dw);
+      DiffSrc src{rows, ents, sr, succ_cnt, outent, reinterpret_cast<const int32_t*>(wsg + L.etime),
+                  reinterpret_cast<const uint32_t*>(wsg + L.passend), s.npass, s.nb, s.nrows, NOUT, NSUCC, actors,
+                  s.nactors, chg, NC, A};
+      diff_scan(src, po, dw);
+      PatchHdr* ph = reinterpret_cast<PatchHdr*>(pbase);
+      ph->status = po.status; ph->pad0 = 0;
+      ph->arg0 = po.arg0; ph->arg1 = po.arg1;
+      ph->nrec = po.nrec; ph->nmval = po.nmval; ph->nheap = po.nheap;
+      ph->max_op = 0; ph->pad1 = 0;
     }
     // heads for the host (hot region may be LDS): mirror into the global workspace
     if (kHotLds)

@@ -351,7 +351,7 @@ __global__ void __launch_bounds__(256) k_bounds(const am_doc_desc* __restrict__ 
   b.R = (uint32_t)R; b.E = (uint32_t)E; b.C = (uint32_t)C; b.D = (uint32_t)D; b.A = (uint32_t)A;
   b.H = (uint32_t)H; b.N = dd.chg_count; b.K = (uint32_t)(H + dd.known_count); b.AM = (uint32_t)AM;
   b.ND = (uint32_t)ND; b.S = S; b.B = B; b.span_lo = lo; b.span_hi = hi;
-  b.P = (dd.flags & AM_DOC_WANT_PATCH) ? 1u : 0u;
+  b.P = (dd.flags & AM_DOC_WANT_PATCH) ? 1u : (dd.flags & AM_DOC_WANT_DIFF) ? 2u : 0u;
   b.pad = 0;
   WsLayout L = ws_layout(b);
   bounds[d] = b;
@@ -451,6 +451,7 @@ struct DocShared {
   uint32_t napplied, nqueued, nactors, nheads;
   uint32_t nrows, nents, nchg, ndeps;     // totals after planning
   uint32_t nout, nnew;
+  uint32_t npass;                         // applyChanges passes that applied changes (P == 2)
   int64_t max_op;
   uint32_t col_len[OC_NCOLS + DC_NCOLS];
   uint32_t col_pos[OC_NCOLS + DC_NCOLS];

@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #include "am_common.h"
+#include "am_diff.h"
 
 #ifndef __HIPCC__
 #define AM_HD
@@ -31,7 +32,7 @@ struct DocBounds {
   uint32_t K;   // changeIndexByHash entries
   uint32_t AM;  // actor-map entries (sum of change actor lists)
   uint32_t ND;  // sum of change deps (plan)
-  uint32_t P;   // 1: write the getPatch() log (am_doc_desc.flags & AM_DOC_WANT_PATCH)
+  uint32_t P;   // 1: write the getPatch() log (AM_DOC_WANT_PATCH); 2: the applyChanges patch (AM_DOC_WANT_DIFF)
   uint32_t pad;
   uint64_t S;   // key + message string bytes over all rows
   uint64_t B;   // input bytes (base + changes)
@@ -52,7 +53,8 @@ struct WsLayout {
   uint64_t hot_total;
   // cold (offsets relative to the document's global workspace, after the hot mirror)
   uint64_t out, out_cap, total;
-  uint64_t patch, patch_nrec, patch_nmval, patch_heap;  // getPatch log (when P)
+  uint64_t patch, patch_nrec, patch_nmval, patch_heap;  // patch log (when P)
+  uint64_t etime, passend, dscr;  // applyChanges patch (P == 2): succ-entry times, pass ends, replay pools
   uint64_t colbuf[OC_NCOLS + DC_NCOLS];
 };
 
@@ -139,7 +141,7 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   // getPatch scratch: make ops (8+4+1 B) and counter states (8+4+8+4 B) per row, counter map
   // (8+4+4 B) per succ entry
   L.pscr = L.u0;
-  const uint64_t pscr_end = L.u0 + (b.P ? 13 * (R + 1) + 24 * (R + 1) + 16 * (E + 1) + 16 * 10 : 0);
+  const uint64_t pscr_end = L.u0 + (b.P == 1 ? 13 * (R + 1) + 24 * (R + 1) + 16 * (E + 1) + 16 * 10 : 0);
   if (pscr_end > uend) uend = pscr_end;
   o = uend;
   L.hot_total = o;
@@ -164,13 +166,26 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   cap += 64 + 10 * (uint64_t)b.A + b.B + 42 * (uint64_t)b.H + 25 * 20 + b.B;
   L.out_cap = cap;
   L.out = take(cap);
-  if (b.P) {
+  if (b.P == 1) {
     L.patch_nrec = 3 * R + b.A + C + 2;
     L.patch_nmval = R + 1;
     L.patch_heap = b.S + 2 * b.B + 16;
     L.patch = take(64 + 64 * L.patch_nrec + 32 * L.patch_nmval + L.patch_heap);
+  } else if (b.P == 2) {
+    // actors + clock + one section per object + keys + prop entries / edits (am_diff.h pools)
+    L.patch_nrec = b.A + C + 2 + 2 * (R + 2) + 8 * R + 128;
+    L.patch_nmval = 4 * R + 64;
+    L.patch_heap = b.S + 2 * b.B + 16;
+    L.patch = take(64 + 64 * L.patch_nrec + 32 * L.patch_nmval + L.patch_heap);
   } else {
     L.patch = L.patch_nrec = L.patch_nmval = L.patch_heap = 0;
+  }
+  if (b.P == 2) {
+    L.etime = take(4 * (E + 1));
+    L.passend = take(4 * (N + 1));
+    L.dscr = take(diff_scratch_bytes(R, E));
+  } else {
+    L.etime = L.passend = L.dscr = 0;
   }
   L.total = o;
   return L;

@@ -88,9 +88,11 @@ typedef struct am_doc_desc {
   uint32_t known_begin, known_count; // extra changeIndexByHash entries (hash, index)
   uint32_t flags;           // bit0: haveHashGraph (fresh doc, or host knows all change hashes)
                             // bit1: AM_DOC_WANT_PATCH -- also write the getPatch() log of the result
+                            // bit2: AM_DOC_WANT_DIFF -- also write the patch applyChanges returns
   uint32_t pad;
 } am_doc_desc;
 #define AM_DOC_WANT_PATCH 2u
+#define AM_DOC_WANT_DIFF 4u
 typedef struct am_known_hash {      // changeIndexByHash entry supplied by the host
   uint8_t hash[32];
   int64_t index;
@@ -152,7 +154,8 @@ int am_batch_chunk_results(am_batch *b, uint8_t *hashes32, int32_t *chg_state, u
 /* Merged document chunk (uncompressed columns) of one document. */
 int am_batch_doc_output(am_batch *b, uint32_t doc, uint8_t *dst, uint64_t cap, uint64_t *len);
 int am_batch_doc_heads(am_batch *b, uint32_t doc, uint8_t *dst32, uint32_t cap, uint32_t *n);
-/* getPatch() log of document `doc` (staged with AM_DOC_WANT_PATCH): PatchHdr | records | values |
+/* Patch log of document `doc`: the getPatch() log (staged with AM_DOC_WANT_PATCH) or the patch
+ * applyChanges returns (AM_DOC_WANT_DIFF, new.js:1862-1865): PatchHdr | records | values |
  * heap as described in automerge_amd/csrc/am_patch.h; materialized by automerge_amd/patch.py or
  * automerge_amd/js/backend.js. cap = 0 returns the size in *len. */
 int am_batch_doc_patch(am_batch *b, uint32_t doc, uint8_t *dst, uint64_t cap, uint64_t *len);
