@@ -21,6 +21,31 @@ sys.path.insert(0, ROOT)
 
 METRIC = "ops merged/sec (batched load+applyChanges) + decode GB/s at 1/2/4/8 GPUs"
 HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic_k_doc.json")
+
+
+def kernel_source_digest():
+    """SHA-256 (16 hex) of the HIP sources the engine is built from."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "automerge_amd", "csrc")
+    for f in sorted(glob.glob(os.path.join(csrc, "*.h")) + glob.glob(os.path.join(csrc, "*.hip"))):
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def measured_traffic(kernel):
+    """roofline.traffic: HBM bytes per launch from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes
+    (tools/gpu_prof.sh -> tools/traffic.py), only when they were measured on these exact sources."""
+    try:
+        rec = json.load(open(TRAFFIC_JSON))
+    except (OSError, ValueError):
+        return None
+    if rec.get("kernel") != kernel or rec.get("src_digest") != kernel_source_digest():
+        return None
+    return rec["traffic_bytes"]
 
 
 def cpu_baseline(arena, chunks, docs, seconds=12.0):
@@ -140,7 +165,7 @@ def main():
                    "docs_per_gpu": D, "total_docs": tot[0], "ops_per_doc_merged": 60,
                    "parallelism": "doc-sharded dp%d" % world},
         "roofline": {"kernel": dom, "bound": "hbm", "limiter": "latency (per-document dependent phases)", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": measured_traffic(dom),
                      "alg_bytes_per_launch": alg[dom], "avg_ms": times[dom]},
         "stage_ms": {"k_chunks(sha256+parse)": t_chunks, "k_bounds+scan": t_bounds, "k_doc(plan+decode+merge+encode)": t_doc,
                      "k_out_hash": t_hash},
