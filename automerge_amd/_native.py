@@ -69,6 +69,8 @@ _sigs = {
     "am_doc_clone": (P, [P]),
     "am_doc_free": (None, [P]),
     "am_doc_apply_changes": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t, C.POINTER(Error)]),
+    "am_doc_apply_changes_patch": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t, C.POINTER(u8p),
+                                             C.POINTER(C.c_size_t), C.POINTER(Error)]),
     "am_doc_save": (C.c_int, [P, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
     "am_doc_get_heads": (C.c_size_t, [P, P, C.c_size_t]),
     "am_doc_pending": (C.c_size_t, [P]),

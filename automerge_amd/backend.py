@@ -67,27 +67,35 @@ def free(backend):
     backend.frozen = True
 
 
-def _apply(backend, changes):
+def _apply(backend, changes, want_patch=False):
     s = _backend_state(backend)
     arr, lens, n = N.buf_array(changes)
     err = N.Error()
-    if N.lib.am_doc_apply_changes(s.ptr, arr, lens, n, C.byref(err)):
+    blob = None
+    if want_patch:
+        out, nb = N.u8p(), C.c_size_t()
+        if N.lib.am_doc_apply_changes_patch(s.ptr, arr, lens, n, C.byref(out), C.byref(nb), C.byref(err)):
+            N.raise_for(err)
+        blob = C.string_at(out, nb.value)
+        N.lib.am_free(out)
+    elif N.lib.am_doc_apply_changes(s.ptr, arr, lens, n, C.byref(err)):
         N.raise_for(err)
     backend.frozen = True
-    return BackendState(s, s.heads())
+    return BackendState(s, s.heads()), blob
 
 
 def applyChanges(backend, changes):
-    """Backend.applyChanges() (backend/backend.js:27-32). Returns (state, patch); patch
-    generation is not part of this engine yet, so the patch carries only the reference's
-    top-level fields (maxOp, clock-free deps, pendingChanges)."""
-    new = _apply(backend, changes)
-    return new, {"maxOp": maxOp(new), "deps": new.heads, "pendingChanges": pendingChanges(new)}
+    """Backend.applyChanges() (backend/backend.js:27-32, new.js:1796-1871). Returns (state, patch):
+    the patch's diffs are replayed on the GPU (k_doc phase P8, am_diff.h) and materialized by
+    automerge_amd/patch.py into {maxOp, clock, deps, pendingChanges, diffs}."""
+    from . import patch as P
+    new, blob = _apply(backend, changes, want_patch=True)
+    return new, P.materialize(blob, new.heads, pendingChanges(new), maxOp(new))
 
 
 def loadChanges(backend, changes):
     """Backend.loadChanges() (backend/backend.js:115-120)."""
-    return _apply(backend, changes)
+    return _apply(backend, changes)[0]
 
 
 def load(data, device=0):

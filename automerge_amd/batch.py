@@ -19,9 +19,14 @@ assert DOC_DT.itemsize == C.sizeof(N.DocDesc)
 assert RESULT_DT.itemsize == C.sizeof(N.DocResult)
 
 
-def pack(docs, device=0):
+WANT_PATCH = 2  # AM_DOC_WANT_PATCH: also write the getPatch() log of the merged document
+WANT_DIFF = 4   # AM_DOC_WANT_DIFF: also write the patch applyChanges returns
+
+
+def pack(docs, device=0, flags=0):
     """docs: iterable of (base_bytes | None, [change bytes]) -> (arena, chunks, docdescs).
-    Compressed inputs go through the host DEFLATE stage (am_stage_change / am_stage_document)."""
+    Compressed inputs go through the host DEFLATE stage (am_stage_change / am_stage_document).
+    flags: WANT_PATCH or WANT_DIFF for every document."""
     parts, chunks, descs = [], [], []
     off = 0
     for base, changes in docs:
@@ -36,7 +41,7 @@ def pack(docs, device=0):
             off += len(base)
         d["chg_begin"] = len(chunks)
         d["chg_count"] = len(changes)
-        d["flags"] = 0 if base else 1  # fresh documents have the full hash graph
+        d["flags"] = (0 if base else 1) | flags  # fresh documents have the full hash graph
         for c in changes:
             chunks.append((off, len(c), 0))
             parts.append(c)
@@ -73,8 +78,8 @@ class Batch:
         self.nchunks = len(chunks)
         self._keep = (arena, chunks, docs, known)
 
-    def stage_docs(self, docs):
-        self.stage(*pack(docs))
+    def stage_docs(self, docs, flags=0):
+        self.stage(*pack(docs, flags=flags))
 
     def run(self):
         if N.lib.am_batch_run(self._b):
@@ -116,6 +121,18 @@ class Batch:
             raise N.AutomergeError("automerge_amd: heads copy failed")
         raw = bytes(buf)
         return [raw[32 * k:32 * k + 32].hex() for k in range(min(n.value, nheads))]
+
+    def doc_patch(self, i):
+        """Patch log of document i (staged with WANT_PATCH or WANT_DIFF); automerge_amd.patch
+        materializes it."""
+        n = C.c_uint64()
+        rc = N.lib.am_batch_doc_patch(self._b, i, None, 0, C.byref(n))
+        if rc:
+            raise N.AutomergeError("automerge_amd: no patch log for document %d (%d)" % (i, rc))
+        buf = (C.c_uint8 * max(n.value, 1))()
+        if N.lib.am_batch_doc_patch(self._b, i, buf, n.value, C.byref(n)):
+            raise N.AutomergeError("automerge_amd: patch copy failed")
+        return bytes(buf)[:n.value]
 
     def stage_times(self):
         ms = (C.c_float * 4)()

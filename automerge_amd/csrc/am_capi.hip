@@ -601,13 +601,13 @@ struct OneResult {
   std::vector<int32_t> chg_state;
   std::vector<std::array<uint8_t, 32>> hashes;
   std::vector<std::array<uint8_t, 32>> heads;
-  std::vector<uint8_t> patch;  // getPatch log (want_patch)
+  std::vector<uint8_t> patch;  // patch log (patch_mode: 1 getPatch, 2 the applyChanges patch)
 };
 
 // Runs one document (optional base chunk + change list) through the GPU pipeline.
 bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified, const std::vector<std::vector<uint8_t>>& chg,
              const std::vector<am_known_hash>& known, bool have_graph, OneResult& res, std::vector<uint8_t>& arena, Err& err,
-             bool want_patch = false) {
+             int patch_mode = 0) {
   arena.clear();
   std::vector<am_chunk_desc> cds;
   am_doc_desc dd{};
@@ -625,7 +625,7 @@ bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified,
   }
   dd.known_begin = 0;
   dd.known_count = (uint32_t)known.size();
-  dd.flags = (have_graph ? 1u : 0u) | (want_patch ? AM_DOC_WANT_PATCH : 0u);
+  dd.flags = (have_graph ? 1u : 0u) | (patch_mode == 1 ? AM_DOC_WANT_PATCH : 0u) | (patch_mode == 2 ? AM_DOC_WANT_DIFF : 0u);
   am_batch* b = scratch_batch(e);
   am_error ce;
   if (am_batch_stage(b, arena.data(), arena.size(), cds.data(), (uint32_t)cds.size(), &dd, 1, known.data(),
@@ -661,7 +661,7 @@ bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified,
   am_batch_doc_heads(b, 0, hb.data(), res.r.nheads, &nh);
   res.heads.resize(nh);
   for (uint32_t i = 0; i < nh; i++) std::memcpy(res.heads[i].data(), hb.data() + 32 * i, 32);
-  if (want_patch) {
+  if (patch_mode) {
     uint64_t plen = 0;
     if (am_batch_doc_patch(b, 0, nullptr, 0, &plen)) {
       err = {AM_U_CAPACITY, false, "automerge_amd: patch copy failed"};
@@ -776,8 +776,32 @@ extern "C" am_doc* am_doc_load(am_engine* eng, const uint8_t* data, size_t len, 
   return d;
 }
 
-// Backend.applyChanges (backend/backend.js:27-32 -> BackendDoc.applyChanges, new.js:1796-1871)
-extern "C" int am_doc_apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* lens, size_t n, am_error* err) {
+// The error a patch log carries (getPatch or applyChanges: updatePatchProperty new.js:944,
+// decodeValue columnar.js:318); false when the log is clean.
+static bool patch_log_error(const std::vector<uint8_t>& log, Err& e) {
+  PatchHdr h;
+  std::memcpy(&h, log.data(), sizeof h);
+  if (!h.status) return false;
+  e = Err{h.status, false, ""};
+  if (h.status == AM_E_FLOAT_LEN) {
+    e.msg = fmt("Invalid length for floating point number: %lld", (long long)h.arg0);
+  } else if (h.status == AM_E_UNKNOWN_COUNTER) {
+    std::string actor = "?";
+    const PatchRec* recs = reinterpret_cast<const PatchRec*>(log.data() + sizeof h);
+    for (uint64_t i = 0; i < h.nrec && recs[i].tag == PR_ACTOR; i++)
+      if ((int64_t)recs[i].a1 == h.arg1) {
+        const uint8_t* heap = log.data() + sizeof h + sizeof(PatchRec) * h.nrec + sizeof(PatchVal) * h.nmval;
+        actor = hexs(heap + recs[i].v0, (size_t)recs[i].v1);
+      }
+    e.msg = fmt("increment operation %lld@%s for unknown counter", (long long)h.arg0, actor.c_str());
+  } else {
+    e.msg = fmt("automerge_amd: the patch is not supported for this document (code %u)", h.status);
+  }
+  return true;
+}
+
+static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* lens, size_t n, std::vector<uint8_t>* patch,
+                  am_error* err) {
   Err e;
   // decoded changes first, then the existing queue (new.js:1814)
   std::vector<std::vector<uint8_t>> orig, staged;
@@ -799,9 +823,15 @@ extern "C" int am_doc_apply_changes(am_doc* d, const uint8_t* const* bufs, const
   }
   OneResult res;
   std::vector<uint8_t> arena;
-  if (!run_one(d->eng, d->state.empty() ? nullptr : &d->state, false, staged, known, d->have_hash_graph, res, arena, e)) {
+  if (!run_one(d->eng, d->state.empty() ? nullptr : &d->state, false, staged, known, d->have_hash_graph, res, arena, e,
+               patch ? 2 : 0)) {
     to_c(e, err);
     return 1;
+  }
+  // the patch is part of the call: an error in it throws before the document changes (new.js:1838)
+  if (patch) {
+    if (patch_log_error(res.patch, e)) { to_c(e, err); return 1; }
+    patch->swap(res.patch);
   }
   // commit (new.js:1838-1860)
   const size_t base = d->state.empty() ? 0 : 1;
@@ -824,6 +854,27 @@ extern "C" int am_doc_apply_changes(am_doc* d, const uint8_t* const* bufs, const
   d->nchanges = res.r.nchanges;
   if (res.r.max_op > d->max_op) d->max_op = res.r.max_op;
   if (err) err->code = 0;
+  return 0;
+}
+
+// Backend.loadChanges (backend/backend.js:115-120): applyChanges without a patch
+extern "C" int am_doc_apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* lens, size_t n, am_error* err) {
+  return apply_changes(d, bufs, lens, n, nullptr, err);
+}
+
+// Backend.applyChanges (backend/backend.js:27-32 -> BackendDoc.applyChanges, new.js:1796-1871): the
+// patch log of the call (k_doc phase P8, am_diff.h) in *out (malloc'd, am_free)
+extern "C" int am_doc_apply_changes_patch(am_doc* d, const uint8_t* const* bufs, const size_t* lens, size_t n,
+                                          uint8_t** out, size_t* len, am_error* err) {
+  std::vector<uint8_t> log;
+  if (apply_changes(d, bufs, lens, n, &log, err)) return 1;
+  *out = static_cast<uint8_t*>(std::malloc(log.size() ? log.size() : 1));
+  if (!*out) {
+    to_c(Err{AM_U_CAPACITY, false, "automerge_amd: out of host memory"}, err);
+    return 1;
+  }
+  std::memcpy(*out, log.data(), log.size());
+  *len = log.size();
   return 0;
 }
 
@@ -906,25 +957,9 @@ extern "C" int am_doc_get_patch(am_doc* d, uint8_t** out, size_t* len, am_error*
     if (!run_one(d->eng, &d->state, false, {}, {}, d->have_hash_graph, res, arena, e, true)) { to_c(e, err); return 1; }
     log.swap(res.patch);
   }
-  PatchHdr h;
-  std::memcpy(&h, log.data(), sizeof h);
-  if (h.status) {  // the RangeError getPatch throws (new.js:944, columnar.js:318)
-    Err e{h.status, false, ""};
-    if (h.status == AM_E_FLOAT_LEN) {
-      e.msg = fmt("Invalid length for floating point number: %lld", (long long)h.arg0);
-    } else if (h.status == AM_E_UNKNOWN_COUNTER) {
-      std::string actor = "?";
-      const PatchRec* recs = reinterpret_cast<const PatchRec*>(log.data() + sizeof h);
-      for (uint64_t i = 0; i < h.nrec && recs[i].tag == PR_ACTOR; i++)
-        if ((int64_t)recs[i].a1 == h.arg1) {
-          const uint8_t* heap = log.data() + sizeof h + sizeof(PatchRec) * h.nrec + sizeof(PatchVal) * h.nmval;
-          actor = hexs(heap + recs[i].v0, (size_t)recs[i].v1);
-        }
-      e.msg = fmt("increment operation %lld@%s for unknown counter", (long long)h.arg0, actor.c_str());
-    } else {
-      e.msg = fmt("automerge_amd: getPatch is not supported for this document (code %u)", h.status);
-    }
-    to_c(e, err);
+  Err pe;
+  if (patch_log_error(log, pe)) {  // the RangeError getPatch throws (new.js:944, columnar.js:318)
+    to_c(pe, err);
     return 1;
   }
   *out = static_cast<uint8_t*>(std::malloc(log.size()));

@@ -165,8 +165,8 @@ static napi_value js_doc_free(napi_env env, napi_callback_info info) {
 
 // applyChanges(handle, [Uint8Array...]) -> undefined (throws on error; the document is unchanged then)
 static napi_value js_doc_apply(napi_env env, napi_callback_info info) {
-  size_t argc = 2;
-  napi_value argv[2];
+  size_t argc = 3;
+  napi_value argv[3];
   NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   DocBox* b = get_box(env, argv[0]);
   if (!b) return NULL;
@@ -188,11 +188,20 @@ static napi_value js_doc_apply(napi_env env, napi_callback_info info) {
       return NULL;
     }
   }
+  // third argument true: Backend.applyChanges -- return the patch log (am_doc_apply_changes_patch)
+  bool want_patch = false;
+  if (argc > 2) napi_get_value_bool(env, argv[2], &want_patch);
   am_error err;
-  int rc = am_doc_apply_changes(b->doc, bufs, lens, n, &err);
+  uint8_t* out = NULL;
+  size_t len = 0;
+  int rc = want_patch ? am_doc_apply_changes_patch(b->doc, bufs, lens, n, &out, &len, &err)
+                      : am_doc_apply_changes(b->doc, bufs, lens, n, &err);
   free(bufs); free(lens);
   if (rc) return throw_am(env, &err);
-  return NULL;
+  if (!want_patch) return NULL;
+  napi_value v = new_u8(env, out, len);
+  am_free(out);
+  return v;
 }
 
 static napi_value js_doc_save(napi_env env, napi_callback_info info) {

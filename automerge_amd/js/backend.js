@@ -11,9 +11,10 @@
  *
  * Hash-graph queries (getChanges, getChangesAdded, getChangeByHash, getMissingDeps) are host
  * traversals over the applied change buffers, as in new.js:1913-2020.
- * getPatch runs documentPatch on the GPU and materializes its log here.
- * Not on the GPU path yet: applyChanges patch diffs (SURVEY.md 8 a20), applyLocalChange
- * (8(f) row 3), and the change history of a loaded document (8(f) row 2); those throw.
+ * getPatch runs documentPatch on the GPU, applyChanges replays the patch of the call on the GPU
+ * (k_doc phase P8, am_diff.h); both logs are materialized here.
+ * Not on the GPU path yet: applyLocalChange (8(f) row 3) and the change history of a loaded
+ * document (8(f) row 2); those throw.
  */
 const path = require('path')
 const zlib = require('zlib')
@@ -44,17 +45,14 @@ function free(backend) {
   backend.frozen = true
 }
 
-function patchFor(state, heads) {
-  const c = native.docCounts(state)
-  return {maxOp: c.maxOp, deps: heads, pendingChanges: c.pending}
-}
-
+// Backend.applyChanges (backend.js:27-32, new.js:1796-1871): {maxOp, clock, deps, pendingChanges, diffs}
 function applyChanges(backend, changes) {
   const state = backendState(backend)
-  native.docApplyChanges(state, changes)
+  const log = native.docApplyChanges(state, changes, true)
   backend.frozen = true
   const heads = native.docHeads(state)
-  return [{state, heads}, patchFor(state, heads)]
+  const c = native.docCounts(state)
+  return [{state, heads}, materializePatch(log, heads, c.pending, c.maxOp)]
 }
 
 function applyLocalChange(backend) {
@@ -135,7 +133,9 @@ function materializePatch(log, deps, pendingChanges, maxOp) {
     switch (tag) {
       case PR.ACTOR: actors.push(toHex(heap.subarray(i64(r + 40), i64(r + 40) + i64(r + 48)))); break
       case PR.CLOCK: clock[actors[a1]] = index; break
-      case PR.OBJ: cur = a1 < 0 ? root : nodes.get(`${c1}@${a1}`); break
+      // getPatch logs announce an object in its parent first; applyChanges logs list object
+      // patches in objectMeta order, so a section may create its node
+      case PR.OBJ: cur = a1 < 0 ? root : node(c1, a1, dt); break
       case PR.KEY: key = utf8.decode(heap.subarray(i64(r + 40), i64(r + 40) + i64(r + 48))); cur.props[key] = {}; break
       case PR.PROP: cur.props[key][opid(c2, a2)] = value(vtag, dt, r + 40); break
       case PR.INSERT:

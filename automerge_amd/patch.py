@@ -120,9 +120,9 @@ def materialize(blob, deps, pending_changes, max_op=None, js_bytes=bytes):
             clock[actors[r["a1"]]] = int(r["index"])
         elif tag == PR_OBJ:
             a1 = int(r["a1"])
-            cur = root if a1 < 0 else nodes.get((int(r["c1"]), a1))
-            if cur is None:  # reachable objects are always announced by their parent first
-                raise RuntimeError("patch log: object %s before its parent" % opid(r["c1"], a1))
+            # getPatch logs announce an object in its parent first; applyChanges logs list the
+            # object patches in objectMeta order, so a section may create its node
+            cur = root if a1 < 0 else node(r["c1"], a1, dt)
         elif tag == PR_KEY:
             key = heap[v0:v0 + v1].decode("utf-8", "replace")
             cur["props"][key] = {}

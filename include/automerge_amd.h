@@ -5,7 +5,7 @@
  * with Automerge.setDefaultBackend(module) (src/automerge.js:147-149; module shape
  * backend/index.js:1-8). This library replaces the hot path behind it:
  *   am_doc_load            <- Backend.load             backend/backend.js:104-107, new.js:1695-1768
- *   am_doc_apply_changes   <- Backend.applyChanges     backend/backend.js:27-32,   new.js:1796-1871
+ *   am_doc_apply_changes_patch <- Backend.applyChanges backend/backend.js:27-32,   new.js:1796-1871
  *   (loadChanges = am_doc_apply_changes without a patch)   backend/backend.js:115-120
  *   am_doc_save            <- Backend.save             backend/backend.js:96-98,   new.js:2025-2047
  *   am_doc_get_heads       <- Backend.getHeads         backend/backend.js:134-136
@@ -182,7 +182,14 @@ am_doc *am_doc_init(am_engine *eng);
 am_doc *am_doc_load(am_engine *eng, const uint8_t *data, size_t len, am_error *err);
 am_doc *am_doc_clone(const am_doc *doc);
 void am_doc_free(am_doc *doc);
+/* Backend.loadChanges: applies without producing a patch */
 int am_doc_apply_changes(am_doc *doc, const uint8_t *const *bufs, const size_t *lens, size_t n, am_error *err);
+/* Backend.applyChanges (backend/backend.js:27-32, new.js:1796-1871): applies and returns the patch log
+ * of the call (malloc'd, am_free; layout of am_batch_doc_patch). Its PR_CLOCK records are the clock;
+ * maxOp / deps / pendingChanges come from am_doc_max_op / am_doc_get_heads / am_doc_pending. An error
+ * the patch raises (unknown counter, float length) fails the call and leaves the document unchanged. */
+int am_doc_apply_changes_patch(am_doc *doc, const uint8_t *const *bufs, const size_t *lens, size_t n,
+                               uint8_t **patch, size_t *patch_len, am_error *err);
 /* Returns a malloc'd buffer (release with am_free). DEFLATE of columns >= 256 bytes is the
  * host stage (columnar.js:1052-1057). */
 int am_doc_save(am_doc *doc, uint8_t **out, size_t *len, am_error *err);

@@ -1,7 +1,8 @@
 'use strict'
 // Replays the golden scenarios (tests/golden/docs.json, produced by the reference backend) through
 // automerge_amd/js/backend.js -- the Node host over the N-API addon -- and reports mismatches of
-// save() bytes, heads, pending counts and thrown error class/message as one JSON line.
+// save() bytes, heads, pending counts, getPatch and applyChanges patches and thrown error
+// class/message as one JSON line.
 const fs = require('fs')
 const path = require('path')
 const B = require(path.join(__dirname, '..', '..', 'automerge_amd', 'js', 'backend.js'))
@@ -17,7 +18,7 @@ const canon = x => {
   return x
 }
 const bad = []
-let steps = 0, patches = 0
+let steps = 0, patches = 0, applied = 0
 for (const sc of docs) {
   let st = null
   for (let i = 0; i < sc.steps.length; i++) {
@@ -28,7 +29,12 @@ for (const sc of docs) {
       else {
         if (st === null) st = B.init()
         const old = st
-        ;[st] = B.applyChanges(st, step.changes.map(hex))
+        let applyPatch
+        ;[st, applyPatch] = B.applyChanges(st, step.changes.map(hex))
+        if (exp.patch) {
+          applied++
+          if (JSON.stringify(canon(applyPatch)) !== JSON.stringify(canon(exp.patch))) bad.push([sc.name, i, 'applyChanges patch'])
+        }
         try { B.save(old); bad.push([sc.name, i, 'old handle not frozen']) } catch (e) {
           if (!/outdated Automerge document/.test(e.message)) bad.push([sc.name, i, 'frozen message', e.message])
         }
@@ -63,4 +69,4 @@ if (sc) {
   graph = {changes: got.length, applied_equal_given: JSON.stringify(got.slice().sort()) === JSON.stringify(all.slice().sort()),
            missing: B.getMissingDeps(st), since_heads: B.getChanges(st, B.getHeads(st)).length}
 }
-console.log(JSON.stringify({scenarios: docs.length, steps, patches, bad: bad.slice(0, 20), nbad: bad.length, graph}))
+console.log(JSON.stringify({scenarios: docs.length, steps, patches, applied, bad: bad.slice(0, 20), nbad: bad.length, graph}))

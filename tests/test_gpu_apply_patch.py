@@ -1,0 +1,110 @@
+"""The patch Backend.applyChanges returns (new.js:1796-1871), replayed on the GPU
+(k_doc phase P8, automerge_amd/csrc/am_diff.h) and materialized by automerge_amd/patch.py.
+
+* every apply step of every golden scenario through automerge_amd.backend.applyChanges, against
+  the reference's own patch (tests/golden/docs.json, produced by the reference);
+* the same steps as ONE batch launch (base = the step's previous saved state, the form the per-
+  document API hands the GPU), against the reference's patches;
+* seeded C4 / C2 batches (the bench's generator) against the CPU oracle's applyChanges patch
+  (oracle/am_apply_patch_oracle.inc, itself pinned by tests/test_apply_patch_oracle.py).
+"""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _jsonable(x):
+    if isinstance(x, (bytes, bytearray)):
+        return {"__bytes": bytes(x).hex()}
+    if isinstance(x, dict):
+        return {k: _jsonable(v) for k, v in x.items()}
+    if isinstance(x, list):
+        return [_jsonable(v) for v in x]
+    return x
+
+
+def test_apply_patch_per_step_matches_reference(docs):
+    from automerge_amd import _native as N
+    from automerge_amd import backend as B
+    n, bad = 0, []
+    for sc in docs:
+        st = None
+        for i, (step, exp) in enumerate(zip(sc["steps"], sc["results"])):
+            if step["op"] == "load":
+                st = B.load(bytes.fromhex(step["bytes"]))
+                continue
+            if st is None:
+                st = B.init()
+            try:
+                st, patch = B.applyChanges(st, [bytes.fromhex(c) for c in step["changes"]])
+                got = _jsonable(patch)
+            except N.AutomergeError as e:
+                got = {"error": str(e)}
+            if "error" in exp:
+                if got.get("error") != exp["error"]["message"]:
+                    bad.append((sc["name"], i, "error", got.get("error")))
+                break
+            n += 1
+            if got != exp["patch"]:
+                bad.append((sc["name"], i, got.get("error")))
+                break
+    assert n > 300
+    assert not bad, (len(bad), bad[:10])
+
+
+def _steps(docs):
+    """(base saved bytes | None, changes, expected patch) of every apply step whose previous state
+    had no queued changes."""
+    out = []
+    for sc in docs:
+        prev = None
+        for step, exp in zip(sc["steps"], sc["results"]):
+            if "error" in exp:
+                break
+            if step["op"] == "apply" and "patch" in exp and not (prev and prev.get("pending")):
+                base = bytes.fromhex(prev["save"]) if prev else None
+                out.append((base, [bytes.fromhex(c) for c in step["changes"]], exp))
+            prev = exp
+    return out
+
+
+def test_apply_patch_one_batch_matches_reference(docs):
+    from automerge_amd import patch as P
+    from automerge_amd.batch import WANT_DIFF, Batch
+    steps = _steps(docs)
+    b = Batch()
+    b.stage_docs([(base, ch) for base, ch, _ in steps], flags=WANT_DIFF)
+    b.run()
+    b.sync()
+    res = b.results()
+    bad = []
+    for i, (_, _, exp) in enumerate(steps):
+        assert int(res[i]["status"]) == 0, (i, int(res[i]["status"]))
+        got = _jsonable(P.materialize(b.doc_patch(i), exp["heads"], exp["pending"], exp["patch"]["maxOp"]))
+        if got != exp["patch"]:
+            bad.append(i)
+    assert len(steps) > 300
+    assert not bad, (len(bad), bad[:10])
+
+
+@pytest.mark.parametrize("kind,first,n", [("c4", 3000, 400), ("c2", 500, 400)])
+def test_workload_apply_patch_matches_oracle(kind, first, n):
+    import oracle_ffi as O
+    from automerge_amd import patch as P
+    from automerge_amd import workload
+    from automerge_amd.batch import WANT_DIFF, Batch
+    arena, chunks, docs, _ = getattr(workload, kind)(first, n)
+    docs = docs.copy()
+    docs["flags"] |= WANT_DIFF
+    b = Batch()
+    b.stage(arena, chunks, docs)
+    b.run()
+    b.sync()
+    r = b.results()
+    for i in range(n):
+        base, changes = workload.doc_chunks(arena, chunks, docs, i)
+        ref = O.Doc.load(base) if base else O.Doc.init()
+        want = ref.apply_patch(changes)
+        assert int(r[i]["status"]) == 0, (i, int(r[i]["status"]))
+        got = _jsonable(P.materialize(b.doc_patch(i), want["deps"], want["pendingChanges"], want["maxOp"]))
+        assert got == want, i

@@ -27,7 +27,7 @@ def replay(sc):
             else:
                 if st is None:
                     st = B.init()
-                st, _ = B.applyChanges(st, [bytes.fromhex(c) for c in step["changes"]])
+                st = B.loadChanges(st, [bytes.fromhex(c) for c in step["changes"]])
             res["save"] = B.save(st).hex()
             res["heads"] = B.getHeads(st)
             res["pending"] = B.pendingChanges(st)
@@ -153,7 +153,7 @@ def test_getpatch_per_step_matches_reference(docs):
             else:
                 if st is None:
                     st = B.init()
-                st, _ = B.applyChanges(st, [bytes.fromhex(c) for c in step["changes"]])
+                st = B.loadChanges(st, [bytes.fromhex(c) for c in step["changes"]])
             want = dict(exp["getPatch"], pendingChanges=exp["pending"])
             try:
                 got = _jsonable(B.getPatch(st))
