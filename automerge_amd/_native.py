@@ -58,6 +58,7 @@ _sigs = {
     "am_batch_results": (C.c_int, [P, P]),
     "am_batch_chunk_results": (C.c_int, [P, P, P, P]),
     "am_batch_doc_output": (C.c_int, [P, C.c_uint32, P, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "am_batch_doc_save": (C.c_int, [P, C.c_uint32, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
     "am_batch_doc_heads": (C.c_int, [P, C.c_uint32, P, C.c_uint32, C.POINTER(C.c_uint32)]),
     "am_batch_stage_times": (C.c_int, [P, C.POINTER(C.c_float)]),
     "am_batch_workspace_bytes": (C.c_uint64, [P]),
@@ -91,6 +92,8 @@ _sigs = {
                                     C.POINTER(C.c_int), C.POINTER(Error)]),
     "am_workload_c4": (C.c_uint64, [C.c_uint64, C.c_uint32, P, C.c_uint64, P, P, C.POINTER(C.c_uint64), C.c_int]),
     "am_workload_c2": (C.c_uint64, [C.c_uint64, C.c_uint32, P, C.c_uint64, P, P, C.POINTER(C.c_uint64), C.c_int]),
+    "am_workload_text": (C.c_uint64, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, C.c_uint64, P, P,
+                                      C.POINTER(C.c_uint64), C.c_int]),
 }
 for _name, (_res, _args) in _sigs.items():
     _f = getattr(lib, _name)

@@ -114,6 +114,18 @@ class Batch:
             raise N.AutomergeError("automerge_amd: output copy failed (%d)" % rc)
         return bytes(buf)[:n.value]
 
+    def doc_save(self, i):
+        """Backend.save() bytes of document i: the merged chunk with its columns of >= 256 bytes
+        DEFLATEd (am_batch_doc_save)."""
+        out = N.u8p()
+        n = C.c_size_t()
+        err = N.Error()
+        if N.lib.am_batch_doc_save(self._b, i, C.byref(out), C.byref(n), C.byref(err)):
+            N.raise_for(err)
+        data = C.string_at(out, n.value)
+        N.lib.am_free(out)
+        return data
+
     def doc_heads(self, i, nheads):
         buf = (C.c_uint8 * (32 * max(nheads, 1)))()
         n = C.c_uint32()

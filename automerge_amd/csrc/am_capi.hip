@@ -878,8 +878,59 @@ extern "C" int am_doc_apply_changes_patch(am_doc* d, const uint8_t* const* bufs,
   return 0;
 }
 
-// Backend.save (new.js:2025-2047): DEFLATE of columns >= 256 bytes is the host stage; the
-// container checksum of the compressed form is computed on the GPU.
+// save() bytes of a merged document chunk as k_doc writes it (columns uncompressed): DEFLATE of
+// columns >= 256 bytes (deflateColumn, columnar.js:1052-1059, DEFLATE_MIN_SIZE :32) is the host
+// stage; the container checksum of the compressed form is computed on the GPU.
+static bool save_bytes(am_engine* eng, const std::vector<uint8_t>& state, std::vector<uint8_t>& bytes, Err& err) {
+  Container c;
+  DocParts parts;
+  if (!read_container(state.data(), state.size(), c) || !split_doc(state.data() + c.data_off, c.data_len, parts)) {
+    err = {AM_U_VALUE, false, "automerge_amd: corrupt internal state"};
+    return false;
+  }
+  bool any = false;
+  for (auto* cols : {&parts.ccols, &parts.ocols})
+    for (auto& col : *cols)
+      if (col.data.size() >= 256) {
+        std::vector<uint8_t> z;
+        if (!zdeflate(col.data.data(), col.data.size(), z)) { err = {AM_U_VALUE, false, "deflate failed"}; return false; }
+        col.data = std::move(z);
+        col.id |= COL_DEFLATE;
+        any = true;
+      }
+  if (!any) { bytes = state; return true; }
+  std::vector<uint8_t> body = join_doc(parts);
+  uint8_t zero[4] = {0, 0, 0, 0};
+  bytes = make_chunk(zero, 0, body);
+  std::vector<std::array<uint8_t, 32>> h;
+  if (!gpu_sha256(eng, {&bytes}, 8, h)) { err = {AM_U_CAPACITY, false, "automerge_amd: GPU hash failed"}; return false; }
+  std::memcpy(bytes.data() + 4, h[0].data(), 4);
+  return true;
+}
+
+/* Backend.save() bytes of batch document `doc` (am_batch_doc_output + the DEFLATE stage). */
+extern "C" int am_batch_doc_save(am_batch* b, uint32_t doc, uint8_t** out, size_t* len, am_error* err) {
+  uint64_t n = 0;
+  std::vector<uint8_t> raw;
+  if (am_batch_doc_output(b, doc, nullptr, 0, &n) > 2) { to_c(Err{AM_U_CAPACITY, false, "automerge_amd: output copy failed"}, err); return 1; }
+  raw.resize(n);
+  if (n && am_batch_doc_output(b, doc, raw.data(), n, &n)) {
+    to_c(Err{AM_U_CAPACITY, false, "automerge_amd: output copy failed"}, err);
+    return 1;
+  }
+  if (!n) { to_c(Err{AM_U_VALUE, false, "automerge_amd: document has no output (failed status)"}, err); return 1; }
+  std::vector<uint8_t> bytes;
+  Err e;
+  if (!save_bytes(b->eng, raw, bytes, e)) { to_c(e, err); return 1; }
+  *out = (uint8_t*)std::malloc(bytes.size() ? bytes.size() : 1);
+  if (!*out) { to_c(Err{AM_U_CAPACITY, false, "automerge_amd: out of host memory"}, err); return 1; }
+  std::memcpy(*out, bytes.data(), bytes.size());
+  *len = bytes.size();
+  if (err) err->code = 0;
+  return 0;
+}
+
+// Backend.save (new.js:2025-2047)
 extern "C" int am_doc_save(am_doc* d, uint8_t** out, size_t* len, am_error* err) {
   std::vector<uint8_t> bytes;
   if (d->has_binary) {
@@ -892,32 +943,8 @@ extern "C" int am_doc_save(am_doc* d, uint8_t** out, size_t* len, am_error* err)
     if (!run_one(d->eng, nullptr, false, {}, {}, true, res, arena, e)) { to_c(e, err); return 1; }
     bytes = res.out;
   } else {
-    Container c;
-    DocParts parts;
-    if (!read_container(d->state.data(), d->state.size(), c) || !split_doc(d->state.data() + c.data_off, c.data_len, parts)) {
-      to_c(Err{AM_U_VALUE, false, "automerge_amd: corrupt internal state"}, err);
-      return 1;
-    }
-    bool any = false;
-    for (auto* cols : {&parts.ccols, &parts.ocols})
-      for (auto& col : *cols)
-        if (col.data.size() >= 256) {  // DEFLATE_MIN_SIZE (columnar.js:32)
-          std::vector<uint8_t> z;
-          if (!zdeflate(col.data.data(), col.data.size(), z)) { to_c(Err{AM_U_VALUE, false, "deflate failed"}, err); return 1; }
-          col.data = std::move(z);
-          col.id |= COL_DEFLATE;
-          any = true;
-        }
-    if (!any) {
-      bytes = d->state;
-    } else {
-      std::vector<uint8_t> body = join_doc(parts);
-      uint8_t zero[4] = {0, 0, 0, 0};
-      bytes = make_chunk(zero, 0, body);
-      std::vector<std::array<uint8_t, 32>> h;
-      if (!gpu_sha256(d->eng, {&bytes}, 8, h)) { to_c(Err{AM_U_CAPACITY, false, "automerge_amd: GPU hash failed"}, err); return 1; }
-      std::memcpy(bytes.data() + 4, h[0].data(), 4);
-    }
+    Err e;
+    if (!save_bytes(d->eng, d->state, bytes, e)) { to_c(e, err); return 1; }
     d->binary = bytes;
     d->has_binary = true;
   }

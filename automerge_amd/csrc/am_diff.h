@@ -71,10 +71,24 @@ struct DiffScratch {
   int32_t* cops; uint8_t* seen;       // changeOps (rows) and predSeen flags
   uint32_t* seen_off;
   uint32_t cap_cops, cap_seen;
+  // O(log n) seek (Fenwick trees over F positions, see Diff::advance)
+  int32_t* bitp;                      // present rows
+  int32_t* bitv;                      // visible list elements (at their insert row)
+  int32_t* nsc;                       // succ count of the row at F position f, as of the replay time
+  int32_t* live;                      // element (insert-row F position): present rows with no succ
+  int32_t* estart;                    // F position -> F position of its element's insert row, -1: map row
+  int32_t* hash; uint32_t hmask;      // element id -> F position of its insert row (open addressing)
+  uint32_t* ev_off; int32_t* ev;      // succ entries bucketed by the stream time of their op
 };
 
 // sizes of the pools for R rows and E pred/succ entries (host and device agree)
-AM_PHD inline void diff_caps(uint64_t R, uint64_t E, uint64_t caps[16]) {
+#define DIFF_NCAPS 24
+AM_PHD inline uint64_t diff_hash_cap(uint64_t R) {
+  uint64_t h = 16;
+  while (h < 2 * R + 2) h <<= 1;
+  return h;
+}
+AM_PHD inline void diff_caps(uint64_t R, uint64_t E, uint64_t caps[DIFF_NCAPS]) {
   caps[0] = R + 2;          // obj
   caps[1] = R + 2;          // kid
   caps[2] = 4 * R + 64;     // kv
@@ -91,18 +105,27 @@ AM_PHD inline void diff_caps(uint64_t R, uint64_t E, uint64_t caps[16]) {
   caps[13] = 8 * R + 128;   // tmp
   caps[14] = R + 2;         // cops (+ seen_off)
   caps[15] = E + 2;         // seen
+  caps[16] = R + 2;         // bitp
+  caps[17] = R + 2;         // bitv
+  caps[18] = R + 2;         // nsc
+  caps[19] = R + 2;         // live
+  caps[20] = R + 2;         // estart
+  caps[21] = diff_hash_cap(R);  // hash
+  caps[22] = R + 2;         // ev_off
+  caps[23] = E + 2;         // ev
 }
 AM_PHD inline uint64_t diff_scratch_bytes(uint64_t R, uint64_t E) {
-  uint64_t c[16];
+  uint64_t c[DIFF_NCAPS];
   diff_caps(R, E, c);
-  const uint64_t sz[16] = {sizeof(DObj), sizeof(DKid), sizeof(DKV), sizeof(DProp), sizeof(DPE), sizeof(DEdit), sizeof(DMV),
-                           sizeof(DPst), sizeof(DVis), sizeof(DCs), sizeof(DCm), 4, 4, 4, 8, 1};
+  const uint64_t sz[DIFF_NCAPS] = {sizeof(DObj), sizeof(DKid), sizeof(DKV), sizeof(DProp), sizeof(DPE), sizeof(DEdit),
+                                   sizeof(DMV), sizeof(DPst), sizeof(DVis), sizeof(DCs), sizeof(DCm), 4, 4, 4, 8, 1,
+                                   4, 4, 4, 4, 4, 4, 4, 4};
   uint64_t t = 0;
-  for (int i = 0; i < 16; i++) t += (c[i] * sz[i] + 15) & ~(uint64_t)15;
+  for (int i = 0; i < DIFF_NCAPS; i++) t += (c[i] * sz[i] + 15) & ~(uint64_t)15;
   return t;
 }
 AM_PHD inline void diff_scratch_bind(uint8_t* p, uint64_t R, uint64_t E, DiffScratch& w) {
-  uint64_t c[16];
+  uint64_t c[DIFF_NCAPS];
   diff_caps(R, E, c);
   uint64_t o = 0;
   auto take = [&](uint64_t bytes) { uint8_t* at = p + o; o += (bytes + 15) & ~(uint64_t)15; return at; };
@@ -125,6 +148,14 @@ AM_PHD inline void diff_scratch_bind(uint8_t* p, uint64_t R, uint64_t E, DiffScr
   w.cap_cops = (uint32_t)c[14];
   w.seen = take(c[15]);
   w.cap_seen = (uint32_t)c[15];
+  w.bitp = reinterpret_cast<int32_t*>(take(c[16] * 4));
+  w.bitv = reinterpret_cast<int32_t*>(take(c[17] * 4));
+  w.nsc = reinterpret_cast<int32_t*>(take(c[18] * 4));
+  w.live = reinterpret_cast<int32_t*>(take(c[19] * 4));
+  w.estart = reinterpret_cast<int32_t*>(take(c[20] * 4));
+  w.hash = reinterpret_cast<int32_t*>(take(c[21] * 4)); w.hmask = (uint32_t)c[21] - 1;
+  w.ev_off = reinterpret_cast<uint32_t*>(take(c[22] * 4));
+  w.ev = reinterpret_cast<int32_t*>(take(c[23] * 4));
   w.nobj = w.nkid = w.nkv = w.nprop = w.npe = w.ned = w.nmv = w.npst = w.nvis = w.ncs = w.ncm = w.noid = 0;
 }
 
@@ -145,7 +176,161 @@ struct Diff {
   DiffScratch& w;
   PatchOut& o;
   bool ok;
+  uint32_t cur_t = 0;   // succ / row events of stream times < cur_t are in the trees
+  int32_t ptotal = 0;   // present rows
   AM_PHD Diff(const Src& src, DiffScratch& ws, PatchOut& out) : s(src), w(ws), o(out), ok(true) {}
+
+  // ---- replay state in Fenwick trees over F positions ----
+  // The reference seeks by scanning the document (seekWithinBlock, new.js:50-192): the position
+  // of an op is the number of present rows before it, and its list index the number of visible
+  // elements before it in its object. Here both are prefix sums at the op's F position: `bitp`
+  // counts present rows, `bitv` counts elements (at their insert row) with at least one present
+  // row without a succ -- exactly the rows visit() counts. advance(W) applies, in stream order,
+  // the rows and succ entries whose op precedes stream position W, so seek and the doc cursor
+  // cost O(log n) instead of O(rows).
+  AM_PHD static uint32_t lsb(uint32_t i) { return i & (~i + 1u); }
+  AM_PHD void bit_add(int32_t* b, uint32_t i, int32_t v) {
+    const uint32_t n = s.nout();
+    for (++i; i <= n; i += lsb(i)) b[i] += v;
+  }
+  AM_PHD int32_t bit_pre(const int32_t* b, uint32_t i) const {  // sum over F positions [0, i)
+    int32_t r = 0;
+    for (; i > 0; i -= lsb(i)) r += b[i];
+    return r;
+  }
+  AM_PHD uint32_t bit_kth(const int32_t* b, int32_t k) const {  // F position of the k-th (1-based) counted one
+    const uint32_t n = s.nout();
+    uint32_t pos = 0, step = 1;
+    while (step * 2 <= n) step *= 2;
+    for (; step; step >>= 1)
+      if (pos + step <= n && b[pos + step] < k) { pos += step; k -= b[pos]; }
+    return pos;
+  }
+  // first present F position >= f, or nout()
+  AM_PHD int32_t next_present(int32_t f) const {
+    if (f >= (int32_t)s.nout()) return (int32_t)s.nout();
+    const int32_t k = bit_pre(w.bitp, (uint32_t)f);
+    return k >= ptotal ? (int32_t)s.nout() : (int32_t)bit_kth(w.bitp, k + 1);
+  }
+  AM_PHD uint32_t hslot(int64_t ctr, int32_t actor) const {
+    uint64_t h = (uint64_t)ctr * 0x9E3779B97F4A7C15ull ^ ((uint64_t)(uint32_t)actor + 1u) * 0xC2B2AE3D27D4EB4Full;
+    return (uint32_t)(h >> 32) & w.hmask;
+  }
+  AM_PHD int32_t elem_find(int64_t ctr, int32_t actor) const {  // F position of the insert row, -1
+    for (uint32_t h = hslot(ctr, actor);; h = (h + 1) & w.hmask) {
+      const int32_t f = w.hash[h];
+      if (f < 0) return -1;
+      const int32_t r = s.frow(f);
+      if (s.id_ctr(r) == ctr && s.id_actor(r) == actor) return f;
+    }
+  }
+  AM_PHD void elem_row_live(int32_t f, int32_t d) {
+    const int32_t e = w.estart[f];
+    if (e < 0) return;
+    const int32_t before = w.live[e];
+    w.live[e] += d;
+    if (before == 0 && d > 0) bit_add(w.bitv, (uint32_t)e, 1);
+    else if (before > 0 && w.live[e] == 0) bit_add(w.bitv, (uint32_t)e, -1);
+  }
+  AM_PHD void fast_init() {
+    const uint32_t n = s.nout(), nstream = s.nrows() - s.nb();
+    for (uint32_t i = 0; i <= n; i++) { w.bitp[i] = 0; w.bitv[i] = 0; }
+    for (uint32_t h = 0; h <= w.hmask; h++) w.hash[h] = -1;
+    for (uint32_t t = 0; t <= nstream; t++) w.ev_off[t] = 0;
+    for (uint32_t f = 0; f < n; f++) {
+      const int32_t r = s.frow((int32_t)f);
+      w.nsc[f] = 0;
+      w.live[f] = 0;
+      if (s.has_key(r)) w.estart[f] = -1;
+      else if (s.insert(r)) w.estart[f] = (int32_t)f;
+      else w.estart[f] = f > 0 && w.estart[f - 1] >= 0 && s.obj_ctr(s.frow((int32_t)f - 1)) == s.obj_ctr(r) &&
+                                 s.obj_actor(s.frow((int32_t)f - 1)) == s.obj_actor(r) ? w.estart[f - 1] : -1;
+      if (!s.has_key(r) && s.insert(r)) {
+        uint32_t h = hslot(s.id_ctr(r), s.id_actor(r));
+        while (w.hash[h] >= 0) h = (h + 1) & w.hmask;
+        w.hash[h] = (int32_t)f;
+      }
+      for (uint32_t k = 0; k < s.f_nsucc(f); k++) {
+        const int64_t t = s.f_succ_time(f, k);
+        if (t < 0) w.nsc[f]++;
+        else if (t < (int64_t)nstream) w.ev_off[t + 1]++;
+      }
+    }
+    for (uint32_t t = 0; t < nstream; t++) w.ev_off[t + 1] += w.ev_off[t];
+    for (uint32_t f = 0; f < n; f++)  // bucket fill: ev_off[t] is the running cursor, restored below
+      for (uint32_t k = 0; k < s.f_nsucc(f); k++) {
+        const int64_t t = s.f_succ_time(f, k);
+        if (t >= 0 && t < (int64_t)nstream) w.ev[w.ev_off[t]++] = (int32_t)f;
+      }
+    for (uint32_t t = nstream; t > 0; t--) w.ev_off[t] = w.ev_off[t - 1];
+    w.ev_off[0] = 0;
+    ptotal = 0;
+    for (uint32_t f = 0; f < n; f++)
+      if (rtime(s.frow((int32_t)f)) < 0) {
+        bit_add(w.bitp, f, 1);
+        ptotal++;
+        if (w.nsc[f] == 0) elem_row_live((int32_t)f, 1);
+      }
+    cur_t = 0;
+  }
+  AM_PHD void advance(int64_t W) {
+    const uint32_t nstream = s.nrows() - s.nb();
+    while ((int64_t)cur_t < W && cur_t < nstream) {
+      const uint32_t t = cur_t++;
+      const int32_t f = w.fpos[srow(t)];
+      if (f >= 0) {
+        bit_add(w.bitp, (uint32_t)f, 1);
+        ptotal++;
+        if (w.nsc[f] == 0) elem_row_live(f, 1);
+      }
+      for (uint32_t q = w.ev_off[t]; q < w.ev_off[t + 1]; q++) {
+        const int32_t g = w.ev[q];
+        if (w.nsc[g]++ == 0 && rtime(s.frow(g)) < (int64_t)t) elem_row_live(g, -1);
+      }
+    }
+  }
+  // seek of the op at stream row `first` from the trees: (skip, visible) as seek() computes them.
+  // Returns false when the op has no F anchor (its element is unknown): seek() then decides.
+  AM_PHD bool fast_seek(int32_t first, uint32_t& skip, int64_t& vis) const {
+    const int64_t q_oc = s.obj_ctr(first);
+    const int32_t q_oa = s.obj_actor(first);
+    const int32_t n = (int32_t)s.nout();
+    auto obj_before = [&](int32_t r) {  // document order of objects: _root, then (ctr, actor)
+      if (q_oa < 0 || q_oc < 0) return false;
+      const int64_t oc = s.obj_ctr(r);
+      const int32_t oa = s.obj_actor(r);
+      if (oc < 0 || oa < 0) return true;
+      return oc < q_oc || (oc == q_oc && act_lt(oa, q_oa));
+    };
+    int32_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int32_t m = (lo + hi) / 2;
+      if (obj_before(s.frow(m))) lo = m + 1; else hi = m;
+    }
+    int32_t target;
+    if (s.has_key(first)) {
+      int32_t a = lo, b = n;
+      while (a < b) {
+        const int32_t m = (a + b) / 2;
+        const int32_t r = s.frow(m);
+        if (s.obj_ctr(r) == q_oc && s.obj_actor(r) == q_oa && s.has_key(r) && s.key_cmp(r, first) < 0) a = m + 1;
+        else b = m;
+      }
+      skip = (uint32_t)bit_pre(w.bitp, (uint32_t)a);
+      vis = 0;
+      return true;
+    }
+    if (s.insert(first)) {
+      target = w.fpos[first];
+    } else {
+      if (!(s.key_ctr(first) > 0 && s.key_actor(first) >= 0)) return false;
+      target = elem_find(s.key_ctr(first), s.key_actor(first));
+    }
+    if (target < 0) return false;
+    skip = (uint32_t)bit_pre(w.bitp, (uint32_t)target);
+    vis = (int64_t)(bit_pre(w.bitv, (uint32_t)target) - bit_pre(w.bitv, (uint32_t)lo));
+    return true;
+  }
 
   AM_PHD bool fail(uint32_t st, int64_t a0 = 0, int64_t a1 = 0) {
     if (ok) { o.status = st; o.arg0 = a0; o.arg1 = a1; }
@@ -359,7 +544,10 @@ struct Diff {
   }
 
   // ---- propState ----
-  AM_PHD int32_t pst_get(int32_t row) const {
+  // propState[elemId]. In a whole-document scan (documentPatch) the rows of one key / element are
+  // contiguous in document order, so only the last entry can match.
+  AM_PHD int32_t pst_get(int32_t row, bool whole_doc) const {
+    if (whole_doc) return w.npst && elem_eq(w.pst[w.npst - 1].elem_row, row) ? (int32_t)w.npst - 1 : -1;
     for (uint32_t k = 0; k < w.npst; k++) if (elem_eq(w.pst[k].elem_row, row)) return (int32_t)k;
     return -1;
   }
@@ -382,7 +570,7 @@ struct Diff {
       const int32_t kd = kid_find(ob, row, true);
       if (kd < 0 || !kv_set(kd, idc, ida, 2, nm)) return false;
     }
-    int32_t ps = pst_get(row);
+    int32_t ps = pst_get(row, whole_doc);
     const bool first_op = ps < 0;
     if (ps < 0) {
       if (w.npst >= w.cap_pst) return fail(PATCH_U_CAPACITY);
@@ -670,7 +858,9 @@ struct Diff {
     const int32_t f_oa = s.obj_actor(first);
     uint32_t skip;
     int64_t visible;
-    if (!seek(f_oc, f_oa, first, s.key_ctr(first), s.key_actor(first), insert, s.id_ctr(first), s.id_actor(first), W, skip,
+    advance(W);
+    if (!fast_seek(first, skip, visible) &&
+        !seek(f_oc, f_oa, first, s.key_ctr(first), s.key_actor(first), insert, s.id_ctr(first), s.id_actor(first), W, skip,
               visible))
       return fail(PATCH_U_VALUE);  // Reference element not found (the merge reports it first)
     if (s.has_key(first)) visible = 0;
@@ -681,9 +871,7 @@ struct Diff {
     bool found_list_elem = false, elem_visible = false;
     w.npst = 0; w.nvis = 0; w.ncs = 0; w.ncm = 0;  // propState = {}
     // the first doc op: the present row after `skip` present rows
-    Cur dc{0};
-    cur_skip(dc, skip, W);
-    cur_norm(dc, W);
+    Cur dc{(int32_t)skip < ptotal ? (int32_t)bit_kth(w.bitp, (int32_t)skip + 1) : (int32_t)s.nout()};
     int32_t doc_f = dc.f < (int32_t)s.nout() ? dc.f : -1;  // F position of docOp, -1: null
     if (doc_f >= 0) dc.f++;
     uint32_t doc_old = doc_f >= 0 ? nsucc_at(doc_f, W) : 0u;
@@ -784,7 +972,7 @@ struct Diff {
       if (take_doc) {
         if (s.insert(dr) && elem_visible) { elem_visible = false; list_index++; }
         if (nsucc_at(doc_f, (int64_t)pos) == 0) elem_visible = true;
-        cur_norm(dc, W);
+        dc.f = next_present(dc.f);
         doc_f = dc.f < (int32_t)s.nout() ? dc.f : -1;
         if (doc_f >= 0) { dc.f++; doc_old = nsucc_at(doc_f, W); }
       }
@@ -967,6 +1155,7 @@ struct Diff {
     for (uint32_t r = 0; r < s.nrows(); r++) w.fpos[r] = -1;
     for (uint32_t f = 0; f < s.nout(); f++) w.fpos[s.frow((int32_t)f)] = (int32_t)f;
     if (!build_meta()) return false;
+    fast_init();
     uint32_t pos = 0;
     const uint32_t nstream = s.nrows() - s.nb();
     for (uint32_t p = 0; p < s.npass() && ok; p++) {

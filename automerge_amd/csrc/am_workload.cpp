@@ -10,7 +10,10 @@
 #include <algorithm>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
+
+#include <zlib.h>
 
 #include "../../include/automerge_amd.h"
 
@@ -350,6 +353,132 @@ void gen_c2(uint32_t doc_index, DocOut& out) {
   out.ops = 14;
 }
 
+// deflateChange (columnar.js:798-808): chunks of >= DEFLATE_MIN_SIZE (256) bytes become type 2
+// with the chunk data raw-DEFLATEd (pako.deflateRaw defaults = zlib level 6, memLevel 8, wbits
+// -15); the magic bytes and the checksum of the uncompressed chunk are kept.
+Bytes maybe_deflate(Bytes b) {
+  if (b.size() < 256) return b;
+  size_t p = 9;
+  while (b[p] & 0x80) p++;
+  p++;
+  z_stream zs;
+  memset(&zs, 0, sizeof zs);
+  if (deflateInit2(&zs, 6, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return b;
+  Bytes z(deflateBound(&zs, b.size() - p) + 16);
+  zs.next_in = b.data() + p;
+  zs.avail_in = (uInt)(b.size() - p);
+  zs.next_out = z.data();
+  zs.avail_out = (uInt)z.size();
+  const int r = deflate(&zs, Z_FINISH);
+  const size_t zn = zs.total_out;
+  deflateEnd(&zs);
+  if (r != Z_STREAM_END) return b;
+  Bytes o(b.begin(), b.begin() + 8);
+  o.push_back(2);
+  pu(o, zn);
+  o.insert(o.end(), z.begin(), z.begin() + zn);
+  return o;
+}
+
+// Text editing histories. Two actors A, B share one text object
+// (change 0 by A: makeText at _root 'text' = 1@A). Changes alternate A, B, A, ... with
+// `per_change` ops each. Every op is, with probability 1/5 (and a non-empty view), a delete of a
+// random live element of the author's view (pred = [elemId]); otherwise an insert of one
+// lowercase character. The first insert of a change goes after a random live element of the
+// view (1/8: at the head), the following ones after the previous insert (typing).
+// The author's view is its own changes plus the other actor's changes up to its last crossing:
+// with cross_every > 0 each actor, at every cross_every-th change of its own, first absorbs all
+// of the other's changes so far (deps = heads of the view; C3 "interleaved"); with
+// cross_every == 0 the two actors never see each other (C1 "concurrent from the same base").
+// startOp = 1 + the largest op counter in the view (Lamport). Changes >= 256 B are deflated.
+// LCG call order per document (seed = doc index): make_actors(2); then per op one draw for
+// del/insert, one for the delete's element, or (first insert of a change) one for head-or-not
+// plus one for the element, then one for the character.
+void gen_text(uint32_t doc_index, uint32_t nchanges, uint32_t per_change, uint32_t cross_every, DocOut& out) {
+  uint32_t s = doc_index;
+  std::vector<Actor> actors;
+  make_actors(s, 2, actors);
+  const int A0 = 0;
+  uint8_t h0[32];
+  out.changes.push_back(maybe_deflate(encode_change(actors, A0, 1, 1, {}, {{-1, 0, "text", -1, 0, false, 4, 0, 0, "", {}}}, h0)));
+  struct Chg { std::vector<uint64_t> ins, del; int64_t last_op; std::vector<uint8_t> hash; };
+  struct View {
+    std::vector<uint64_t> live;                 // element ids (ctr << 1 | actor)
+    std::unordered_map<uint64_t, uint32_t> at;  // element -> index in live
+    std::vector<std::vector<uint8_t>> heads;
+    int64_t maxop = 1;
+    uint32_t absorbed = 0;                      // changes of the other actor in the view
+    int64_t seq = 0;
+    void add(uint64_t e) { at[e] = (uint32_t)live.size(); live.push_back(e); }
+    void remove(uint64_t e) {
+      auto it = at.find(e);
+      if (it == at.end()) return;
+      const uint32_t i = it->second;
+      at.erase(it);
+      const uint64_t last = live.back();
+      live.pop_back();
+      if (i < live.size()) { live[i] = last; at[last] = i; }
+    }
+  };
+  View v[2];
+  std::vector<Chg> hist[2];
+  for (int a = 0; a < 2; a++) v[a].heads.push_back(std::vector<uint8_t>(h0, h0 + 32));
+  v[0].seq = 1;
+  for (uint32_t k = 1; k <= nchanges; k++) {
+    const int a = (int)((k - 1) & 1), o = 1 - a;
+    View& V = v[a];
+    if (cross_every && (uint32_t)(hist[a].size() + 1) % cross_every == 0 && V.absorbed < hist[o].size()) {
+      for (uint32_t j = V.absorbed; j < hist[o].size(); j++) {
+        for (uint64_t e : hist[o][j].ins) V.add(e);
+        for (uint64_t e : hist[o][j].del) V.remove(e);
+        V.maxop = std::max(V.maxop, hist[o][j].last_op);
+      }
+      V.absorbed = (uint32_t)hist[o].size();
+      // my last change is an ancestor of the other's latest iff the other absorbed all of mine
+      std::vector<std::vector<uint8_t>> nh = {hist[o].back().hash};
+      if (!(hist[a].empty() || v[o].absorbed == hist[a].size())) nh.push_back(hist[a].back().hash);
+      V.heads = nh;
+    }
+    const int64_t start = V.maxop + 1;
+    std::vector<Op> ops;
+    Chg rec;
+    bool have_ref = false;
+    uint64_t ref = 0;
+    for (uint32_t i = 0; i < per_change; i++) {
+      const int64_t ctr = start + i;
+      if (lcg(s) % 5 == 0 && !V.live.empty()) {
+        const uint64_t e = V.live[lcg(s) % V.live.size()];
+        ops.push_back({A0, 1, "", (int)(e & 1), (int64_t)(e >> 1), false, 3, 0, 0, "", {{(int64_t)(e >> 1), (int)(e & 1)}}});
+        V.remove(e);
+        rec.del.push_back(e);
+      } else {
+        if (!have_ref) {
+          have_ref = true;
+          if (lcg(s) % 8 == 0 || V.live.empty()) ref = 0;
+          else ref = V.live[lcg(s) % V.live.size()];
+        }
+        const char c = (char)(97 + lcg(s) % 26);
+        if (ref == 0) ops.push_back({A0, 1, "", -1, 0, true, 1, 6, 0, std::string(1, c), {}});
+        else ops.push_back({A0, 1, "", (int)(ref & 1), (int64_t)(ref >> 1), true, 1, 6, 0, std::string(1, c), {}});
+        const uint64_t e = ((uint64_t)ctr << 1) | (uint64_t)a;
+        V.add(e);
+        rec.ins.push_back(e);
+        ref = e;
+      }
+    }
+    std::vector<std::vector<uint8_t>> deps = V.heads;
+    std::sort(deps.begin(), deps.end());
+    uint8_t h[32];
+    out.changes.push_back(maybe_deflate(encode_change(actors, a, ++V.seq, start, deps, ops, h)));
+    rec.last_op = start + per_change - 1;
+    rec.hash.assign(h, h + 32);
+    V.maxop = rec.last_op;
+    V.heads = {rec.hash};
+    hist[a].push_back(std::move(rec));
+  }
+  out.ops = 1 + (uint64_t)nchanges * per_change;
+}
+
 // Lays out documents [base?][changes...] back to back in the arena
 uint64_t layout(std::vector<DocOut>& outs, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks, am_doc_desc* docs,
                 uint64_t* ops_out) {
@@ -376,7 +505,7 @@ uint64_t layout(std::vector<DocOut>& outs, uint8_t* arena, uint64_t cap, am_chun
     docs[d].chg_count = (uint32_t)o.changes.size();
     docs[d].known_begin = 0;
     docs[d].known_count = 0;
-    docs[d].flags = 0;
+    docs[d].flags = o.base.empty() ? 1u : 0u;  // fresh documents have the full hash graph
     docs[d].pad = 0;
     for (auto& c : o.changes) {
       chunks[ci++] = {off, (uint32_t)c.size(), 0};
@@ -417,6 +546,16 @@ uint64_t am_workload_c4(uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap
 uint64_t am_workload_c2(uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks, am_doc_desc* docs,
                         uint64_t* ops_out, int nthreads) {
   return generate(gen_c2, first, n, arena, cap, chunks, docs, ops_out, nthreads);
+}
+
+/* Text editing histories (gen_text above; C1: cross_every 0, C3: cross_every 10): documents
+ * [first, first + n), each = Backend.init() + (1 + nchanges) change chunks, deflated when
+ * >= 256 B as encodeChange does. */
+uint64_t am_workload_text(uint64_t first, uint32_t n, uint32_t nchanges, uint32_t per_change, uint32_t cross_every,
+                          uint8_t* arena, uint64_t cap, am_chunk_desc* chunks, am_doc_desc* docs, uint64_t* ops_out,
+                          int nthreads) {
+  auto gen = [=](uint32_t d, DocOut& o) { gen_text(d, nchanges, per_change, cross_every, o); };
+  return generate(gen, first, n, arena, cap, chunks, docs, ops_out, nthreads);
 }
 
 }  // extern "C"

@@ -153,6 +153,9 @@ int am_batch_results(am_batch *b, am_doc_result *out);
 int am_batch_chunk_results(am_batch *b, uint8_t *hashes32, int32_t *chg_state, uint32_t *status);
 /* Merged document chunk (uncompressed columns) of one document. */
 int am_batch_doc_output(am_batch *b, uint32_t doc, uint8_t *dst, uint64_t cap, uint64_t *len);
+/* Backend.save() bytes of one document (backend.js:96-98, new.js:2025-2047): the merged chunk with
+ * columns >= 256 bytes DEFLATEd (deflateColumn, columnar.js:1052). *out is malloc'd (am_free). */
+int am_batch_doc_save(am_batch *b, uint32_t doc, uint8_t **out, size_t *len, am_error *err);
 int am_batch_doc_heads(am_batch *b, uint32_t doc, uint8_t *dst32, uint32_t cap, uint32_t *n);
 /* Patch log of document `doc`: the getPatch() log (staged with AM_DOC_WANT_PATCH) or the patch
  * applyChanges returns (AM_DOC_WANT_DIFF, new.js:1862-1865): PatchHdr | records | values |
@@ -255,6 +258,13 @@ uint64_t am_workload_c4(uint64_t first_doc, uint32_t ndocs, uint8_t *arena, uint
  * two concurrent changes incrementing the counter and overwriting k1), 3 chunks per document. */
 uint64_t am_workload_c2(uint64_t first_doc, uint32_t ndocs, uint8_t *arena, uint64_t cap, am_chunk_desc *chunks,
                         am_doc_desc *docs, uint64_t *ops_out, int nthreads);
+/* Text editing histories (C1: cross_every 0, two actors concurrent from the same base; C3:
+ * cross_every 10, interleaved): document i = Backend.init() + 1 + nchanges change chunks (change 0
+ * = makeText), per_change ops each (1/5 deletes of live elements, otherwise one-character
+ * inserts), chunks >= 256 B deflated as encodeChange does (columnar.js:738). */
+uint64_t am_workload_text(uint64_t first_doc, uint32_t ndocs, uint32_t nchanges, uint32_t per_change,
+                          uint32_t cross_every, uint8_t *arena, uint64_t cap, am_chunk_desc *chunks,
+                          am_doc_desc *docs, uint64_t *ops_out, int nthreads);
 
 #ifdef __cplusplus
 }
