@@ -58,6 +58,9 @@ _sigs = {
     "am_batch_results": (C.c_int, [P, P]),
     "am_batch_chunk_results": (C.c_int, [P, P, P, P]),
     "am_batch_doc_output": (C.c_int, [P, C.c_uint32, P, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "am_inflate_raw": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t, C.POINTER(u8p),
+                                 C.POINTER(C.c_size_t), P, C.POINTER(Error)]),
+    "am_batch_inflate_info": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_float)]),
     "am_batch_doc_save": (C.c_int, [P, C.c_uint32, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
     "am_batch_doc_heads": (C.c_int, [P, C.c_uint32, P, C.c_uint32, C.POINTER(C.c_uint32)]),
     "am_batch_stage_times": (C.c_int, [P, C.POINTER(C.c_float)]),
@@ -166,3 +169,24 @@ def stage_document(data, device=0):
     b = C.string_at(out, n.value)
     lib.am_free(out)
     return b, bool(v.value)
+
+
+def inflate_raw(buffers, device=0):
+    """pako.inflateRaw over many buffers on the GPU (am_inflate_raw): a list of bytes, or None for a
+    buffer that is not a valid raw DEFLATE stream."""
+    n = len(buffers)
+    if not n:
+        return []
+    arr = (C.c_char_p * n)(*[bytes(b) for b in buffers])
+    lens = (C.c_size_t * n)(*[len(b) for b in buffers])
+    outs = (u8p * n)()
+    olens = (C.c_size_t * n)()
+    ok = (C.c_uint8 * n)()
+    err = Error()
+    if lib.am_inflate_raw(engine(device), arr, lens, n, outs, olens, ok, C.byref(err)):
+        raise_for(err)
+    res = []
+    for i in range(n):
+        res.append(C.string_at(outs[i], olens[i]) if ok[i] else None)
+        lib.am_free(outs[i])
+    return res

@@ -25,14 +25,15 @@ WANT_DIFF = 4   # AM_DOC_WANT_DIFF: also write the patch applyChanges returns
 
 def pack(docs, device=0, flags=0):
     """docs: iterable of (base_bytes | None, [change bytes]) -> (arena, chunks, docdescs).
-    Compressed inputs go through the host DEFLATE stage (am_stage_change / am_stage_document).
+    Compressed change chunks (type 2) are inflated on the GPU when the batch is staged
+    (am_inflate.hip); base documents with DEFLATEd columns go through am_stage_document.
     flags: WANT_PATCH or WANT_DIFF for every document."""
     parts, chunks, descs = [], [], []
     off = 0
     for base, changes in docs:
         d = np.zeros((), DOC_DT)
         d["base_chunk"] = -1
-        changes = [N.stage_change(c) for c in changes]
+        changes = [bytes(c) for c in changes]
         if base:
             base, verified = N.stage_document(base, device)
             d["base_chunk"] = len(chunks)
@@ -165,6 +166,15 @@ class Batch:
         if self.ndocs and N.lib.am_batch_fast_flags(self._b, out.ctypes.data):
             raise N.AutomergeError("automerge_amd: flag copy failed")
         return out.astype(bool)
+
+    def inflate_info(self):
+        """(change chunks inflated on the GPU, inflated arena bytes, ms of the two inflate passes)
+        of the last stage."""
+        n = C.c_uint64()
+        nb = C.c_uint64()
+        ms = C.c_float()
+        N.lib.am_batch_inflate_info(self._b, C.byref(n), C.byref(nb), C.byref(ms))
+        return int(n.value), int(nb.value), float(ms.value)
 
     def workspace_bytes(self):
         return N.lib.am_batch_workspace_bytes(self._b)

@@ -294,6 +294,9 @@ struct am_batch {
   uint32_t nchunks = 0, ndocs = 0;
   uint64_t ws_need = 0;
   bool timed = false;
+  uint32_t inflated = 0;      // change chunks inflated on the GPU by the last stage
+  float inflate_ms = 0.f;     // their two inflate passes (HIP events)
+  uint64_t inflated_bytes = 0;
 
   BatchDev dev() {
     BatchDev b;
@@ -354,6 +357,73 @@ extern "C" am_batch* am_batch_create(am_engine* eng) {
   return b;
 }
 
+// DEFLATE-compressed change chunks (type 2, columnar.js:742/784 -> inflateChange :813) are inflated
+// on the GPU (am_inflate.hip) into a new arena: pass 1 sizes every stream, the host lays the chunks
+// out again in index order (a document's chunks stay adjacent), pass 2 writes the inflated chunks
+// and copies the others. Base document chunks are never inflated here (a type-2 chunk is not a
+// document; k_chunks reports it). Streams that do not inflate keep their bytes and type 2, which
+// k_chunks rejects.
+static bool inflate_stage(am_batch* b, const uint8_t* arena, uint64_t arena_len, const am_chunk_desc* chunks,
+                          uint32_t nchunks, const am_doc_desc* docs, uint32_t ndocs) {
+  std::vector<uint8_t> is_base(nchunks, 0);
+  for (uint32_t d = 0; d < ndocs; d++)
+    if (docs[d].base_chunk >= 0 && (uint64_t)docs[d].base_chunk < nchunks) is_base[docs[d].base_chunk] = 1;
+  std::vector<uint32_t> zidx;
+  for (uint32_t c = 0; c < nchunks; c++) {
+    const am_chunk_desc& k = chunks[c];
+    if (!is_base[c] && k.len > 9 && k.off + k.len <= arena_len && arena[k.off + 8] == 2 &&
+        std::memcmp(arena + k.off, "\x85\x6f\x4a\x83", 4) == 0)
+      zidx.push_back(c);
+  }
+  b->inflated = (uint32_t)zidx.size();
+  b->inflate_ms = 0.f;
+  if (zidx.empty()) return true;
+  hipStream_t s = b->eng->stream;
+  const uint32_t nz = (uint32_t)zidx.size();
+  DevBuf<uint32_t> d_zidx, d_zlen;
+  DevBuf<am_chunk_desc> d_new;
+  DevBuf<uint8_t> d_flag, d_arena;
+  if (!d_zidx.ensure(nz) || !d_zlen.ensure(nz) || !d_new.ensure(nchunks) || !d_flag.ensure(nchunks)) return false;
+  HIPCHECK(hipMemcpyAsync(d_zidx.p, zidx.data(), 4ull * nz, hipMemcpyHostToDevice, s));
+  (void)hipEventRecord(b->eng->ev[0], s);
+  am_launch_inflate_size(b->arena.p, b->chunks.p, d_zidx.p, nz, d_zlen.p, s);
+  (void)hipEventRecord(b->eng->ev[1], s);
+  std::vector<uint32_t> zlen(nz);
+  HIPCHECK(hipMemcpyAsync(zlen.data(), d_zlen.p, 4ull * nz, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  float ms1 = 0.f;
+  // new layout in chunk-index order
+  std::vector<am_chunk_desc> nc(chunks, chunks + nchunks);
+  std::vector<uint8_t> flag(nchunks, 0);
+  for (uint32_t i = 0; i < nz; i++)
+    if (zlen[i] != 0xFFFFFFFFu) {
+      flag[zidx[i]] = 1;
+      uint32_t u = 1;
+      for (uint64_t v = zlen[i]; v >= 0x80; v >>= 7) u++;
+      nc[zidx[i]].len = 9 + u + zlen[i];
+    }
+  uint64_t off = 0;
+  for (uint32_t c = 0; c < nchunks; c++) { nc[c].off = off; off += nc[c].len; }
+  if (!d_arena.ensure(off + 64)) return false;
+  HIPCHECK(hipMemcpyAsync(d_new.p, nc.data(), sizeof(am_chunk_desc) * nchunks, hipMemcpyHostToDevice, s));
+  HIPCHECK(hipMemcpyAsync(d_flag.p, flag.data(), nchunks, hipMemcpyHostToDevice, s));
+  HIPCHECK(hipMemsetAsync(d_arena.p + off, 0, 64, s));
+  (void)hipEventRecord(b->eng->ev[2], s);
+  am_launch_inflate_write(b->arena.p, b->chunks.p, d_new.p, d_zidx.p, nz, d_zlen.p, d_flag.p, nchunks, d_arena.p, s);
+  (void)hipEventRecord(b->eng->ev[3], s);
+  HIPCHECK(hipMemcpyAsync(b->chunks.p, nc.data(), sizeof(am_chunk_desc) * nchunks, hipMemcpyHostToDevice, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  HIPCHECK(hipGetLastError());
+  float ms2 = 0.f;
+  (void)hipEventElapsedTime(&ms1, b->eng->ev[0], b->eng->ev[1]);
+  (void)hipEventElapsedTime(&ms2, b->eng->ev[2], b->eng->ev[3]);
+  b->inflate_ms = ms1 + ms2;
+  b->inflated_bytes = off;
+  std::swap(b->arena.p, d_arena.p);
+  std::swap(b->arena.cap, d_arena.cap);
+  return true;
+}
+
 static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, const am_chunk_desc* chunks, uint32_t nchunks,
                        const am_doc_desc* docs, uint32_t ndocs, const am_known_hash* known, uint32_t nknown) {
   am_engine* e = b->eng;
@@ -372,6 +442,7 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   if (nknown) HIPCHECK(hipMemcpyAsync(b->known.p, known, sizeof(am_known_hash) * nknown, hipMemcpyHostToDevice, s));
   b->nchunks = nchunks;
   b->ndocs = ndocs;
+  if (!inflate_stage(b, arena, arena_len, chunks, nchunks, docs, ndocs)) return false;
   // sizing pass: chunk counts -> per-document workspace bounds -> total
   BatchDev d = b->dev();
   am_launch_chunks(d, s);
@@ -537,6 +608,82 @@ extern "C" int am_batch_fast_flags(am_batch* b, uint8_t* flags) {
 }
 
 extern "C" uint64_t am_batch_workspace_bytes(am_batch* b) { return b->ws_need; }
+
+// pako.inflateRaw over n independent buffers on the GPU (the kernels of the batch stage). outs[i]
+// (malloc'd, am_free) / out_lens[i]; ok[i] = 0 when buffer i is not a valid raw DEFLATE stream.
+extern "C" int am_inflate_raw(am_engine* eng, const uint8_t* const* bufs, const size_t* lens, size_t n, uint8_t** outs,
+                              size_t* out_lens, uint8_t* ok, am_error* err) {
+  auto fail = [&](const char* m) { to_c(Err{AM_U_CAPACITY, false, m}, err); return 1; };
+  if (!set_device(eng)) return fail("automerge_amd: no device");
+  hipStream_t s = eng->stream;
+  std::vector<uint8_t> arena;
+  std::vector<am_chunk_desc> ch(n);
+  std::vector<uint32_t> zidx(n);
+  for (size_t i = 0; i < n; i++) {
+    if (lens[i] > 0xFFFFFF00u) return fail("automerge_amd: buffer too large");
+    const uint8_t hdr[9] = {0x85, 0x6f, 0x4a, 0x83, 0, 0, 0, 0, 2};
+    ch[i].off = arena.size();
+    arena.insert(arena.end(), hdr, hdr + 9);
+    put_u(arena, lens[i]);
+    arena.insert(arena.end(), bufs[i], bufs[i] + lens[i]);
+    ch[i].len = (uint32_t)(arena.size() - ch[i].off);
+    ch[i].flags = 0;
+    zidx[i] = (uint32_t)i;
+  }
+  if (!n) return 0;
+  DevBuf<uint8_t> d_arena, d_out, d_flag;
+  DevBuf<am_chunk_desc> d_ch, d_new;
+  DevBuf<uint32_t> d_zidx, d_zlen;
+  if (!d_arena.ensure(arena.size() + 64) || !d_ch.ensure(n) || !d_new.ensure(n) || !d_zidx.ensure(n) || !d_zlen.ensure(n) ||
+      !d_flag.ensure(n))
+    return fail("automerge_amd: device allocation failed");
+  std::vector<uint32_t> zlen(n);
+  std::vector<am_chunk_desc> nc(ch);
+  std::vector<uint8_t> flag(n, 1);
+  uint64_t off = 0;
+  bool okc = hipMemcpyAsync(d_arena.p, arena.data(), arena.size(), hipMemcpyHostToDevice, s) == hipSuccess &&
+             hipMemcpyAsync(d_ch.p, ch.data(), sizeof(am_chunk_desc) * n, hipMemcpyHostToDevice, s) == hipSuccess &&
+             hipMemcpyAsync(d_zidx.p, zidx.data(), 4 * n, hipMemcpyHostToDevice, s) == hipSuccess;
+  if (okc) {
+    am_launch_inflate_size(d_arena.p, d_ch.p, d_zidx.p, (uint32_t)n, d_zlen.p, s);
+    okc = hipMemcpyAsync(zlen.data(), d_zlen.p, 4 * n, hipMemcpyDeviceToHost, s) == hipSuccess &&
+          hipStreamSynchronize(s) == hipSuccess;
+  }
+  if (!okc) return fail("automerge_amd: inflate pass 1 failed");
+  for (size_t i = 0; i < n; i++) {
+    uint32_t u = 1;
+    for (uint64_t v = zlen[i] == 0xFFFFFFFFu ? 0 : zlen[i]; v >= 0x80; v >>= 7) u++;
+    nc[i].off = off;
+    nc[i].len = zlen[i] == 0xFFFFFFFFu ? 0 : 9 + u + zlen[i];
+    off += nc[i].len;
+  }
+  if (!d_out.ensure(off + 64)) return fail("automerge_amd: device allocation failed");
+  std::vector<uint8_t> out(off);
+  okc = hipMemcpyAsync(d_new.p, nc.data(), sizeof(am_chunk_desc) * n, hipMemcpyHostToDevice, s) == hipSuccess &&
+        hipMemcpyAsync(d_flag.p, flag.data(), n, hipMemcpyHostToDevice, s) == hipSuccess;
+  if (okc) {
+    am_launch_inflate_write(d_arena.p, d_ch.p, d_new.p, d_zidx.p, (uint32_t)n, d_zlen.p, d_flag.p, (uint32_t)n, d_out.p, s);
+    okc = (off == 0 || hipMemcpyAsync(out.data(), d_out.p, off, hipMemcpyDeviceToHost, s) == hipSuccess) &&
+          hipStreamSynchronize(s) == hipSuccess && hipGetLastError() == hipSuccess;
+  }
+  if (!okc) return fail("automerge_amd: inflate pass 2 failed");
+  for (size_t i = 0; i < n; i++) {
+    ok[i] = zlen[i] != 0xFFFFFFFFu;
+    const size_t m = ok[i] ? zlen[i] : 0;
+    outs[i] = (uint8_t*)std::malloc(m ? m : 1);
+    if (m) std::memcpy(outs[i], out.data() + nc[i].off + nc[i].len - m, m);
+    out_lens[i] = m;
+  }
+  if (err) err->code = 0;
+  return 0;
+}
+
+extern "C" int am_batch_inflate_info(am_batch* b, uint64_t* nchunks, uint64_t* arena_bytes, float* ms) {
+  if (nchunks) *nchunks = b->inflated;
+  if (arena_bytes) *arena_bytes = b->inflated_bytes;
+  if (ms) *ms = b->inflate_ms;
+  return 0;
+}
 // launch shape of the document kernels of the staged batch: [0] k_doc dynamic LDS bytes, [1] the
 // k_doc_fast LDS slice per document (0: no document in its envelope), [2] largest k_doc hot set
 extern "C" int am_batch_kernel_info(am_batch* b, uint64_t* out3) {
@@ -804,14 +951,11 @@ static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* le
                   am_error* err) {
   Err e;
   // decoded changes first, then the existing queue (new.js:1814)
-  std::vector<std::vector<uint8_t>> orig, staged;
+  // compressed changes travel as they are: the batch stage inflates them on the GPU (am_inflate.hip)
+  std::vector<std::vector<uint8_t>> orig;
   for (size_t i = 0; i < n; i++) orig.emplace_back(bufs[i], bufs[i] + lens[i]);
   for (auto& q : d->queue) orig.push_back(q);
-  for (auto& o : orig) {
-    std::vector<uint8_t> s;
-    if (!stage_change(o, s, e)) { to_c(e, err); return 1; }
-    staged.push_back(std::move(s));
-  }
+  const std::vector<std::vector<uint8_t>>& staged = orig;
   std::vector<am_known_hash> known;
   if (d->have_hash_graph) {
     for (size_t i = 0; i < d->hashes.size(); i++) {

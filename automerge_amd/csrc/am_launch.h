@@ -37,6 +37,12 @@ void am_launch_out_hash(const BatchDev& b, hipStream_t s);
 void am_launch_digest(const BatchDev& b, uint64_t first, uint64_t* d_out, hipStream_t s);
 void am_launch_sha256(const uint8_t* arena, const am_chunk_desc* msgs, uint32_t n, uint8_t* out, hipStream_t s);
 size_t am_scan_tmp_elems(uint32_t n);
+// DEFLATE of compressed change chunks (am_inflate.hip): pass 1 sizes, pass 2 writes the new arena
+void am_launch_inflate_size(const uint8_t* arena, const am_chunk_desc* chunks, const uint32_t* zidx, uint32_t nz,
+                            uint32_t* zlen, hipStream_t s);
+void am_launch_inflate_write(const uint8_t* arena, const am_chunk_desc* chunks, const am_chunk_desc* nchunks,
+                             const uint32_t* zidx, uint32_t nz, const uint32_t* zlen, const uint8_t* inflated,
+                             uint32_t n, uint8_t* dst, hipStream_t s);
 
 // engine internals shared with am_sync.hip
 struct am_engine;

@@ -153,6 +153,15 @@ int am_batch_results(am_batch *b, am_doc_result *out);
 int am_batch_chunk_results(am_batch *b, uint8_t *hashes32, int32_t *chg_state, uint32_t *status);
 /* Merged document chunk (uncompressed columns) of one document. */
 int am_batch_doc_output(am_batch *b, uint32_t doc, uint8_t *dst, uint64_t cap, uint64_t *len);
+/* DEFLATE-compressed change chunks (type 2) inflated on the GPU by the last am_batch_stage
+ * (inflateChange, columnar.js:813-823): their number, the inflated arena bytes and the time of the
+ * two inflate passes (ms, HIP events). */
+int am_batch_inflate_info(am_batch *b, uint64_t *nchunks, uint64_t *arena_bytes, float *ms);
+/* pako.inflateRaw (the call inside inflateChange / inflateColumn, columnar.js:816, 1064) over n
+ * independent buffers on the GPU. outs[i] is malloc'd (am_free); ok[i] = 0 when buffer i is not a
+ * valid raw DEFLATE stream. */
+int am_inflate_raw(am_engine *eng, const uint8_t *const *bufs, const size_t *lens, size_t n, uint8_t **outs,
+                   size_t *out_lens, uint8_t *ok, am_error *err);
 /* Backend.save() bytes of one document (backend.js:96-98, new.js:2025-2047): the merged chunk with
  * columns >= 256 bytes DEFLATEd (deflateColumn, columnar.js:1052). *out is malloc'd (am_free). */
 int am_batch_doc_save(am_batch *b, uint32_t doc, uint8_t **out, size_t *len, am_error *err);

@@ -1,0 +1,97 @@
+"""DEFLATE inflate on the GPU (automerge_amd/csrc/am_inflate.hip) against
+zlib's raw inflate (the reference calls pako.inflateRaw, columnar.js:816 and :1064; inflate is
+unambiguous, so any conforming decoder must return the same bytes).
+
+Streams cover every block type: stored (level 0), fixed Huffman (Z_FIXED), dynamic Huffman (levels
+1-9, Z_HUFFMAN_ONLY, Z_RLE), multi-block streams, back-references across the 32 KiB window, empty
+input, plus malformed streams that must be rejected. The change-chunk path (type 2 chunks inflated
+in the batch stage) is covered end to end by tests/test_gpu_text.py and tests/test_gpu_parity.py."""
+import random
+import zlib
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _deflate(data, level=6, strategy=zlib.Z_DEFAULT_STRATEGY, mem=8):
+    c = zlib.compressobj(level, zlib.DEFLATED, -15, mem, strategy)
+    return c.compress(data) + c.flush()
+
+
+def _corpus(rng):
+    out = [b"", b"a", bytes(range(256)), b"abc" * 1000]
+    for n in (10, 100, 255, 256, 1000, 5000, 40000, 150000):
+        text = bytes(rng.choice(b"abcdefghij      ") for _ in range(n))
+        noise = bytes(rng.getrandbits(8) for _ in range(n))
+        mixed = bytes(text[i] if (i // 64) % 3 else noise[i] for i in range(n))
+        out += [text, noise, mixed]
+    return out
+
+
+def test_inflate_matches_zlib():
+    from automerge_amd import _native as N
+    rng = random.Random(1234)
+    data, streams = [], []
+    for d in _corpus(rng):
+        for level, strat in [(6, zlib.Z_DEFAULT_STRATEGY), (0, zlib.Z_DEFAULT_STRATEGY), (1, zlib.Z_DEFAULT_STRATEGY),
+                             (9, zlib.Z_DEFAULT_STRATEGY), (6, zlib.Z_FIXED), (6, zlib.Z_HUFFMAN_ONLY), (6, zlib.Z_RLE)]:
+            data.append(d)
+            streams.append(_deflate(d, level, strat))
+    # a stream of many small blocks (sync flushes between pieces)
+    c = zlib.compressobj(6, zlib.DEFLATED, -15)
+    pieces = [bytes(rng.choice(b"xyz ") for _ in range(rng.randint(0, 300))) for _ in range(50)]
+    s = b""
+    for p in pieces:
+        s += c.compress(p) + c.flush(zlib.Z_SYNC_FLUSH)
+    s += c.flush()
+    data.append(b"".join(pieces))
+    streams.append(s)
+    got = N.inflate_raw(streams)
+    for i, (d, z, g) in enumerate(zip(data, streams, got)):
+        assert zlib.decompress(z, -15) == d
+        assert g == d, (i, len(d), None if g is None else len(g))
+
+
+def test_inflate_rejects_malformed():
+    from automerge_amd import _native as N
+    good = _deflate(b"hello hello hello world" * 20)
+    bad = [
+        b"\x07",                            # block type 3 (reserved)
+        good[: len(good) // 2],             # truncated
+        b"\x01\x05\x00\x00\x00abc",         # stored block with LEN != ~NLEN
+        b"\x01\x05\x00\xfa\xffab",          # stored block longer than the input
+        bytes.fromhex("030200"),            # fixed block: a match at output position 0 (distance too far back)
+    ]
+    got = N.inflate_raw(bad + [good])
+    assert got[:-1] == [None] * len(bad)
+    assert got[-1] == zlib.decompress(good, -15)
+
+
+def test_deflated_change_chunks_inflate_in_the_batch_stage():
+    """Compressed change chunks (columnar.js:738 writes them for changes >= 256 B) go through the
+    batch as they are: the stage inflates them on the GPU, the hashes and merged bytes equal the
+    oracle's (which inflates with zlib)."""
+    import oracle_ffi as O
+    from automerge_amd import workload as W
+    from automerge_amd.batch import Batch
+    arena, chunks, docs, _ = W.text(5, 6, 30, 60, 4)
+    b = Batch()
+    b.stage(arena, chunks, docs)
+    ninf, nbytes, ms = b.inflate_info()
+    nz = sum(1 for c in chunks if arena[int(c["off"]) + 8] == 2)
+    assert nz > 100 and ninf == nz
+    b.run()
+    b.sync()
+    r = b.results()
+    hashes, _, _ = b.chunk_results()
+    k = 0
+    for i in range(len(docs)):
+        _, chg = W.doc_chunks(arena, chunks, docs, i)
+        ref = O.Doc.init()
+        ref.apply(chg)
+        assert int(r[i]["status"]) == 0
+        assert b.doc_save(i) == ref.save()
+        for c in chg:
+            assert hashes[k].tobytes().hex() == O.change_meta(c)["hash"]
+            k += 1
