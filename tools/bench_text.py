@@ -1,0 +1,115 @@
+"""Text-history throughput on one MI355X (BASELINE configs[2] = SURVEY.md §8(d) C3: 1k text
+documents with 100k-op interleaved editing histories; --cross 0 --docs 1 --changes 100 gives C1).
+
+Each document is Backend.load(base) + Backend.applyChanges(rest): base = save() of the first half
+of the history (made by the engine in an untimed preparation launch), rest = the second half as
+compressed (type 2) change chunks, exactly as encodeChange writes them. Timed per step, inputs
+resident in HBM: the GPU pipeline (SHA-256 + parse, causal queue, decode, merge, re-encode,
+checksums) over all documents. The GPU DEFLATE inflate of the compressed changes runs in the batch
+stage and is reported separately (inflate_ms, inflate_GBps of inflated bytes). Documents 0 and 1
+are checked against the reference backend's own digests (tests/golden/text.json, c3full) when the
+configuration matches; the rest against the engine's own second run (determinism).
+
+  python tools/bench_text.py [--docs 1000] [--changes 1000] [--per-change 100] [--cross 10] [--steps 3]
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--docs", type=int, default=1000)
+    ap.add_argument("--changes", type=int, default=1000)
+    ap.add_argument("--per-change", type=int, default=100)
+    ap.add_argument("--cross", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--cpu-baseline", action="store_true", help="time the oracle on document 0 (load + apply)")
+    args = ap.parse_args()
+    from automerge_amd import workload as W
+    from automerge_amd.batch import Batch, pack
+
+    t0 = time.perf_counter()
+    arena, chunks, docs, _ = W.text(0, args.docs, args.changes, args.per_change, args.cross)
+    hist = [W.doc_chunks(arena, chunks, docs, i)[1] for i in range(args.docs)]
+    half = (1 + args.changes) // 2
+    gen_s = time.perf_counter() - t0
+    print("generated %d docs in %.1f s" % (args.docs, gen_s), flush=True)
+
+    # preparation (untimed): base documents = save() of the first half of every history
+    t0 = time.perf_counter()
+    prep = Batch()
+    prep.stage(*pack([(None, h[:half]) for h in hist]))
+    prep.run()
+    prep.sync()
+    r = prep.results()
+    assert (r["status"] == 0).all(), "preparation failed"
+    bases = [prep.doc_save(i) for i in range(args.docs)]
+    del prep
+    print("bases ready in %.1f s (%.1f MB)" % (time.perf_counter() - t0, sum(map(len, bases)) / 1e6), flush=True)
+
+    rest = [h[half:] for h in hist]
+    ops_applied = sum(args.per_change for h in rest for _ in h)
+    arena2, chunks2, docs2 = pack(list(zip(bases, rest)))
+    b = Batch()
+    t0 = time.perf_counter()
+    b.stage(arena2, chunks2, docs2)
+    stage_s = time.perf_counter() - t0
+    ninf, inf_bytes, inf_ms = b.inflate_info()
+    print("staged in %.1f s: %d chunks inflated on the GPU in %.2f ms" % (stage_s, ninf, inf_ms), flush=True)
+    for _ in range(args.warmup):
+        b.run()
+    b.sync()
+    stage_ms = [0.0] * 4
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        b.run()
+        b.sync()
+        for i, x in enumerate(b.stage_times()):
+            stage_ms[i] += x
+    elapsed = (time.perf_counter() - t0) / args.steps
+    r = b.results()
+    nerr = int((r["status"] != 0).sum())
+    checked = []
+    golden = json.load(open(os.path.join(ROOT, "tests", "golden", "text.json")))
+    ref = {c["name"]: c for c in golden}.get("c3full")
+    if ref and (args.changes, args.per_change, args.cross) == (ref["nchanges"], ref["per_change"], ref["cross_every"]):
+        for i, e in enumerate(ref["docs"][:args.docs]):
+            assert hashlib.sha256(bases[i]).hexdigest() == e["split"]["base"], "base %d differs from the reference" % i
+            assert hashlib.sha256(b.doc_save(i)).hexdigest() == e["split"]["save"], "doc %d differs from the reference" % i
+            checked.append(i)
+    cpu = None
+    if args.cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_ffi as O
+        t0 = time.perf_counter()
+        d = O.Doc.load(bases[0])
+        d.apply(rest[0])
+        d.save()
+        dt = time.perf_counter() - t0
+        cpu = {"value": len(rest[0]) * args.per_change / dt, "unit": "ops/s", "cores": 1, "kind": "port",
+               "sample": "document 0 (load + applyChanges + save) by oracle/liboracle.so, 1 thread, %.1f s" % dt}
+    k = args.steps
+    line = {
+        "workload": "C3 text histories: load(save(first half)) + applyChanges(second half, deflated chunks)",
+        "docs": args.docs, "ops_per_doc": 1 + args.changes * args.per_change, "ops_applied": ops_applied,
+        "value": ops_applied / elapsed, "unit": "ops/s", "ms_per_step": elapsed * 1e3, "steps": k,
+        "stage_ms": {"k_chunks": stage_ms[0] / k, "k_bounds+scan": stage_ms[1] / k, "k_doc": stage_ms[2] / k,
+                     "k_out_hash": stage_ms[3] / k},
+        "inflate": {"chunks": ninf, "ms": inf_ms, "inflated_arena_bytes": inf_bytes,
+                    "GBps_out": inf_bytes / (inf_ms * 1e-3) / 1e9 if inf_ms else None},
+        "errors": nerr, "verified_vs_reference": checked, "workspace_bytes": int(b.workspace_bytes()),
+        "input_bytes": int(arena2.nbytes), "gen_s": gen_s, "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
