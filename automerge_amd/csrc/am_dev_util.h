@@ -508,15 +508,30 @@ __device__ static uint32_t block_excl_scan(uint32_t* a, uint32_t n, uint32_t* s_
 // Bitonic sort of a[0..P) (P power of two, padded with elements that compare as +inf).
 template <typename T, typename Less>
 __device__ static void block_bitonic_sort(T* a, uint32_t P, Less less) {
+  // Each lane keeps kU compare-exchange pairs in flight (loads first, then the swaps): the pairs
+  // of one step are disjoint, and for documents whose keys live in global memory the step is
+  // latency-bound, so memory-level parallelism is what sets its speed.
+  constexpr uint32_t kU = 4;
+  const uint32_t B = blockDim.x;
   for (uint32_t k = 2; k <= P; k <<= 1) {
     for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = threadIdx.x; i < P; i += blockDim.x) {
-        uint32_t l = i ^ j;
-        if (l > i) {
-          T x = a[i], y = a[l];
-          bool asc = (i & k) == 0;
-          bool sw = asc ? less(y, x) : less(x, y);
-          if (sw) { a[i] = y; a[l] = x; }
+      for (uint32_t i0 = threadIdx.x; i0 < P; i0 += kU * B) {
+        T x[kU], y[kU];
+        bool act[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+          const uint32_t i = i0 + u * B, l = i ^ j;
+          act[u] = i < P && l > i;
+          if (act[u]) { x[u] = a[i]; y[u] = a[l]; }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+          const uint32_t i = i0 + u * B, l = i ^ j;
+          if (act[u]) {
+            const bool asc = (i & k) == 0;
+            const bool sw = asc ? less(y[u], x[u]) : less(x[u], y[u]);
+            if (sw) { a[i] = y[u]; a[l] = x[u]; }
+          }
         }
       }
       __syncthreads();

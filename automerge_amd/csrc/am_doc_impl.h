@@ -1210,10 +1210,26 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
     }
     __syncthreads();
     for (uint32_t span = 1; span < 2 * R; span <<= 1) {
-      for (uint32_t x = t; x < 2 * R; x += T) {
-        int32_t nx = nxtA[x];
-        if (nx != END) { wB[x] = wA[x] + wA[nx]; nxtB[x] = nxtA[nx]; }
-        else { wB[x] = wA[x]; nxtB[x] = END; }
+      // 8 independent jumps in flight per lane (the gathers are latency-bound in global mode)
+      constexpr uint32_t kJ = 8;
+      for (uint32_t x0 = t; x0 < 2 * R; x0 += kJ * T) {
+        int32_t nx[kJ], w0[kJ], w1[kJ], n1[kJ];
+#pragma unroll
+        for (uint32_t u = 0; u < kJ; u++) {
+          const uint32_t x = x0 + u * T;
+          nx[u] = x < 2 * R ? nxtA[x] : END;
+          w0[u] = x < 2 * R ? wA[x] : 0;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kJ; u++) {
+          w1[u] = nx[u] != END ? wA[nx[u]] : 0;
+          n1[u] = nx[u] != END ? nxtA[nx[u]] : END;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kJ; u++) {
+          const uint32_t x = x0 + u * T;
+          if (x < 2 * R) { wB[x] = w0[u] + w1[u]; nxtB[x] = n1[u]; }
+        }
       }
       __syncthreads();
       int32_t* tp = nxtA; nxtA = nxtB; nxtB = tp;

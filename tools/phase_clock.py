@@ -23,13 +23,17 @@ FAST = ["F0 status+stage input", "F1 headers+hashes+refs", "F2 canon+actor table
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--docs", type=int, default=65536)
+    ap.add_argument("--text", type=int, default=0, help="C3 text histories of this many changes instead of C4")
     args = ap.parse_args()
     from automerge_amd import _native, workload
     from automerge_amd.batch import Batch
     lib = _native.lib
     f = lib.amx_phase_cycles
     f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-    arena, chunks, docs, ops = workload.c4(0, args.docs)
+    if args.text:
+        arena, chunks, docs, ops = workload.text(0, args.docs, args.text, 100, 10)
+    else:
+        arena, chunks, docs, ops = workload.c4(0, args.docs)
     b = Batch(device=0)
     b.stage(arena, chunks, docs)
     b.run(); b.sync()
