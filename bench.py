@@ -48,7 +48,7 @@ def measured_traffic(kernel):
     return rec["traffic_bytes"]
 
 
-def cpu_baseline(arena, chunks, docs, seconds=12.0):
+def cpu_baseline(arena, chunks, docs, seconds=12.0, ops_per_doc=60, name="C4"):
     """The oracle (CPU restatement of the reference algorithm, oracle/) timed on one host core over
     a bounded sample of the same documents: ops merged per second (load + applyChanges)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -59,14 +59,14 @@ def cpu_baseline(arena, chunks, docs, seconds=12.0):
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds and n < len(docs):
         base, changes = workload.doc_chunks(arena, chunks, docs, n)
-        d = O.Doc.load(base)
+        d = O.Doc.load(base) if base else O.Doc.init()
         d.apply(changes)
         d.save()
-        ops += 60
+        ops += ops_per_doc
         n += 1
     dt = time.perf_counter() - t0
     return {"value": ops / dt, "unit": "ops/s", "cores": 1, "kind": "port",
-            "sample": "%d C4 documents (load + applyChanges + save) by oracle/liboracle.so, 1 thread, %.1f s" % (n, dt)}
+            "sample": "%d %s documents (load + applyChanges + save) by oracle/liboracle.so, 1 thread, %.1f s" % (n, name, dt)}
 
 
 def main():
@@ -77,6 +77,8 @@ def main():
     ap.add_argument("--docs", type=int, default=131072, help="documents per GPU (8 GPUs x 131072 = the 1M-doc C4 job)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", type=int, default=32, help="documents verified against the oracle (rank 0)")
+    ap.add_argument("--workload", choices=["c4", "c2"], default="c4",
+                    help="c4 (default, the metric's config) or c2 (configs[1]: 10k-doc-class map/counter docs)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -94,7 +96,7 @@ def main():
 
     first, D = shard.shard_range(rank, world, args.docs)
     t_gen = time.perf_counter()
-    arena, chunks, docs, ops_per_rank = workload.c4(first, D)
+    arena, chunks, docs, ops_per_rank = getattr(workload, args.workload)(first, D)
     t_gen = time.perf_counter() - t_gen
     b = Batch(device=local)
     b.stage(arena, chunks, docs)  # H2D once: inputs resident in HBM before timing
@@ -152,17 +154,21 @@ def main():
         import oracle_ffi as O
         for i in range(min(args.check, D)):
             base, changes = workload.doc_chunks(arena, chunks, docs, i)
-            ref = O.Doc.load(base)
+            ref = O.Doc.load(base) if base else O.Doc.init()
             ref.apply(changes)
             assert b.doc_output(i, res[i]) == ref.save(), "document %d differs from the oracle" % i
             checked += 1
-    cpu = None if args.no_cpu_baseline else cpu_baseline(arena, chunks, docs)
+    per_doc = ops_per_rank // max(D, 1)
+    cpu = None if args.no_cpu_baseline else cpu_baseline(arena, chunks, docs, ops_per_doc=per_doc,
+                                                         name=args.workload.upper())
+    wl = {"c4": "C4: load base doc + applyChanges of 12 concurrent changes (4 actors x 3), 62 ops/doc",
+          "c2": "C2: applyChanges of 3 changes (10 map/counter/string sets + 2 concurrent inc/overwrite), 14 ops/doc"}
     line = {
         "metric": METRIC, "value": value, "unit": "ops/s", "n_gpus": world, "steps": k, "warmup": args.warmup,
         "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u8", "data": "synthetic (seeded C4 generator, SURVEY.md 8(d); bytes pinned to the reference encoder)",
-        "config": {"workload": "C4: load base doc + applyChanges of 12 concurrent changes (4 actors x 3), 62 ops/doc",
-                   "docs_per_gpu": D, "total_docs": tot[0], "ops_per_doc_merged": 60,
+        "dtype": "u8", "data": "synthetic (seeded %s generator, SURVEY.md 8(d); bytes pinned to the reference encoder)" % args.workload.upper(),
+        "config": {"workload": wl[args.workload],
+                   "docs_per_gpu": D, "total_docs": tot[0], "ops_per_doc_merged": per_doc,
                    "parallelism": "doc-sharded dp%d" % world},
         "roofline": {"kernel": dom, "bound": "hbm", "limiter": "latency (per-document dependent phases)", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": measured_traffic(dom),
