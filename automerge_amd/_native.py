@@ -58,6 +58,9 @@ _sigs = {
     "am_batch_results": (C.c_int, [P, P]),
     "am_batch_chunk_results": (C.c_int, [P, P, P, P]),
     "am_batch_doc_output": (C.c_int, [P, C.c_uint32, P, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "am_document_changes": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.POINTER(C.c_uint64)),
+                                      C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
+    "am_doc_compute_hash_graph": (C.c_int, [P, C.POINTER(Error)]),
     "am_inflate_raw": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t, C.POINTER(u8p),
                                  C.POINTER(C.c_size_t), P, C.POINTER(Error)]),
     "am_batch_inflate_info": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_float)]),
@@ -189,4 +192,24 @@ def inflate_raw(buffers, device=0):
     for i in range(n):
         res.append(C.string_at(outs[i], olens[i]) if ok[i] else None)
         lib.am_free(outs[i])
+    return res
+
+
+def document_changes(doc):
+    """decodeChanges([doc]) re-encoded (computeHashGraph, new.js:1879-1904): [(change bytes, hash hex)]
+    of a saved document in its change order (am_document_changes, host stage)."""
+    out, hs = u8p(), u8p()
+    offs = C.POINTER(C.c_uint64)()
+    n = C.c_size_t()
+    err = Error()
+    if lib.am_document_changes(bytes(doc), len(doc), C.byref(out), C.byref(offs), C.byref(hs), C.byref(n),
+                               C.byref(err)):
+        raise_for(err)
+    res = []
+    for i in range(n.value):
+        a, b = offs[i], offs[i + 1]
+        res.append((C.string_at(C.addressof(out.contents) + a, b - a) if b > a else b"",
+                    C.string_at(C.addressof(hs.contents) + 32 * i, 32).hex()))
+    for p in (out, offs, hs):
+        lib.am_free(p)
     return res

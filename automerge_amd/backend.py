@@ -147,9 +147,18 @@ def maxOp(backend):
     return N.lib.am_doc_max_op(_backend_state(backend).ptr)
 
 
+def _hash_graph(s):
+    # computeHashGraph (new.js:1879-1904) for a loaded document, once
+    err = N.Error()
+    if N.lib.am_doc_compute_hash_graph(s.ptr, C.byref(err)):
+        N.raise_for(err)
+
+
 def getAllChanges(backend):
-    """Backend.getAllChanges() for documents built by applyChanges (full hash graph)."""
+    """Backend.getAllChanges() (backend/backend.js:142-144 -> getChanges(backend, [])): the whole
+    history; a loaded document first reconstructs it from save() (computeHashGraph)."""
     s = _backend_state(backend)
+    _hash_graph(s)
     out = []
     i = 0
     while True:
@@ -165,6 +174,7 @@ def getAllChanges(backend):
 def getChangeByHash(backend, hash_hex):
     """Backend.getChangeByHash() (backend/backend.js:166-168)."""
     s = _backend_state(backend)
+    _hash_graph(s)
     i = 0
     h = (C.c_uint8 * 32)()
     while True:

@@ -1106,7 +1106,31 @@ extern "C" size_t am_doc_get_heads(const am_doc* d, uint8_t* out32, size_t cap) 
 extern "C" size_t am_doc_pending(const am_doc* d) { return d->queue.size(); }
 extern "C" int64_t am_doc_max_op(const am_doc* d) { return d->max_op; }
 extern "C" size_t am_doc_num_changes(const am_doc* d) { return d->nchanges; }
+// computeHashGraph (new.js:1879-1904): the history decoded from save() (am_history.cpp)
+extern "C" int am_doc_compute_hash_graph(am_doc* d, am_error* err) {
+  if (err) err->code = 0;
+  if (d->have_hash_graph) return 0;
+  uint8_t *out = nullptr, *hs = nullptr;
+  uint64_t* offs = nullptr;
+  size_t n = 0;
+  if (am_document_changes(d->state.data(), d->state.size(), &out, &offs, &hs, &n, err)) return 1;
+  d->changes.clear();
+  d->hashes.clear();
+  for (size_t i = 0; i < n; i++) {
+    d->changes.emplace_back(out + offs[i], out + offs[i + 1]);
+    std::array<uint8_t, 32> h;
+    std::memcpy(h.data(), hs + 32 * i, 32);
+    d->hashes.push_back(h);
+  }
+  std::free(out);
+  std::free(offs);
+  std::free(hs);
+  d->have_hash_graph = true;
+  return 0;
+}
+
 extern "C" int am_doc_change(const am_doc* d, size_t i, const uint8_t** data, size_t* len, uint8_t* hash32) {
+  if (!d->have_hash_graph && am_doc_compute_hash_graph(const_cast<am_doc*>(d), nullptr)) return 2;
   if (i >= d->changes.size()) return 1;
   *data = d->changes[i].data();
   *len = d->changes[i].size();

@@ -240,7 +240,17 @@ static napi_value js_doc_changes(napi_env env, napi_callback_info info) {
   NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   DocBox* b = get_box(env, argv[0]);
   if (!b) return NULL;
-  const size_t n = am_doc_num_changes(b->doc);
+  am_error e;
+  if (am_doc_compute_hash_graph(b->doc, &e)) {  /* computeHashGraph of a loaded document (new.js:1879) */
+    napi_throw_range_error(env, NULL, e.message);
+    return NULL;
+  }
+  size_t n = 0;
+  {
+    const uint8_t* d0;
+    size_t l0;
+    while (am_doc_change(b->doc, n, &d0, &l0, NULL) == 0) n++;
+  }
   napi_value arr;
   NAPI_OK(napi_create_array_with_length(env, n, &arr));
   for (size_t i = 0; i < n; i++) {

@@ -13,8 +13,9 @@
  * traversals over the applied change buffers, as in new.js:1913-2020.
  * getPatch runs documentPatch on the GPU, applyChanges replays the patch of the call on the GPU
  * (k_doc phase P8, am_diff.h); both logs are materialized here.
- * Not on the GPU path yet: applyLocalChange (8(f) row 3) and the change history of a loaded
- * document (8(f) row 2); those throw.
+ * The change history of a loaded document is reconstructed from save() on first use
+ * (computeHashGraph, new.js:1879-1904; am_document_changes, 8(f) row 2).
+ * Not on the GPU path yet: applyLocalChange (8(f) row 3); it throws.
  */
 const path = require('path')
 const zlib = require('zlib')

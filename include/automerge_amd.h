@@ -67,6 +67,7 @@ enum am_status {
   AM_E_LAST_REFERENCE_ERROR,
   AM_E_FLOAT_LEN = 31,      // Invalid length for floating point number: %a0 (getPatch)
   AM_E_UNKNOWN_COUNTER = 32,// increment operation %a0@%s for unknown counter (getPatch)
+  AM_E_HISTORY = 33,        // RangeError of decodeDocument / groupChangeOps / decodeDocumentChanges (message as given)
   AM_U_HASH_GRAPH = 100,    // needs the deferred hash graph of a loaded document (new.js:1826-1832)
   AM_U_UNKNOWN_COLUMN,      // column id outside DOC_OPS_COLUMNS / CHANGE_COLUMNS (new.js:1387-1425)
   AM_U_NONCAUSAL,           // opId counters violate Lamport order (insert after a later element, ...)
@@ -157,6 +158,15 @@ int am_batch_doc_output(am_batch *b, uint32_t doc, uint8_t *dst, uint64_t cap, u
  * (inflateChange, columnar.js:813-823): their number, the inflated arena bytes and the time of the
  * two inflate passes (ms, HIP events). */
 int am_batch_inflate_info(am_batch *b, uint64_t *nchunks, uint64_t *arena_bytes, float *ms);
+/* computeHashGraph (new.js:1879-1904) / decodeDocument (columnar.js:1040-1046, groupChangeOps :876-943,
+ * decodeDocumentChanges :945-981): the change history of a document chunk, every change re-encoded
+ * by encodeChange (deflated when >= 256 B) in the document's change order. *out = the changes back
+ * to back, (*offs)[0..n] their offsets, *hashes32 their hashes (all malloc'd, am_free). Host stage. */
+int am_document_changes(const uint8_t *doc, size_t len, uint8_t **out, uint64_t **offs, uint8_t **hashes32,
+                        size_t *nchanges, am_error *err);
+/* Backend state of a loaded document: fills in its hash graph (new.js:1879-1904) so that
+ * getAllChanges / getChanges / getChangeByHash see the whole history; no-op when it is known. */
+int am_doc_compute_hash_graph(am_doc *d, am_error *err);
 /* pako.inflateRaw (the call inside inflateChange / inflateColumn, columnar.js:816, 1064) over n
  * independent buffers on the GPU. outs[i] is malloc'd (am_free); ok[i] = 0 when buffer i is not a
  * valid raw DEFLATE stream. */
