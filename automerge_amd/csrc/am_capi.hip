@@ -947,6 +947,8 @@ static bool patch_log_error(const std::vector<uint8_t>& log, Err& e) {
   return true;
 }
 
+extern "C" int am_doc_compute_hash_graph(am_doc* d, am_error* err);
+
 static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* lens, size_t n, std::vector<uint8_t>* patch,
                   am_error* err) {
   Err e;
@@ -957,20 +959,30 @@ static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* le
   for (auto& q : d->queue) orig.push_back(q);
   const std::vector<std::vector<uint8_t>>& staged = orig;
   std::vector<am_known_hash> known;
-  if (d->have_hash_graph) {
+  auto fill_known = [&]() {
+    known.clear();
+    if (!d->have_hash_graph) return;
     for (size_t i = 0; i < d->hashes.size(); i++) {
       am_known_hash k;
       std::memcpy(k.hash, d->hashes[i].data(), 32);
       k.index = (int64_t)i;
       known.push_back(k);
     }
-  }
+  };
+  fill_known();
   OneResult res;
   std::vector<uint8_t> arena;
   if (!run_one(d->eng, d->state.empty() ? nullptr : &d->state, false, staged, known, d->have_hash_graph, res, arena, e,
                patch ? 2 : 0)) {
-    to_c(e, err);
-    return 1;
+    // a loaded document without its hash graph: compute it and run again (new.js:1826-1832)
+    if (e.code != AM_U_HASH_GRAPH || d->have_hash_graph) { to_c(e, err); return 1; }
+    if (am_doc_compute_hash_graph(d, err)) return 1;
+    fill_known();
+    e = Err{};
+    if (!run_one(d->eng, &d->state, false, staged, known, true, res, arena, e, patch ? 2 : 0)) {
+      to_c(e, err);
+      return 1;
+    }
   }
   // the patch is part of the call: an error in it throws before the document changes (new.js:1838)
   if (patch) {

@@ -47,3 +47,28 @@ def test_backend_get_all_changes_after_load():
             from automerge_amd import _native as N
             h = N.document_changes(bytes.fromhex(c["doc"]))[-1][1]
             assert B.getChangeByHash(st, h).hex() == got[-1]
+
+
+@pytest.mark.gpu
+def test_apply_change_depending_on_history_of_loaded_document():
+    """A change whose dependency is a non-head change of a loaded document: the loaded state only
+    knows its heads, so applyChanges computes the hash graph and retries (new.js:1826-1832)."""
+    import oracle_ffi as O
+    from automerge_amd import backend as B
+    from automerge_amd import workload as W
+    arena, chunks, docs, _ = W.text(3, 1, 6, 5, 0)  # two actors that never meet: B's deps = [change 0]
+    _, chg = W.doc_chunks(arena, chunks, docs, 0)
+    ref = O.Doc.init()
+    ref.apply(chg[:2])                                # change 0 (A) + change 1 (A): heads = {change 1}
+    base = ref.save()
+    st = B.load(base)
+    st, _ = B.applyChanges(st, [chg[2]])              # change 2 (B) depends on change 0 only
+    # the oracle does not restate computeHashGraph; the reference's load(base) + applyChanges([c2])
+    # saves the same bytes as init + apply([c0, c1]) + apply([c2]) (checked under Node when this
+    # test was written)
+    want = O.Doc.init()
+    want.apply(chg[:2])
+    want.apply([chg[2]])
+    assert B.save(st) == want.save()
+    assert B.getHeads(st) == want.heads()
+    assert len(B.getAllChanges(st)) == 3
