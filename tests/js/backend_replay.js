@@ -69,4 +69,15 @@ if (sc) {
   graph = {changes: got.length, applied_equal_given: JSON.stringify(got.slice().sort()) === JSON.stringify(all.slice().sort()),
            missing: B.getMissingDeps(st), since_heads: B.getChanges(st, B.getHeads(st)).length}
 }
-console.log(JSON.stringify({scenarios: docs.length, steps, patches, applied, bad: bad.slice(0, 20), nbad: bad.length, graph}))
+// change history of loaded documents (computeHashGraph, new.js:1879-1904) against the reference's
+// getAllChanges(load(saved)) (tests/golden/history.json)
+const hist = JSON.parse(fs.readFileSync(path.join(__dirname, '..', 'golden', 'history.json')))
+let histDocs = 0
+for (let i = 0; i < hist.length; i += 3) {
+  const h = hist[i]
+  let got
+  try { got = B.getAllChanges(B.load(hex(h.doc))).map(toHex) } catch (e) { got = {error: e.message} }
+  if (JSON.stringify(got) !== JSON.stringify(h.changes)) bad.push(['history', i])
+  histDocs++
+}
+console.log(JSON.stringify({scenarios: docs.length, steps, patches, applied, histDocs, bad: bad.slice(0, 20), nbad: bad.length, graph}))

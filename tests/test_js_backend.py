@@ -38,6 +38,7 @@ def test_js_backend_replays_golden_scenarios():
     res = json.loads(out.stdout.strip().splitlines()[-1])
     assert res["scenarios"] > 300
     assert res["applied"] > 300  # applyChanges patches compared with the reference's
+    assert res["histDocs"] > 100  # getAllChanges(load(saved)) compared with the reference's
     assert res["nbad"] == 0, res["bad"]
     g = res["graph"]
     assert g["applied_equal_given"] and g["missing"] == [] and g["since_heads"] == 0
