@@ -852,6 +852,11 @@ bool gpu_sha256(am_engine* e, const std::vector<const std::vector<uint8_t>*>& ms
 // Host stage of Backend.load for documents with DEFLATE-compressed columns: the checksum of the
 // original chunk is verified on the GPU, then the columns are inflated (inflateColumn,
 // columnar.js:1062) into an uncompressed chunk marked as verified.
+}  // namespace
+extern "C" int am_inflate_raw(am_engine* eng, const uint8_t* const* bufs, const size_t* lens, size_t n, uint8_t** outs,
+                              size_t* out_lens, uint8_t* ok, am_error* err);
+namespace {
+
 bool stage_doc(am_engine* e, const std::vector<uint8_t>& in, std::vector<uint8_t>& out, bool& verified, Err& err) {
   verified = false;
   Container c;
@@ -866,8 +871,6 @@ bool stage_doc(am_engine* e, const std::vector<uint8_t>& in, std::vector<uint8_t
   for (auto* cols : {&parts.ccols, &parts.ocols})
     for (auto& col : *cols) any |= (col.id & COL_DEFLATE) != 0;
   if (!any) { out = in; return true; }
-  std::vector<std::array<uint8_t, 32>> h;
-  if (!gpu_sha256(e, {&in}, 8, h)) { err = {AM_U_CAPACITY, false, "automerge_amd: GPU hash failed"}; return false; }
   std::vector<uint8_t> whole(in.begin() + 8, in.begin() + c.end);
   std::vector<std::array<uint8_t, 32>> hh;
   if (!gpu_sha256(e, {&whole}, 0, hh)) { err = {AM_U_CAPACITY, false, "automerge_amd: GPU hash failed"}; return false; }
@@ -875,14 +878,39 @@ bool stage_doc(am_engine* e, const std::vector<uint8_t>& in, std::vector<uint8_t
     err = {AM_E_CHECKSUM, false, message_for(AM_E_CHECKSUM, 0, 0, "")};
     return false;
   }
+  // the DEFLATEd columns (inflateColumn, columnar.js:1062-1068) inflate on the GPU in one batch
+  std::vector<std::vector<uint8_t>*> zcol;
+  std::vector<uint64_t*> zid;
+  std::vector<const uint8_t*> zb;
+  std::vector<size_t> zl;
   for (auto* cols : {&parts.ccols, &parts.ocols})
     for (auto& col : *cols)
       if (col.id & COL_DEFLATE) {
-        std::vector<uint8_t> dec;
-        if (!zinflate(col.data.data(), col.data.size(), dec)) { err = {AM_E_SUBARRAY, false, "invalid deflate data"}; return false; }
-        col.data = std::move(dec);
-        col.id ^= COL_DEFLATE;
+        zcol.push_back(&col.data);
+        zid.push_back(&col.id);
+        zb.push_back(col.data.data());
+        zl.push_back(col.data.size());
       }
+  const size_t nz = zb.size();
+  std::vector<uint8_t*> zo(nz, nullptr);
+  std::vector<size_t> zn(nz, 0);
+  std::vector<uint8_t> zok(nz, 0);
+  am_error ae;
+  if (am_inflate_raw(e, zb.data(), zl.data(), nz, zo.data(), zn.data(), zok.data(), &ae)) {
+    err = {AM_U_CAPACITY, false, ae.message};
+    return false;
+  }
+  bool all_ok = true;
+  for (size_t i = 0; i < nz; i++) {
+    if (zok[i]) {
+      zcol[i]->assign(zo[i], zo[i] + zn[i]);
+      *zid[i] ^= COL_DEFLATE;
+    } else {
+      all_ok = false;
+    }
+    std::free(zo[i]);
+  }
+  if (!all_ok) { err = {AM_E_SUBARRAY, false, "invalid deflate data"}; return false; }
   out = make_chunk(in.data() + 4, 0, join_doc(parts));
   verified = true;
   return true;
