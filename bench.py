@@ -171,7 +171,7 @@ def main():
                    "docs_per_gpu": D, "total_docs": tot[0], "ops_per_doc_merged": per_doc,
                    "parallelism": "doc-sharded dp%d" % world},
         "roofline": {"kernel": dom, "bound": "hbm", "limiter": "VALU issue of k_doc_fast (~16.6k VALU per document-wave, DESIGN.md 4); not HBM", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": measured_traffic(dom),
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": measured_traffic(dom) if (args.workload, D) == ("c4", 131072) else None,
                      "alg_bytes_per_launch": alg[dom], "avg_ms": times[dom]},
         "stage_ms": {"k_chunks(sha256+parse)": t_chunks, "k_bounds+scan": t_bounds, "k_doc(plan+decode+merge+encode)": t_doc,
                      "k_out_hash": t_hash},
