@@ -196,3 +196,112 @@ def changeHashes(changes, device=0):
         N.raise_for(err)
     raw = bytes(out)
     return [raw[32 * i:32 * i + 32].hex() for i in range(n)]
+
+
+# ---- hash-graph queries (new.js:1913-2020), host traversals over the change history ----
+def _uleb(b, o):
+    v = sh = 0
+    while True:
+        c = b[o]
+        o += 1
+        v |= (c & 0x7F) << sh
+        sh += 7
+        if not c & 0x80:
+            return v, o
+
+
+def _change_deps(data):
+    """deps (hex) of a binary change (decodeChangeMeta, columnar.js:783-793)."""
+    b = N.stage_change(data)
+    _, o = _uleb(b, 9)
+    n, o = _uleb(b, o)
+    return [b[o + 32 * i:o + 32 * i + 32].hex() for i in range(n)]
+
+
+def _graph(s):
+    _hash_graph(s)
+    changes = []
+    i = 0
+    h = (C.c_uint8 * 32)()
+    while True:
+        p = N.u8p()
+        n = C.c_size_t()
+        if N.lib.am_doc_change(s.ptr, i, C.byref(p), C.byref(n), h):
+            break
+        changes.append((bytes(h).hex(), C.string_at(p, n.value)))
+        i += 1
+    index = {hh: k for k, (hh, _) in enumerate(changes)}
+    deps_of = {hh: _change_deps(b) for hh, b in changes}
+    dependents = {hh: [] for hh, _ in changes}
+    for hh, _ in changes:
+        for d in deps_of[hh]:
+            dependents.setdefault(d, []).append(hh)
+    return changes, index, deps_of, dependents
+
+
+def getChanges(backend, haveDeps):
+    """Backend.getChanges() (backend/backend.js:150-156 -> BackendDoc.getChanges, new.js:1913-1966)."""
+    if not isinstance(haveDeps, list):
+        raise TypeError("Pass an array of hashes to Backend.getChanges()")
+    s = _backend_state(backend)
+    changes, index, deps_of, dependents = _graph(s)
+    if not haveDeps:
+        return [b for _, b in changes]
+    stack, seen, to_return = [], set(), []
+    for h in haveDeps:
+        seen.add(h)
+        if h not in dependents:
+            raise N.AutomergeError("hash not found: %s" % h, 0, "RangeError")
+        stack += dependents[h]
+    while stack:
+        h = stack.pop()
+        seen.add(h)
+        to_return.append(h)
+        if not all(d in seen for d in deps_of[h]):
+            break
+        stack += dependents[h]
+    if not stack and all(h in seen for h in backend.heads):
+        return [changes[index[h]][1] for h in to_return]
+    stack, seen = list(haveDeps), set()
+    while stack:
+        h = stack.pop()
+        if h not in seen:
+            if h not in deps_of:
+                raise N.AutomergeError("hash not found: %s" % h, 0, "RangeError")
+            stack += deps_of[h]
+            seen.add(h)
+    return [b for h, b in changes if h not in seen]
+
+
+def getChangesAdded(backend1, backend2):
+    """Backend.getChangesAdded() (new.js:1971-1988): changes in backend2 that backend1 lacks."""
+    _, other, _, _ = _graph(_backend_state(backend1))
+    changes, index, deps_of, _ = _graph(_backend_state(backend2))
+    stack, seen, to_return = list(backend2.heads), set(), []
+    while stack:
+        h = stack.pop()
+        if h not in seen and h not in other:
+            seen.add(h)
+            to_return.append(h)
+            stack += deps_of[h]
+    return [changes[index[h]][1] for h in reversed(to_return)]
+
+
+def getMissingDeps(backend, heads=None):
+    """Backend.getMissingDeps() (new.js:2005-2020)."""
+    s = _backend_state(backend)
+    _, index, _, _ = _graph(s)
+    all_deps, in_queue = set(heads or []), set()
+    queued = []
+    i = 0
+    while True:
+        p = N.u8p()
+        n = C.c_size_t()
+        if N.lib.am_doc_queued(s.ptr, i, C.byref(p), C.byref(n)):
+            break
+        queued.append(C.string_at(p, n.value))
+        i += 1
+    for b, h in zip(queued, changeHashes(queued) if queued else []):
+        in_queue.add(h)
+        all_deps.update(_change_deps(b))
+    return sorted(h for h in all_deps if h not in index and h not in in_queue)

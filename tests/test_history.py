@@ -72,3 +72,27 @@ def test_apply_change_depending_on_history_of_loaded_document():
     assert B.save(st) == want.save()
     assert B.getHeads(st) == want.heads()
     assert len(B.getAllChanges(st)) == 3
+
+
+@pytest.mark.gpu
+def test_backend_hash_graph_queries():
+    """getChanges(haveDeps) / getChangesAdded / getMissingDeps of the Python mirror (new.js:1913-2020)
+    on two concurrent chains, loaded from save() (history reconstructed) and freshly applied."""
+    from automerge_amd import backend as B
+    from automerge_amd import workload as W
+    arena, chunks, docs, _ = W.text(9, 1, 8, 4, 0)  # change 0, then A and B alternate, never meeting
+    _, chg = W.doc_chunks(arena, chunks, docs, 0)
+    hashes = B.changeHashes(chg)
+    st, _ = B.applyChanges(B.init(), chg)
+    loaded = B.load(B.save(st))
+    for s in (st, loaded):
+        assert B.getChanges(s, []) == B.getAllChanges(s)
+        assert B.getChanges(s, B.getHeads(s)) == []
+        assert B.getMissingDeps(s) == []
+        # A's changes are 1, 3, 5, 7: everything except change 0 and A's chain is concurrent to A's head
+        got = B.getChanges(s, [hashes[7]])
+        assert sorted(B.changeHashes(got)) == sorted(hashes[k] for k in (2, 4, 6, 8))
+    part, _ = B.applyChanges(B.init(), chg[:4])
+    assert sorted(B.changeHashes(B.getChangesAdded(part, st))) == sorted(hashes[4:])
+    q, _ = B.applyChanges(B.init(), [chg[0], chg[3]])  # change 3 waits for change 1
+    assert B.getMissingDeps(q) == [hashes[1]]
