@@ -286,6 +286,7 @@ struct am_batch {
   DevBuf<uint8_t> fast_done;
   uint32_t fast_lds = 0;
   bool fast_only = false;
+  bool any_diff = false;
   uint32_t lds_bytes = 0;
   uint64_t max_hot_v = 0;
   DevBuf<uint8_t> ws;
@@ -302,7 +303,7 @@ struct am_batch {
     BatchDev b;
     b.arena = arena.p; b.chunks = chunks.p; b.docs = docs.p; b.known = known.p; b.info = info.p; b.hdr = hdr.p; b.bounds = bounds.p;
     b.ws_bytes = ws_bytes.p; b.ws_off = ws_off.p; b.scan_tmp = scan_tmp.p; b.ws_total = ws_total.p; b.max_hot = max_hot.p; b.lds_bytes = lds_bytes; b.max_hot_host = max_hot_v; b.ws = ws.p;
-    b.fast_lds = fast_lds; b.fast_done = fast_done.p; b.fast_only = fast_only;
+    b.fast_lds = fast_lds; b.fast_done = fast_done.p; b.fast_only = fast_only; b.any_diff = any_diff;
     b.ws_cap = ws.cap; b.results = results.p; b.chg_state = chg_state.p; b.nchunks = nchunks; b.ndocs = ndocs;
     return b;
   }
@@ -442,6 +443,8 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   if (nknown) HIPCHECK(hipMemcpyAsync(b->known.p, known, sizeof(am_known_hash) * nknown, hipMemcpyHostToDevice, s));
   b->nchunks = nchunks;
   b->ndocs = ndocs;
+  b->any_diff = false;
+  for (uint32_t d = 0; d < ndocs && !b->any_diff; d++) b->any_diff = (docs[d].flags & AM_DOC_WANT_DIFF) != 0;
   if (!inflate_stage(b, arena, arena_len, chunks, nchunks, docs, ndocs)) return false;
   // sizing pass: chunk counts -> per-document workspace bounds -> total
   BatchDev d = b->dev();
@@ -557,27 +560,18 @@ extern "C" int am_batch_doc_patch(am_batch* b, uint32_t doc, uint8_t* dst, uint6
   if (hipMemcpy(&r, b->results.p + doc, sizeof r, hipMemcpyDeviceToHost) != hipSuccess) return 1;
   if (hipMemcpy(&bd, b->bounds.p + doc, sizeof bd, hipMemcpyDeviceToHost) != hipSuccess) return 1;
   if (r.status) return 3;  // the document failed: there is no patch
-  if (!bd.P) return 4;     // not staged with AM_DOC_WANT_PATCH
+  if (!bd.P) return 4;     // not staged with AM_DOC_WANT_PATCH / AM_DOC_WANT_DIFF
   const WsLayout L = ws_layout(bd);
-  const uint8_t* base = b->ws.p + r.ws_off + L.patch;
-  PatchHdr h;
+  // the wire form (am_patch.h): PatchHdr2 + stream, written by the kernel that merged the document
+  const uint8_t* base = b->ws.p + r.ws_off + L.pwire;
+  PatchHdr2 h;
   if (hipMemcpy(&h, base, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-  if (h.nrec > L.patch_nrec || h.nmval > L.patch_nmval || h.nheap > L.patch_heap) return 1;
-  const uint64_t total = sizeof h + sizeof(PatchRec) * h.nrec + sizeof(PatchVal) * h.nmval + h.nheap;
+  if (h.magic != AM_PATCH_MAGIC || sizeof h + h.nbytes > L.pwire_cap) return 1;
+  const uint64_t total = sizeof h + h.nbytes;
   *len = total;
   if (cap == 0) return 0;
   if (cap < total) return 2;
-  std::memcpy(dst, &h, sizeof h);
-  uint8_t* o = dst + sizeof h;
-  const uint8_t* rec = base + sizeof h;
-  const uint8_t* mval = rec + sizeof(PatchRec) * L.patch_nrec;
-  const uint8_t* heap = mval + sizeof(PatchVal) * L.patch_nmval;
-  if (h.nrec && hipMemcpy(o, rec, sizeof(PatchRec) * h.nrec, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-  o += sizeof(PatchRec) * h.nrec;
-  if (h.nmval && hipMemcpy(o, mval, sizeof(PatchVal) * h.nmval, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-  o += sizeof(PatchVal) * h.nmval;
-  if (h.nheap && hipMemcpy(o, heap, h.nheap, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-  return 0;
+  return hipMemcpy(dst, base, total, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
 
 extern "C" int am_batch_stage_times(am_batch* b, float* ms4) {
@@ -953,22 +947,29 @@ extern "C" am_doc* am_doc_load(am_engine* eng, const uint8_t* data, size_t len, 
 
 // The error a patch log carries (getPatch or applyChanges: updatePatchProperty new.js:944,
 // decodeValue columnar.js:318); false when the log is clean.
+// actor id i of a wire-form log (its ACTOR records come first), hex
+static std::string wire_actor(const std::vector<uint8_t>& log, int64_t want) {
+  HRd r{log.data(), log.size(), sizeof(PatchHdr2)};
+  for (int64_t i = 0; r.off < r.n && log[r.off] == PR_ACTOR; i++) {
+    r.off++;
+    const uint64_t l = r.u();
+    const uint8_t* p = r.raw(l);
+    if (!r.ok) break;
+    if (i == want) return hexs(p, l);
+  }
+  return "?";
+}
+
 static bool patch_log_error(const std::vector<uint8_t>& log, Err& e) {
-  PatchHdr h;
+  PatchHdr2 h;
+  if (log.size() < sizeof h) { e = Err{AM_U_CAPACITY, false, "automerge_amd: truncated patch log"}; return true; }
   std::memcpy(&h, log.data(), sizeof h);
   if (!h.status) return false;
   e = Err{h.status, false, ""};
   if (h.status == AM_E_FLOAT_LEN) {
     e.msg = fmt("Invalid length for floating point number: %lld", (long long)h.arg0);
   } else if (h.status == AM_E_UNKNOWN_COUNTER) {
-    std::string actor = "?";
-    const PatchRec* recs = reinterpret_cast<const PatchRec*>(log.data() + sizeof h);
-    for (uint64_t i = 0; i < h.nrec && recs[i].tag == PR_ACTOR; i++)
-      if ((int64_t)recs[i].a1 == h.arg1) {
-        const uint8_t* heap = log.data() + sizeof h + sizeof(PatchRec) * h.nrec + sizeof(PatchVal) * h.nmval;
-        actor = hexs(heap + recs[i].v0, (size_t)recs[i].v1);
-      }
-    e.msg = fmt("increment operation %lld@%s for unknown counter", (long long)h.arg0, actor.c_str());
+    e.msg = fmt("increment operation %lld@%s for unknown counter", (long long)h.arg0, wire_actor(log, h.arg1).c_str());
   } else {
     e.msg = fmt("automerge_amd: the patch is not supported for this document (code %u)", h.status);
   }
@@ -1182,7 +1183,8 @@ extern "C" int am_doc_get_patch(am_doc* d, uint8_t** out, size_t* len, am_error*
   if (err) err->code = 0;
   std::vector<uint8_t> log;
   if (d->state.empty()) {  // Backend.init(): documentPatch of an empty document
-    PatchHdr h{};
+    PatchHdr2 h{};
+    h.magic = AM_PATCH_MAGIC;
     log.resize(sizeof h);
     std::memcpy(log.data(), &h, sizeof h);
   } else {

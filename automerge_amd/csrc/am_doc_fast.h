@@ -117,7 +117,7 @@ __host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t n
 }
 
 __host__ __device__ inline bool fast_eligible(const DocBounds& b, const am_doc_desc& dd) {
-  if (dd.flags & (AM_DOC_WANT_PATCH | AM_DOC_WANT_DIFF)) return false;
+  if (dd.flags & AM_DOC_WANT_PATCH) return false;  // getPatch: k_doc (P7); applyChanges patches: fast_diff
   if (b.B == 0 || doc_scattered(b)) return false;
   if (dd.base_chunk < 0 && dd.chg_count == 0) return false;
   if (b.span_hi - b.span_lo > FD_SPAN_MAX) return false;
@@ -509,6 +509,275 @@ __device__ __forceinline__ uint32_t enc32k(uint8_t kind, uint32_t n, int32_t v, 
   }
 }
 
+// decodeValue (columnar.js:300-329) of a row's valLen / valRaw as the patch log carries it;
+// strings and byte arrays point into the staged input (v0 = offset, v1 = length). false: the
+// value raises an error (float length, integer range) -- k_doc reports it.
+__device__ __forceinline__ bool fd_value(const uint8_t* in, int32_t vlen, uint32_t voff, uint32_t& vt, uint32_t& dt, int64_t& v0,
+                                         int64_t& v1) {
+  const uint32_t tag = vlen == FD_NULL ? 0u : (uint32_t)vlen;
+  dt = 0;
+  v0 = v1 = 0;
+  if (tag <= 2) { vt = PV_NULL + tag; return true; }
+  const uint32_t t = tag & 15, len = tag >> 4;
+  if (t == 5) {
+    if (len != 8) return false;
+    uint64_t x = 0;
+    for (int q = 0; q < 8; q++) x |= (uint64_t)in[voff + q] << (8 * q);
+    v0 = (int64_t)x;
+    vt = PV_F64;
+    return true;
+  }
+  if (t == 3 || t == 4 || t == 8 || t == 9) {
+    Rd rd{in + voff, len, 0};
+    int64_t x;
+    if ((t == 3 ? rd_u53(rd, x) : rd_i53(rd, x)) != AM_OK) return false;
+    v0 = x;
+    vt = t == 3 ? PV_UINT : t == 4 ? PV_INT : t == 8 ? PV_COUNTER : PV_TIMESTAMP;
+    return true;
+  }
+  v0 = voff;
+  v1 = len;
+  vt = t == 6 ? PV_STR : PV_BYTES;
+  dt = t == 6 ? 0u : t;
+  return true;
+}
+
+// The patch Backend.applyChanges returns (new.js:1796-1871), written by the whole wave in wire form
+// (am_patch.h) for the common shape of a batch of concurrent edits: every applied op is a `set` of
+// a map key of the root object, or a `set` that inserts a list element into one list/text object
+// whose make op is the only visible value of its root key. For that shape the serial replay of
+// am_diff.h reduces to closed forms:
+//   * a touched key's props are its visible ops in the merged document (each mergeDocChangeOps
+//     call over a key rewrites props[key] from every op of the key, new.js:884-1040, and the last
+//     call sees the final set);
+//   * an insert's index is the number of visible elements of the list that precede it in the
+//     merged order and exist when it applies (base elements with a row without succ, earlier
+//     inserts of the call): a popcount over row masks;
+//   * appendEdit's multi-insert coalescing (new.js:747-782) joins an insert to the previous edit of
+//     the list iff index, element counter and actor continue it with the same datatype and JS
+//     type -- a segmented run over the insert lanes;
+//   * setupPatches links the list to the root through its key (new.js:1461-1528).
+// Anything else returns false before any result is committed and the document goes to k_doc,
+// whose lane-0 replay covers every shape. Scratch: 320 bytes at PS (the output image has left).
+__device__ __forceinline__ bool fast_diff(const uint8_t* IN, uint8_t* PS, uint32_t ps_cap, uint8_t* out, uint64_t out_cap,
+                                          uint32_t R, uint32_t nb, uint32_t NOUT, uint32_t NA, uint32_t NC, uint32_t nbc,
+                                          uint32_t k_row, uint32_t sc_k, bool r_chg, int32_t r_act, bool keyed, int32_t r_key,
+                                          uint32_t r_krank, int32_t r_objc, int32_t r_obja, uint64_t r_objkey, bool r_ins,
+                                          int32_t r_idc, int32_t r_ida, int32_t r_vlen, uint32_t r_voff, int32_t r_elem,
+                                          uint32_t a_len, uint32_t a_off, uint32_t bc_actor, int64_t bc_seq, uint32_t a_dp,
+                                          const ChgHdrC* chh) {
+  const uint32_t l = lane();
+  bool pbad = ps_cap < 512;
+  if (__any(pbad)) return false;
+  uint8_t* const POS = PS;        // row -> output position
+  uint8_t* const SCR = PS + 64;   // row -> succ count in the merged document
+  uint8_t* const EV = PS + 128;   // element (insert row) -> visible
+  uint8_t* const TCH = PS + 192;  // key rank -> set by a change op of the call
+  uint32_t* const LASTC = reinterpret_cast<uint32_t*>(PS + 256);  // doc actor -> its last change row
+  const bool isrow = l < R;
+  EV[l] = 0;
+  TCH[l] = 0;
+  LASTC[l] = 0;
+  wsync();
+  if (l < NOUT) { POS[k_row] = (uint8_t)l; SCR[k_row] = (uint8_t)(sc_k > 255 ? 255 : sc_k); }
+  const bool set_root = r_chg && r_act == 1 && keyed && r_objc == FD_NULL;
+  const bool list_ins = r_chg && r_act == 1 && !keyed && r_ins;
+  pbad |= r_chg && !(set_root || list_ins);
+  if (set_root) TCH[r_krank] = 1;
+  wsync();
+  if (__any(pbad)) return false;
+  // visible elements: an element is visible while one of its rows has no succ (new.js:50-192)
+  if (isrow && !r_chg && r_elem >= 0 && SCR[l] == 0) EV[r_elem] = 1;
+  // the list object of the inserts: exactly one
+  const uint64_t mli = __ballot(list_ins);
+  const uint32_t f0 = mli ? ctz64(mli) : 0u;
+  const uint64_t lkey = __shfl(r_objkey, f0, 64);
+  const int32_t lc = __shfl(r_objc, f0, 64), la = __shfl(r_obja, f0, 64);
+  pbad |= list_ins && r_objkey != lkey;
+  // its make op M: a visible base row of a root key that no change touched, the key's only
+  // visible value (objectMeta children of the root, new.js:894-930)
+  const uint64_t mm = mli ? __ballot(isrow && r_idc == lc && r_ida == la) : 0ull;
+  const uint32_t mrow = mm ? ctz64(mm) : 0u;
+  const int32_t m_act = __shfl(r_act, mrow, 64), m_objc = __shfl(r_objc, mrow, 64), m_key = __shfl(r_key, mrow, 64);
+  const uint32_t m_kr = __shfl(r_krank, mrow, 64);
+  wsync();
+  if (mli) {
+    pbad |= l == 0 && (!mm || mrow >= nb || m_objc != FD_NULL || m_key == FD_NULL || (m_key & 255) == 0 ||
+                       (m_act != 2 && m_act != 4) || SCR[mrow] != 0 || TCH[m_kr]);
+    pbad |= isrow && r_objc == FD_NULL && keyed && r_krank == m_kr && l != mrow && SCR[l] == 0;
+  }
+  // the rows of a touched key are plain sets (no child objects, no increments), keys non-empty
+  const bool touched = isrow && keyed && r_objc == FD_NULL && TCH[r_krank];
+  pbad |= touched && (r_act != 1 || (r_key & 255) == 0);
+  if (__any(pbad)) return false;
+
+  // ---- record sizes; segments in stream order: actors, clock, root object, root keys, list ----
+  // actors (PR_ACTOR)
+  uint32_t tot;
+  const uint32_t b_act = l < NA ? 1u + pk_uleb_len(a_len) + a_len : 0u;
+  const uint32_t o_act = excl_add(b_act, tot);
+  uint32_t base = tot;
+  // clock (PR_CLOCK): each actor's last change row
+  const uint32_t kc = l >= nbc ? l - nbc : 0u;
+  const uint32_t kc_adp = __shfl(a_dp, kc & 63, 64);  // every lane takes part in the shuffle
+  const uint32_t c_actor = l < nbc ? bc_actor : kc_adp;
+  const int64_t c_seq = l < nbc ? bc_seq : chh[kc < 64 ? kc : 0].seq;
+  if (l < NC) atomicMax(&LASTC[c_actor], l);
+  wsync();
+  const bool c_emit = l < NC && LASTC[c_actor] == l;
+  const uint32_t b_clk = c_emit ? 1u + pk_uleb_len(c_actor) + pk_uleb_len((uint64_t)c_seq) : 0u;
+  const uint32_t o_clk = base + excl_add(b_clk, tot);
+  base += tot;
+  const uint32_t o_root = base;  // PR_OBJ _root: tag, sleb -1, sleb -1, uleb 0
+  base += 4;
+  // root keys (PR_KEY / PR_PROP), output lane p holds the row at position p
+  const uint32_t r = k_row;
+  const bool outl = l < NOUT;
+  const int32_t k_objc = __shfl(r_objc, r, 64), k_key = __shfl(r_key, r, 64), k_vlen = __shfl(r_vlen, r, 64);
+  const uint32_t k_kr = __shfl(r_krank, r, 64), k_voff = __shfl(r_voff, r, 64);
+  const int32_t k_idc = __shfl(r_idc, r, 64), k_ida = __shfl(r_ida, r, 64);
+  const bool k_keyed = outl && k_key != FD_NULL && k_objc == FD_NULL;
+  const bool k_tch = k_keyed && (TCH[k_kr] || (mli && k_kr == m_kr));
+  const uint32_t p_kr = wave::up1(k_kr, ~0u);
+  const bool p_tch = wave::up1((uint32_t)k_tch, 0u) != 0;
+  const bool emit_key = k_tch && !(l > 0 && p_tch && p_kr == k_kr);
+  const bool emit_prop = k_tch && SCR[r] == 0;
+  const bool is_m = mli && r == mrow;
+  uint32_t pvt = 0, pdt = 0;
+  int64_t pv0 = 0, pv1 = 0;
+  if (emit_prop) {
+    if (is_m) { pvt = PV_CHILD; pdt = m_act == 2 ? 1u : 2u; pv0 = lc; pv1 = la; }
+    else pbad |= !fd_value(IN, k_vlen, k_voff, pvt, pdt, pv0, pv1);
+  }
+  const uint32_t klen = (uint32_t)k_key & 255;
+  const uint32_t b_key = (emit_key ? 1u + pk_uleb_len(klen) + klen : 0u) +
+                         (emit_prop ? 1u + pk_uleb_len((uint64_t)k_idc) + pk_uleb_len((uint64_t)k_ida) +
+                                          pk_value_len(pvt, pdt, pv0, pv1)
+                                    : 0u);
+  const uint32_t o_key = base + excl_add(b_key, tot);
+  base += tot;
+  // the list object: PR_OBJ, then its edits in application order (lane = change row)
+  const uint32_t o_lobj = base;
+  const uint32_t ltype = m_act == 2 ? 1u : 2u;
+  if (mli) base += 1 + pk_sleb_len(lc) + pk_sleb_len(la) + pk_uleb_len(ltype);
+  // index: visible elements of the list before the insert's position that exist when it applies
+  uint64_t below;  // rows at output positions < this lane's position (exclusive OR-scan)
+  {
+    uint64_t x = outl ? (1ull << r) : 0ull;
+    uint64_t inc = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y = __shfl_up(inc, d, 64);
+      if ((int)l >= d) inc |= y;
+    }
+    below = inc & ~x;
+  }
+  const uint64_t el_l = __ballot(isrow && r_elem == (int32_t)l && r_objkey == lkey);  // elements of the list
+  const uint64_t vis_base = __ballot(isrow && l < nb && EV[l]);
+  uint32_t ins_vt = 0, ins_dt = 0, dtc = 0;
+  int64_t ins_v0 = 0, ins_v1 = 0;
+  int64_t idx = 0;
+  const uint64_t bl = __shfl(below, POS[l] & 63, 64);
+  if (list_ins) {
+    const uint64_t exist = (vis_base | (nb >= 64 ? 0ull : ~0ull << nb)) & lt_mask();  // visible base elements, earlier inserts
+    idx = __popcll(el_l & exist & bl);
+    pbad |= !fd_value(IN, r_vlen, r_voff, ins_vt, ins_dt, ins_v0, ins_v1);
+    dtc = pv_dtcode(ins_vt, ins_dt);
+    pbad |= dtc == 100;  // datatype 0 (falsy): appendEdit's chain rule differs; k_doc replays it
+  }
+  // appendEdit chain: previous insert of the call (same list), contiguous index / id, same types
+  const uint64_t before = mli & lt_mask();
+  const uint32_t prev = before ? 63u - (uint32_t)__clzll(before) : 0u;
+  const int64_t p_idx = __shfl(idx, prev, 64);
+  const int32_t p_idc = __shfl(r_idc, prev, 64), p_ida = __shfl(r_ida, prev, 64);
+  const uint32_t p_dtc = __shfl(dtc, prev, 64), p_ty = __shfl((uint32_t)pv_typeof(ins_vt), prev, 64);
+  const bool chain = list_ins && before && p_idx + 1 == idx && p_ida == r_ida && p_idc + 1 == r_idc && p_dtc == dtc &&
+                     p_ty == (uint32_t)pv_typeof(ins_vt);
+  const bool start = list_ins && !chain;
+  const uint64_t smask = __ballot(start);
+  const uint64_t above = l == 63 ? 0ull : (smask >> (l + 1)) << (l + 1);
+  const uint32_t nxt = above ? ctz64(above) : 64u;
+  const uint64_t span = (nxt >= 64 ? ~0ull : ((1ull << nxt) - 1)) & ~((1ull << l) - 1);
+  const uint32_t run = start ? (uint32_t)__popcll(mli & span) : 0u;
+  const uint32_t mdt = pv_dt_truthy(dtc) ? dtc : 0u;
+  uint32_t b_ed = 0;
+  if (list_ins) {
+    if (start && run >= 2)
+      b_ed = 1 + pk_uleb_len((uint64_t)idx) + pk_uleb_len((uint64_t)r_idc) + pk_uleb_len((uint64_t)r_ida) + pk_uleb_len(mdt) +
+             pk_uleb_len(run);
+    else if (start)
+      b_ed = 1 + pk_uleb_len((uint64_t)idx) + 2 * (pk_uleb_len((uint64_t)r_idc) + pk_uleb_len((uint64_t)r_ida));
+    b_ed += pk_value_len(ins_vt, ins_dt, ins_v0, ins_v1);
+  }
+  const uint32_t o_ed = base + excl_add(b_ed, tot);
+  base += tot;
+  pbad |= sizeof(PatchHdr2) + (uint64_t)base > out_cap;
+  if (__any(pbad)) return false;
+
+  // ---- write ----
+  uint8_t* const o = out + sizeof(PatchHdr2);
+  if (b_act) {
+    uint8_t* p = o + o_act;
+    *p++ = PR_ACTOR;
+    p = pk_uleb(p, a_len);
+    for (uint32_t q = 0; q < a_len; q++) p[q] = IN[a_off + q];
+  }
+  if (b_clk) {
+    uint8_t* p = o + o_clk;
+    *p++ = PR_CLOCK;
+    p = pk_uleb(p, c_actor);
+    pk_uleb(p, (uint64_t)c_seq);
+  }
+  if (l == 0) { o[o_root] = PR_OBJ; o[o_root + 1] = 0x7f; o[o_root + 2] = 0x7f; o[o_root + 3] = 0; }
+  if (b_key) {
+    uint8_t* p = o + o_key;
+    if (emit_key) {
+      *p++ = PR_KEY;
+      p = pk_uleb(p, klen);
+      const uint32_t ko = (uint32_t)k_key >> 8;
+      for (uint32_t q = 0; q < klen; q++) *p++ = IN[ko + q];
+    }
+    if (emit_prop) {
+      *p++ = PR_PROP;
+      p = pk_uleb(p, (uint64_t)k_idc);
+      p = pk_uleb(p, (uint64_t)k_ida);
+      pk_value(p, pvt, pdt, pv0, pv1, pv_has_bytes(pvt) ? IN + pv0 : nullptr);
+    }
+  }
+  if (mli && l == 0) {
+    uint8_t* p = o + o_lobj;
+    *p++ = PR_OBJ;
+    p = pk_sleb(p, lc);
+    p = pk_sleb(p, la);
+    pk_uleb(p, ltype);
+  }
+  if (list_ins) {
+    uint8_t* p = o + o_ed;
+    if (start && run >= 2) {
+      *p++ = PR_MULTI;
+      p = pk_uleb(p, (uint64_t)idx);
+      p = pk_uleb(p, (uint64_t)r_idc);
+      p = pk_uleb(p, (uint64_t)r_ida);
+      p = pk_uleb(p, mdt);
+      p = pk_uleb(p, run);
+    } else if (start) {
+      *p++ = PR_INSERT;
+      p = pk_uleb(p, (uint64_t)idx);
+      p = pk_uleb(p, (uint64_t)r_idc);
+      p = pk_uleb(p, (uint64_t)r_ida);
+      p = pk_uleb(p, (uint64_t)r_idc);
+      p = pk_uleb(p, (uint64_t)r_ida);
+    }
+    pk_value(p, ins_vt, ins_dt, ins_v0, ins_v1, pv_has_bytes(ins_vt) ? IN + ins_v0 : nullptr);
+  }
+  if (l == 0) {
+    PatchHdr2 h;
+    h.magic = AM_PATCH_MAGIC; h.status = 0; h.arg0 = 0; h.arg1 = 0; h.max_op = 0; h.nbytes = base; h.pad = 0;
+    *reinterpret_cast<PatchHdr2*>(out) = h;
+  }
+  return true;
+}
+
 }  // namespace fastdoc
 
 // registers for three waves per SIMD (<= 168 VGPRs): with the LDS slice of a C4 document (~13 KB)
@@ -517,6 +786,9 @@ __device__ __forceinline__ uint32_t enc32k(uint8_t kind, uint32_t n, int32_t v, 
 #define AM_FAST_WAVES 3
 #endif
 #define FD_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(AM_FAST_WAVES, 8)))
+// kDiff: the variant launched for batches that ask for applyChanges patches (it also merges the
+// documents that do not); the other keeps the register budget of the plain merge.
+template <bool kDiff>
 __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     k_doc_fast(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks, const am_doc_desc* __restrict__ docs,
                const am_known_hash* __restrict__ known, const ChunkInfo* __restrict__ info,
@@ -1528,6 +1800,12 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     }
   }
   FPH(13);
+  if (!kDiff && b.P == 2) return;  // launched without the patch writer: k_doc replays the patch
+  if (kDiff && b.P == 2 && !fast_diff(IN, S + F.cells, F.cells_cap, wsg + L.pwire, L.pwire_cap, R, nb, NOUT, NA, NC, nbc, k_row, sc_k,
+                             r_chg, r_act, keyed, r_key, r_krank, r_objc, r_obja, r_objkey, r_ins, r_idc, r_ida, r_vlen,
+                             r_voff, r_elem, a_len, l < NA ? RO[2 * M[FM_DP2REF + l]] : 0u, bc_actor, bc_seq, a_dp, chh))
+    return;  // outside the shapes fast_diff covers: k_doc replays the patch (am_diff.h)
+  FPH(14);
   if (l < N) chg_state[dd.chg_begin + l] = (int32_t)l;
   if (l == 0) {
     am_doc_result r;

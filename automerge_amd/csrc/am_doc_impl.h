@@ -876,6 +876,14 @@ struct DiffSrc {
   __device__ uint32_t pass_end(uint32_t p) const { return pend[p]; }
 };
 
+// the log in wire form (am_patch.h patch_pack); a log that does not fit its region reports the
+// engine's capacity limit instead (never a truncated patch)
+__device__ static void wire_out(PatchOut& po, int64_t max_op, uint8_t* dst, uint64_t cap) {
+  if (patch_pack(po, max_op, dst, cap)) return;
+  po.status = PATCH_U_CAPACITY;
+  patch_pack(po, max_op, dst, cap);
+}
+
 __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
                                                const am_doc_desc* __restrict__ docs, const am_known_hash* __restrict__ known,
                                                const ChunkInfo* __restrict__ info, const DocBounds* __restrict__ bounds,
@@ -1515,11 +1523,7 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
       RowSrc src{rows, sr, succ_cnt, outent, NOUT, NSUCC, actors, s.nactors, chg, NC, A};
       int64_t pmax = 0;
       patch_scan(src, po, w, pmax);
-      PatchHdr* ph = reinterpret_cast<PatchHdr*>(pbase);
-      ph->status = po.status; ph->pad0 = 0;
-      ph->arg0 = po.arg0; ph->arg1 = po.arg1;
-      ph->nrec = po.nrec; ph->nmval = po.nmval; ph->nheap = po.nheap;
-      ph->max_op = pmax; ph->pad1 = 0;
+      wire_out(po, pmax, wsg + L.pwire, L.pwire_cap);
     }
     // P8: the patch applyChanges returns (am_diff.h), lane 0, after the merge
     if (s.b.P == 2 && t == 0) {
@@ -1535,11 +1539,7 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
                   reinterpret_cast<const uint32_t*>(wsg + L.passend), s.npass, s.nb, s.nrows, NOUT, NSUCC, actors,
                   s.nactors, chg, NC, A};
       diff_scan(src, po, dw);
-      PatchHdr* ph = reinterpret_cast<PatchHdr*>(pbase);
-      ph->status = po.status; ph->pad0 = 0;
-      ph->arg0 = po.arg0; ph->arg1 = po.arg1;
-      ph->nrec = po.nrec; ph->nmval = po.nmval; ph->nheap = po.nheap;
-      ph->max_op = 0; ph->pad1 = 0;
+      wire_out(po, 0, wsg + L.pwire, L.pwire_cap);
     }
     // heads for the host (hot region may be LDS): mirror into the global workspace
     if (kHotLds)

@@ -548,7 +548,7 @@ __global__ void __launch_bounds__(256) k_sha256(const uint8_t* __restrict__ aren
 #include "am_launch.h"
 
 static_assert(sizeof(Row) == AM_SZ_ROW, "Row");
-static_assert(sizeof(PatchRec) == 64 && sizeof(PatchVal) == 32 && sizeof(PatchHdr) == 64, "patch log layout");
+static_assert(sizeof(PatchRec) == 64 && sizeof(PatchVal) == 32 && sizeof(PatchHdr2) == 48, "patch log layout");
 static_assert(PATCH_E_FLOAT_LEN == AM_E_FLOAT_LEN && PATCH_E_UNKNOWN_COUNTER == AM_E_UNKNOWN_COUNTER &&
               PATCH_U_CAPACITY == AM_U_CAPACITY && PATCH_U_VALUE == AM_U_VALUE, "patch status codes");
 static_assert(sizeof(Ent) == AM_SZ_ENT, "Ent");
@@ -601,7 +601,7 @@ void am_launch_doc(const BatchDev& b, hipStream_t s) {
   const uint8_t* fd = nullptr;
   if (b.fast_lds && b.fast_done) {
     (void)hipMemsetAsync(b.fast_done, 0, b.ndocs, s);
-    hipLaunchKernelGGL(k_doc_fast, dim3((b.ndocs + FD_DOCS_PER_WG - 1) / FD_DOCS_PER_WG), dim3(64 * FD_DOCS_PER_WG),
+    hipLaunchKernelGGL(b.any_diff ? k_doc_fast<true> : k_doc_fast<false>, dim3((b.ndocs + FD_DOCS_PER_WG - 1) / FD_DOCS_PER_WG), dim3(64 * FD_DOCS_PER_WG),
                        FD_DOCS_PER_WG * b.fast_lds, s, b.arena, b.chunks, b.docs, b.known, b.info, b.hdr, b.bounds, b.ws_off, b.ws,
                        b.ws_cap, b.fast_lds, b.ndocs, b.results, b.chg_state, b.fast_done);
     fd = b.fast_done;

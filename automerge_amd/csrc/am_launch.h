@@ -23,6 +23,7 @@ struct BatchDev {
   uint32_t fast_lds;       // k_doc_fast LDS slice per document (0: no document in its envelope / disabled)
   uint8_t* fast_done;      // per doc: 1 = merged by k_doc_fast
   bool fast_only;          // every document is in the fast envelope: skip the k_doc launches
+  bool any_diff;           // some document asks for its applyChanges patch (k_doc_fast<true>)
   uint8_t* ws;
   uint64_t ws_cap;
   am_doc_result* results;

@@ -53,7 +53,8 @@ struct WsLayout {
   uint64_t hot_total;
   // cold (offsets relative to the document's global workspace, after the hot mirror)
   uint64_t out, out_cap, total;
-  uint64_t patch, patch_nrec, patch_nmval, patch_heap;  // patch log (when P)
+  uint64_t patch, patch_nrec, patch_nmval, patch_heap;  // patch log, working form (when P)
+  uint64_t pwire, pwire_cap;  // the same log in wire form (PatchHdr2 + stream, am_patch.h)
   uint64_t etime, passend, dscr;  // applyChanges patch (P == 2): succ-entry times, pass ends, replay pools
   uint64_t colbuf[OC_NCOLS + DC_NCOLS];
 };
@@ -180,6 +181,9 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   } else {
     L.patch = L.patch_nrec = L.patch_nmval = L.patch_heap = 0;
   }
+  // a packed record never exceeds its working-form size (am_patch.h patch_pack)
+  L.pwire_cap = b.P ? 64 + 64 * L.patch_nrec + 32 * L.patch_nmval + L.patch_heap : 0;
+  L.pwire = b.P ? take(L.pwire_cap) : 0;
   if (b.P == 2) {
     L.etime = take(4 * (E + 1));
     L.passend = take(4 * (N + 1));

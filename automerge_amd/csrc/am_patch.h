@@ -20,7 +20,7 @@
 #define AM_PHD __attribute__((always_inline))
 #endif
 
-// ---- log layout: PatchHdr, then nrec PatchRec, then nmval PatchVal, then nheap bytes ----
+// ---- working form of the log: nrec PatchRec, nmval PatchVal, nheap bytes (wire form below) ----
 enum : uint32_t {
   PR_ACTOR = 1,   // actor id i: heap [v0, v0 + v1)
   PR_CLOCK = 2,   // clock[actor a1] = index
@@ -60,15 +60,6 @@ struct PatchVal {  // 32 bytes: a multi-insert value (the primitive only)
   uint32_t vtag, dt;
   int64_t v0, v1, pad;
 };
-struct PatchHdr {  // 64 bytes
-  uint32_t status;       // 0 ok, else AM_* code of the error getPatch throws
-  uint32_t pad0;
-  int64_t arg0, arg1;    // error arguments (counter increment: ctr, actor index)
-  uint64_t nrec, nmval, nheap;
-  int64_t max_op;        // documentPatch's maxOp (max op id / succ counter)
-  uint64_t pad1;
-};
-
 struct PatchOut {
   PatchRec* rec;
   PatchVal* mval;
@@ -77,6 +68,182 @@ struct PatchOut {
   uint32_t status;
   int64_t arg0, arg1;
 };
+
+// ---- wire form: what leaves the device and what the host stages read ----
+// The fixed-size records above are the writers' working form (the scans pop and rewrite the tail
+// of the log in place). The log handed to the host is PatchHdr2 followed by a byte stream of the
+// same records, LEB128 fields and inline strings, 10-20x smaller than the working form:
+//   ACTOR  uleb len, bytes               CLOCK  uleb actor, uleb seq
+//   OBJ    sleb ctr, sleb actor, uleb type (root: -1, -1)
+//   KEY    uleb len, bytes               PROP   uleb ctr, uleb actor, VALUE
+//   INSERT uleb index, uleb elem ctr, uleb elem actor, uleb op ctr, uleb op actor, VALUE
+//   MULTI  uleb index, uleb elem ctr, uleb elem actor, uleb datatype code, uleb n, n x VALUE
+//   UPDATE uleb index, uleb op ctr, uleb op actor, VALUE
+//   REMOVE uleb index, uleb count
+//   VALUE  vtag byte, then: STR uleb len + bytes | UINT uleb | INT / COUNTER / TIMESTAMP sleb |
+//          F64 8 bytes LE | BYTES uleb datatype, uleb len, bytes | CHILD uleb ctr, uleb actor,
+//          uleb type | nothing for NULL / FALSE / TRUE
+// Every record starts with its tag byte. Hosts: automerge_amd/patch.py, automerge_amd/js/backend.js.
+#define AM_PATCH_MAGIC 0x32504d41u  // "AMP2"
+struct PatchHdr2 {  // 48 bytes
+  uint32_t magic;
+  uint32_t status;    // 0 ok, else the AM_* code of the error the call throws
+  int64_t arg0, arg1; // error arguments (counter increment: ctr, actor index)
+  int64_t max_op;     // documentPatch's maxOp (getPatch logs)
+  uint64_t nbytes;    // stream bytes after the header
+  uint64_t pad;
+};
+
+AM_PHD inline uint32_t pk_uleb_len(uint64_t v) {
+  uint32_t n = 1;
+  while (v >= 0x80) { v >>= 7; n++; }
+  return n;
+}
+AM_PHD inline uint32_t pk_sleb_len(int64_t v) {
+  uint32_t n = 1;
+  while (!((v >= -64) && (v < 64))) { v >>= 7; n++; }
+  return n;
+}
+AM_PHD inline uint8_t* pk_uleb(uint8_t* o, uint64_t v) {
+  while (v >= 0x80) { *o++ = (uint8_t)(v | 0x80); v >>= 7; }
+  *o++ = (uint8_t)v;
+  return o;
+}
+AM_PHD inline uint8_t* pk_sleb(uint8_t* o, int64_t v) {
+  for (;;) {
+    const uint8_t b = (uint8_t)(v & 0x7f);
+    v >>= 7;
+    if ((v == 0 && !(b & 0x40)) || (v == -1 && (b & 0x40))) { *o++ = b; return o; }
+    *o++ = (uint8_t)(b | 0x80);
+  }
+}
+// bytes of a VALUE (vtag, dt, v0, v1; strings / bytes at heap + v0)
+AM_PHD inline uint32_t pk_value_len(uint32_t vtag, uint32_t dt, int64_t v0, int64_t v1) {
+  switch (vtag) {
+    case PV_STR: return 1 + pk_uleb_len((uint64_t)v1) + (uint32_t)v1;
+    case PV_UINT: return 1 + pk_uleb_len((uint64_t)v0);
+    case PV_INT: case PV_COUNTER: case PV_TIMESTAMP: return 1 + pk_sleb_len(v0);
+    case PV_F64: return 9;
+    case PV_BYTES: return 1 + pk_uleb_len(dt) + pk_uleb_len((uint64_t)v1) + (uint32_t)v1;
+    case PV_CHILD: return 1 + pk_uleb_len((uint64_t)v0) + pk_uleb_len((uint64_t)v1) + pk_uleb_len(dt);
+    default: return 1;
+  }
+}
+AM_PHD inline uint8_t* pk_value(uint8_t* o, uint32_t vtag, uint32_t dt, int64_t v0, int64_t v1, const uint8_t* bytes) {
+  *o++ = (uint8_t)vtag;
+  switch (vtag) {
+    case PV_STR:
+      o = pk_uleb(o, (uint64_t)v1);
+      for (int64_t q = 0; q < v1; q++) *o++ = bytes[q];
+      break;
+    case PV_UINT: o = pk_uleb(o, (uint64_t)v0); break;
+    case PV_INT: case PV_COUNTER: case PV_TIMESTAMP: o = pk_sleb(o, v0); break;
+    case PV_F64:
+      for (int q = 0; q < 8; q++) *o++ = (uint8_t)((uint64_t)v0 >> (8 * q));
+      break;
+    case PV_BYTES:
+      o = pk_uleb(o, dt);
+      o = pk_uleb(o, (uint64_t)v1);
+      for (int64_t q = 0; q < v1; q++) *o++ = bytes[q];
+      break;
+    case PV_CHILD:
+      o = pk_uleb(o, (uint64_t)v0);
+      o = pk_uleb(o, (uint64_t)v1);
+      o = pk_uleb(o, dt);
+      break;
+    default: break;
+  }
+  return o;
+}
+AM_PHD inline bool pv_has_bytes(uint32_t vtag) { return vtag == PV_STR || vtag == PV_BYTES; }
+
+// Serializes a working-form log into its wire form at dst (capacity cap bytes, header included).
+// Returns the total bytes, or 0 when cap is too small.
+AM_PHD inline uint64_t patch_pack(const PatchOut& o, int64_t max_op, uint8_t* dst, uint64_t cap) {
+  PatchHdr2 h;
+  h.magic = AM_PATCH_MAGIC;
+  h.status = o.status;
+  h.arg0 = o.arg0;
+  h.arg1 = o.arg1;
+  h.max_op = max_op;
+  h.pad = 0;
+  uint64_t n = 0;
+  if (!o.status) {
+    uint64_t mv = 0;
+    for (uint64_t k = 0; k < o.nrec; k++) {
+      const PatchRec& r = o.rec[k];
+      uint64_t b = 1;
+      switch (r.tag) {
+        case PR_ACTOR: case PR_KEY: b += pk_uleb_len((uint64_t)r.v1) + (uint64_t)r.v1; break;
+        case PR_CLOCK: b += pk_uleb_len((uint64_t)r.a1) + pk_uleb_len((uint64_t)r.index); break;
+        case PR_OBJ: b += pk_sleb_len(r.c1) + pk_sleb_len(r.a1) + pk_uleb_len(r.dt); break;
+        case PR_PROP: b += pk_uleb_len((uint64_t)r.c2) + pk_uleb_len((uint64_t)r.a2) + pk_value_len(r.vtag, r.dt, r.v0, r.v1); break;
+        case PR_INSERT:
+          b += pk_uleb_len((uint64_t)r.index) + pk_uleb_len((uint64_t)r.c1) + pk_uleb_len((uint64_t)r.a1) +
+               pk_uleb_len((uint64_t)r.c2) + pk_uleb_len((uint64_t)r.a2) + pk_value_len(r.vtag, r.dt, r.v0, r.v1);
+          break;
+        case PR_MULTI:
+          b += pk_uleb_len((uint64_t)r.index) + pk_uleb_len((uint64_t)r.c1) + pk_uleb_len((uint64_t)r.a1) +
+               pk_uleb_len(r.dt) + pk_uleb_len(r.n);
+          for (uint32_t q = 0; q < r.n; q++) {
+            const PatchVal& v = o.mval[mv + q];
+            b += pk_value_len(v.vtag, v.dt, v.v0, v.v1);
+          }
+          mv += r.n;
+          break;
+        case PR_UPDATE:
+          b += pk_uleb_len((uint64_t)r.index) + pk_uleb_len((uint64_t)r.c2) + pk_uleb_len((uint64_t)r.a2) +
+               pk_value_len(r.vtag, r.dt, r.v0, r.v1);
+          break;
+        default: b += pk_uleb_len((uint64_t)r.index) + pk_uleb_len(r.n); break;  // PR_REMOVE
+      }
+      n += b;
+    }
+  }
+  h.nbytes = n;
+  if (sizeof(PatchHdr2) + n > cap) return 0;
+  const uint8_t* hb = reinterpret_cast<const uint8_t*>(&h);
+  for (uint32_t q = 0; q < sizeof(PatchHdr2); q++) dst[q] = hb[q];
+  uint8_t* p = dst + sizeof(PatchHdr2);
+  if (o.status) return sizeof(PatchHdr2);
+  uint64_t mv = 0;
+  for (uint64_t k = 0; k < o.nrec; k++) {
+    const PatchRec& r = o.rec[k];
+    *p++ = (uint8_t)r.tag;
+    switch (r.tag) {
+      case PR_ACTOR: case PR_KEY:
+        p = pk_uleb(p, (uint64_t)r.v1);
+        for (int64_t q = 0; q < r.v1; q++) *p++ = o.heap[r.v0 + q];
+        break;
+      case PR_CLOCK: p = pk_uleb(p, (uint64_t)r.a1); p = pk_uleb(p, (uint64_t)r.index); break;
+      case PR_OBJ: p = pk_sleb(p, r.c1); p = pk_sleb(p, r.a1); p = pk_uleb(p, r.dt); break;
+      case PR_PROP:
+        p = pk_uleb(p, (uint64_t)r.c2); p = pk_uleb(p, (uint64_t)r.a2);
+        p = pk_value(p, r.vtag, r.dt, r.v0, r.v1, pv_has_bytes(r.vtag) ? o.heap + r.v0 : nullptr);
+        break;
+      case PR_INSERT:
+        p = pk_uleb(p, (uint64_t)r.index); p = pk_uleb(p, (uint64_t)r.c1); p = pk_uleb(p, (uint64_t)r.a1);
+        p = pk_uleb(p, (uint64_t)r.c2); p = pk_uleb(p, (uint64_t)r.a2);
+        p = pk_value(p, r.vtag, r.dt, r.v0, r.v1, pv_has_bytes(r.vtag) ? o.heap + r.v0 : nullptr);
+        break;
+      case PR_MULTI:
+        p = pk_uleb(p, (uint64_t)r.index); p = pk_uleb(p, (uint64_t)r.c1); p = pk_uleb(p, (uint64_t)r.a1);
+        p = pk_uleb(p, r.dt); p = pk_uleb(p, r.n);
+        for (uint32_t q = 0; q < r.n; q++) {
+          const PatchVal& v = o.mval[mv + q];
+          p = pk_value(p, v.vtag, v.dt, v.v0, v.v1, pv_has_bytes(v.vtag) ? o.heap + v.v0 : nullptr);
+        }
+        mv += r.n;
+        break;
+      case PR_UPDATE:
+        p = pk_uleb(p, (uint64_t)r.index); p = pk_uleb(p, (uint64_t)r.c2); p = pk_uleb(p, (uint64_t)r.a2);
+        p = pk_value(p, r.vtag, r.dt, r.v0, r.v1, pv_has_bytes(r.vtag) ? o.heap + r.v0 : nullptr);
+        break;
+      default: p = pk_uleb(p, (uint64_t)r.index); p = pk_uleb(p, r.n); break;
+    }
+  }
+  return sizeof(PatchHdr2) + n;
+}
 
 // errors of getPatch (mirrors include/automerge_amd.h codes; see am_common.h static_asserts)
 #define PATCH_E_FLOAT_LEN 31u   // Invalid length for floating point number: arg0

@@ -86,13 +86,22 @@ const NAMED_DT = {5: 'uint', 6: 'int', 7: 'float64', 8: 'counter', 9: 'timestamp
 const OBJ_TYPES = ['map', 'list', 'text', 'table']
 const utf8 = new TextDecoder('utf-8')
 
+// Wire form (am_patch.h): PatchHdr2 (48 B: magic, status, arg0, arg1, maxOp, nbytes, pad) + stream
 function materializePatch(log, deps, pendingChanges, maxOp) {
   const dv = new DataView(log.buffer, log.byteOffset, log.byteLength)
-  const i64 = o => Number(dv.getBigInt64(o, true))
-  const nrec = i64(24), nmval = i64(32), nheap = i64(40)
-  const recAt = k => 64 + 64 * k, valAt = k => 64 + 64 * nrec + 32 * k
-  const heapOff = 64 + 64 * nrec + 32 * nmval
-  const heap = log.subarray(heapOff, heapOff + nheap)
+  const end = 48 + Number(dv.getBigUint64(32, true))
+  let o = 48
+  const u = () => {
+    let v = 0, mul = 1, b
+    do { b = log[o++]; v += (b & 0x7f) * mul; mul *= 128 } while (b & 0x80)
+    return v
+  }
+  const s = () => {
+    let v = 0, mul = 1, b
+    do { b = log[o++]; v += (b & 0x7f) * mul; mul *= 128 } while (b & 0x80)
+    return (b & 0x40) ? v - mul : v
+  }
+  const raw = n => { const r = log.subarray(o, o + n); o += n; return r }
   const actors = [], clock = {}, nodes = new Map()
   const opid = (c, a) => `${c}@${actors[a]}`
   const node = (c, a, t) => {
@@ -105,56 +114,59 @@ function materializePatch(log, deps, pendingChanges, maxOp) {
     }
     return n
   }
-  const prim = (vtag, dt, o) => {
-    switch (vtag) {
-      case PV.NULL: return null
-      case PV.FALSE: return false
-      case PV.TRUE: return true
-      case PV.STR: return utf8.decode(heap.subarray(i64(o), i64(o) + i64(o + 8)))
-      case PV.F64: return dv.getFloat64(o, true)
-      case PV.BYTES: return heap.slice(i64(o), i64(o) + i64(o + 8))
-      default: return i64(o)
+  // [vtag, datatype code, primitive] of the VALUE at the cursor
+  const prim = () => {
+    const vt = log[o++]
+    switch (vt) {
+      case PV.NULL: return [vt, 0, null]
+      case PV.FALSE: return [vt, 0, false]
+      case PV.TRUE: return [vt, 0, true]
+      case PV.STR: return [vt, 0, utf8.decode(raw(u()))]
+      case PV.UINT: return [vt, 0, u()]
+      case PV.INT: case PV.COUNTER: case PV.TIMESTAMP: return [vt, 0, s()]
+      case PV.F64: { const x = dv.getFloat64(o, true); o += 8; return [vt, 0, x] }
+      case PV.BYTES: { const dt = u(); return [vt, dt, raw(u()).slice()] }
+      case PV.CHILD: { const c = u(), a = u(), t = u(); return [vt, t, [c, a]] }
+      default: throw new RangeError(`automerge_amd: bad patch value tag ${vt}`)
     }
   }
-  const value = (vtag, dt, o) => {
-    if (vtag === PV.CHILD) return node(i64(o), i64(o + 8), dt)
-    const v = {type: 'value', value: prim(vtag, dt, o)}
-    if (NAMED_DT[vtag]) v.datatype = NAMED_DT[vtag]
-    else if (vtag === PV.BYTES) v.datatype = dt
+  const value = () => {
+    const [vt, dt, x] = prim()
+    if (vt === PV.CHILD) return node(x[0], x[1], dt)
+    const v = {type: 'value', value: x}
+    if (NAMED_DT[vt]) v.datatype = NAMED_DT[vt]
+    else if (vt === PV.BYTES) v.datatype = dt
     return v
   }
   const root = {objectId: '_root', type: 'map', props: {}}
-  let cur = root, key = null, mv = 0
-  for (let k = 0; k < nrec; k++) {
-    const r = recAt(k)
-    const tag = dv.getUint32(r, true), vtag = dv.getUint32(r + 4, true)
-    const index = i64(r + 8), c1 = i64(r + 16), c2 = i64(r + 24)
-    const a1 = dv.getInt32(r + 32, true), a2 = dv.getInt32(r + 36, true)
-    const dt = dv.getUint32(r + 56, true), n = dv.getUint32(r + 60, true)
+  let cur = root, key = null
+  while (o < end) {
+    const tag = log[o++]
     switch (tag) {
-      case PR.ACTOR: actors.push(toHex(heap.subarray(i64(r + 40), i64(r + 40) + i64(r + 48)))); break
-      case PR.CLOCK: clock[actors[a1]] = index; break
+      case PR.ACTOR: actors.push(toHex(raw(u()))); break
+      case PR.CLOCK: { const a = u(); clock[actors[a]] = u(); break }
       // getPatch logs announce an object in its parent first; applyChanges logs list object
       // patches in objectMeta order, so a section may create its node
-      case PR.OBJ: cur = a1 < 0 ? root : node(c1, a1, dt); break
-      case PR.KEY: key = utf8.decode(heap.subarray(i64(r + 40), i64(r + 40) + i64(r + 48))); cur.props[key] = {}; break
-      case PR.PROP: cur.props[key][opid(c2, a2)] = value(vtag, dt, r + 40); break
-      case PR.INSERT:
-        cur.edits.push({action: 'insert', index, elemId: opid(c1, a1), opId: opid(c2, a2), value: value(vtag, dt, r + 40)})
+      case PR.OBJ: { const c = s(), a = s(), t = u(); cur = a < 0 ? root : node(c, a, t); break }
+      case PR.KEY: key = utf8.decode(raw(u())); cur.props[key] = {}; break
+      case PR.PROP: { const c = u(), a = u(); cur.props[key][opid(c, a)] = value(); break }
+      case PR.INSERT: {
+        const index = u(), ec = u(), ea = u(), oc = u(), oa = u()
+        cur.edits.push({action: 'insert', index, elemId: opid(ec, ea), opId: opid(oc, oa), value: value()})
         break
+      }
       case PR.MULTI: {
-        const e = {action: 'multi-insert', index, elemId: opid(c1, a1)}
+        const index = u(), ec = u(), ea = u(), dt = u(), n = u()
+        const e = {action: 'multi-insert', index, elemId: opid(ec, ea)}
         if (dt) e.datatype = dt < 100 ? NAMED_DT[PV.UINT + dt - 1] : dt - 100
         e.values = []
-        for (let q = 0; q < n; q++, mv++) {
-          const vo = valAt(mv)
-          e.values.push(prim(dv.getUint32(vo, true), dv.getUint32(vo + 4, true), vo + 8))
-        }
+        for (let q = 0; q < n; q++) e.values.push(prim()[2])
         cur.edits.push(e)
         break
       }
-      case PR.UPDATE: cur.edits.push({action: 'update', index, opId: opid(c2, a2), value: value(vtag, dt, r + 40)}); break
-      case PR.REMOVE: cur.edits.push({action: 'remove', index, count: n}); break
+      case PR.UPDATE: { const index = u(), oc = u(), oa = u(); cur.edits.push({action: 'update', index, opId: opid(oc, oa), value: value()}); break }
+      case PR.REMOVE: { const index = u(); cur.edits.push({action: 'remove', index, count: u()}); break }
+      default: throw new RangeError(`automerge_amd: bad patch record tag ${tag}`)
     }
   }
   return {maxOp, clock, deps, pendingChanges, diffs: root}

@@ -15,7 +15,7 @@ const cases = JSON.parse(fs.readFileSync(process.argv[2]))
 const bad = []
 cases.forEach((c, i) => {
   const log = Uint8Array.from(Buffer.from(c.log, 'hex'))
-  const maxOp = Number(Buffer.from(c.log, 'hex').readBigInt64LE(48))
+  const maxOp = Number(Buffer.from(c.log, 'hex').readBigInt64LE(24))
   const got = B._materializePatch(log, c.deps, c.pending, maxOp)
   if (JSON.stringify(canon(got)) !== JSON.stringify(canon(c.expect))) bad.push(i)
 })

@@ -97,15 +97,12 @@ int main(int argc, char** argv) {
                       (uint32_t)nsucc + 1};
     int64_t max_op = 0;
     patch_scan(src, o, w, max_op);
-    PatchHdr h = {};
-    h.status = o.status; h.arg0 = o.arg0; h.arg1 = o.arg1;
-    h.nrec = o.nrec; h.nmval = o.nmval; h.nheap = o.nheap; h.max_op = max_op;
-    const uint32_t total = (uint32_t)(sizeof h + o.nrec * sizeof(PatchRec) + o.nmval * sizeof(PatchVal) + o.nheap);
+    // the wire form the device hands to the host (am_patch.h patch_pack)
+    std::vector<uint8_t> wire(64 + 64 * rec.size() + 32 * mval.size() + hp.size());
+    const uint32_t total = (uint32_t)patch_pack(o, max_op, wire.data(), wire.size());
+    if (!total) return 5;
     std::fwrite(&total, 4, 1, out);
-    std::fwrite(&h, sizeof h, 1, out);
-    std::fwrite(rec.data(), sizeof(PatchRec), o.nrec, out);
-    std::fwrite(mval.data(), sizeof(PatchVal), o.nmval, out);
-    std::fwrite(hp.data(), 1, o.nheap, out);
+    std::fwrite(wire.data(), 1, total, out);
     oc_export_free(e);
   }
   std::fclose(out);

@@ -108,3 +108,46 @@ def test_workload_apply_patch_matches_oracle(kind, first, n):
         assert int(r[i]["status"]) == 0, (i, int(r[i]["status"]))
         got = _jsonable(P.materialize(b.doc_patch(i), want["deps"], want["pendingChanges"], want["maxOp"]))
         assert got == want, i
+
+
+def test_fast_and_general_patch_writers_agree(docs):
+    """The wave-parallel patch writer of k_doc_fast (fast_diff, am_doc_fast.h) against k_doc's serial
+    replay (am_diff.h): every golden apply step and seeded C4 / C2 documents staged with WANT_DIFF,
+    once with the fast kernel and once without it (AM_FAST=0); the materialized patches must be
+    equal, and the fast writer must take every C4 document (the bench's shape)."""
+    import os
+    from automerge_amd import patch as P
+    from automerge_amd import workload
+    from automerge_amd.batch import WANT_DIFF, Batch
+    items = [(base, ch) for base, ch, _ in _steps(docs)]
+    nc4 = 600
+    for kind, first in (("c4", 11), ("c2", 7)):
+        arena, chunks, dd, _ = getattr(workload, kind)(first, nc4)
+        items += [workload.doc_chunks(arena, chunks, dd, i) for i in range(nc4)]
+
+    def run(fast):
+        old = os.environ.get("AM_FAST")
+        os.environ["AM_FAST"] = "1" if fast else "0"
+        try:
+            b = Batch()
+            b.stage_docs(items, flags=WANT_DIFF)
+        finally:
+            if old is None:
+                del os.environ["AM_FAST"]
+            else:
+                os.environ["AM_FAST"] = old
+        b.run()
+        b.sync()
+        r = b.results()
+        pats = [_jsonable(P.materialize(b.doc_patch(i), [], 0, 0)) if r[i]["status"] == 0 else None
+                for i in range(len(items))]
+        outs = [b.doc_output(i, r[i]) if r[i]["status"] == 0 else b"" for i in range(len(items))]
+        return r, pats, outs, b.fast_flags()
+
+    rf, pf, of, flags = run(True)
+    rg, pg, og, gflags = run(False)
+    assert not gflags.any()
+    assert flags[-2 * nc4:-nc4].all(), "every C4 document must take the fast patch writer"
+    bad = [i for i in range(len(items)) if pf[i] != pg[i] or of[i] != og[i] or rf[i]["status"] != rg[i]["status"]]
+    assert not bad, (int(flags.sum()), bad[:10])
+    print("fast patch writer took %d of %d documents" % (int(flags.sum()), len(items)))
