@@ -41,6 +41,16 @@ class DocResult(C.Structure):
                 ("ws_bytes", C.c_uint64)]
 
 
+class DocSummary(C.Structure):
+    _fields_ = [("status", C.c_uint32), ("nqueued", C.c_uint32), ("out_len", C.c_uint32), ("patch_len", C.c_uint32),
+                ("out_off", C.c_uint64), ("patch_off", C.c_uint64)]
+
+
+class PipeCaps(C.Structure):
+    _fields_ = [("arena_bytes", C.c_uint64), ("chunks", C.c_uint32), ("docs", C.c_uint32), ("ws_bytes", C.c_uint64),
+                ("out_bytes", C.c_uint64), ("patch_bytes", C.c_uint64), ("fast_lds", C.c_uint32), ("slots", C.c_uint32)]
+
+
 class Error(C.Structure):
     _fields_ = [("code", C.c_uint32), ("is_type_error", C.c_int32), ("message", C.c_char * 480)]
 
@@ -96,10 +106,14 @@ _sigs = {
     "am_stage_change": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
     "am_stage_document": (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t),
                                     C.POINTER(C.c_int), C.POINTER(Error)]),
-    "am_workload_c4": (C.c_uint64, [C.c_uint64, C.c_uint32, P, C.c_uint64, P, P, C.POINTER(C.c_uint64), C.c_int]),
-    "am_workload_c2": (C.c_uint64, [C.c_uint64, C.c_uint32, P, C.c_uint64, P, P, C.POINTER(C.c_uint64), C.c_int]),
-    "am_workload_text": (C.c_uint64, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P, C.c_uint64, P, P,
-                                      C.POINTER(C.c_uint64), C.c_int]),
+    "am_host_alloc": (P, [C.c_size_t]),
+    "am_host_free": (None, [P]),
+    "am_pipe_create": (P, [P, C.POINTER(PipeCaps), C.POINTER(Error)]),
+    "am_pipe_destroy": (None, [P]),
+    "am_pipe_submit": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, C.c_uint32, P, P, C.c_uint64, P, C.c_uint64,
+                                 C.POINTER(C.c_uint64), C.POINTER(Error)]),
+    "am_pipe_drain": (C.c_int, [P, P, C.c_uint32, C.POINTER(Error)]),
+    "am_pipe_times": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_uint32)]),
 }
 for _name, (_res, _args) in _sigs.items():
     _f = getattr(lib, _name)

@@ -4,8 +4,11 @@
 // op columns or merges operations. There is no CPU fallback: without a HIP device the entry points
 // fail with an error.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <zlib.h>
 
+#include <algorithm>
 #include <array>
 #include <cstdarg>
 #include <cstdio>
@@ -684,6 +687,304 @@ extern "C" int am_batch_kernel_info(am_batch* b, uint64_t* out3) {
   out3[0] = b->lds_bytes;
   out3[1] = b->fast_lds;
   out3[2] = b->max_hot_v;
+  return 0;
+}
+
+// =============================================================================================
+// pipelined batches (am_pipe_*): H2D of batch k+1 and D2H of batch k-1 overlap the kernels of k
+// =============================================================================================
+extern "C" void* am_host_alloc(size_t n) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, n ? n : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+extern "C" void am_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
+namespace {
+struct PipeSlot {
+  am_batch b;                                  // device inputs, workspace, results
+  DevBuf<uint64_t> olen, ooff, plen, poff, tmp, totals;
+  DevBuf<uint8_t> dout, dpatch;
+  DevBuf<am_doc_summary> summ;
+  uint64_t* h_totals = nullptr;                // pinned: the two arena sizes of the last run
+  hipEvent_t ev_c0 = nullptr, ev_d0 = nullptr, ev_d1 = nullptr, ev_comp = nullptr, ev_in = nullptr, ev_out = nullptr;
+  bool busy = false, finalized = false;
+  uint64_t ticket = 0;
+  am_doc_summary* h_summ = nullptr;
+  uint8_t *h_out = nullptr, *h_patch = nullptr;
+  uint64_t h_out_cap = 0, h_patch_cap = 0;
+  hsa_signal_t home{};                         // SDMA copies home of the last batch (counts down to 0)
+  bool home_sdma = false;                      // the copies home went to the SDMA engines
+};
+}  // namespace
+
+struct am_pipe {
+  am_engine* eng = nullptr;
+  hipStream_t s_in = nullptr, s_c = nullptr, s_out = nullptr;
+  am_pipe_caps caps{};
+  std::vector<PipeSlot*> slots;
+  uint64_t next = 0;                           // ticket of the next submission
+  std::vector<uint64_t> totals;                // per finalized batch since the last drain: out, patch bytes
+  float ms_comp = 0.f, ms_doc = 0.f;           // kernel times of the drained batches
+  uint32_t nms = 0;
+};
+
+static void pipe_free(am_pipe* p) {
+  if (!p) return;
+  set_device(p->eng);
+  for (PipeSlot* sl : p->slots) {
+    for (hipEvent_t e : {sl->ev_c0, sl->ev_d0, sl->ev_d1, sl->ev_comp, sl->ev_in, sl->ev_out})
+      if (e) (void)hipEventDestroy(e);
+    if (sl->h_totals) (void)hipHostFree(sl->h_totals);
+    if (sl->home.handle) (void)hsa_signal_destroy(sl->home);
+    delete sl;
+  }
+  for (hipStream_t s : {p->s_in, p->s_c, p->s_out})
+    if (s) (void)hipStreamDestroy(s);
+  delete p;
+}
+
+extern "C" void am_pipe_destroy(am_pipe* p) {
+  if (!p) return;
+  set_device(p->eng);
+  (void)hipDeviceSynchronize();
+  pipe_free(p);
+}
+
+extern "C" am_pipe* am_pipe_create(am_engine* eng, const am_pipe_caps* caps, am_error* err) {
+  auto fail = [&](am_pipe* p, const char* m) -> am_pipe* {
+    to_c(Err{AM_U_CAPACITY, false, m}, err);
+    pipe_free(p);
+    return nullptr;
+  };
+  if (!eng || !caps || caps->slots < 2 || !caps->docs) return fail(nullptr, "automerge_amd: bad pipeline capacities");
+  if (!set_device(eng)) return fail(nullptr, "automerge_amd: no device");
+  am_pipe* p = new am_pipe();
+  p->eng = eng;
+  p->caps = *caps;
+  for (hipStream_t* s : {&p->s_in, &p->s_c, &p->s_out})
+    if (hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess) return fail(p, "automerge_amd: cannot create a HIP stream");
+  const am_pipe_caps& c = *caps;
+  for (uint32_t k = 0; k < c.slots; k++) {
+    PipeSlot* sl = new PipeSlot();
+    p->slots.push_back(sl);
+    am_batch& b = sl->b;
+    b.eng = eng;
+    const bool ok =
+        b.arena.ensure(c.arena_bytes + 64) && b.chunks.ensure(c.chunks) && b.docs.ensure(c.docs) && b.known.ensure(1) &&
+        b.info.ensure(c.chunks) && b.hdr.ensure(c.chunks) && b.bounds.ensure(c.docs) && b.ws_bytes.ensure(c.docs) &&
+        b.ws_off.ensure(c.docs) && b.scan_tmp.ensure(am_scan_tmp_elems(c.docs)) && b.ws_total.ensure(1) &&
+        b.max_hot.ensure(2) && b.fast_done.ensure(c.docs) && b.results.ensure(c.docs) && b.chg_state.ensure(c.chunks) &&
+        b.ws.ensure(c.ws_bytes + 16) && sl->olen.ensure(c.docs) && sl->ooff.ensure(c.docs) && sl->plen.ensure(c.docs) &&
+        sl->poff.ensure(c.docs) && sl->tmp.ensure(am_scan_tmp_elems(c.docs)) && sl->totals.ensure(2) &&
+        sl->dout.ensure(c.out_bytes + 16) && sl->dpatch.ensure(c.patch_bytes + 16) && sl->summ.ensure(c.docs);
+    if (!ok) return fail(p, "automerge_amd: device allocation failed (pipeline capacities too large)");
+    if (hipHostMalloc(reinterpret_cast<void**>(&sl->h_totals), 2 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess)
+      return fail(p, "automerge_amd: pinned allocation failed");
+    for (hipEvent_t* e : {&sl->ev_c0, &sl->ev_d0, &sl->ev_d1, &sl->ev_comp, &sl->ev_in, &sl->ev_out})
+      if (hipEventCreate(e) != hipSuccess) return fail(p, "automerge_amd: cannot create a HIP event");
+    if (hsa_signal_create(0, 0, nullptr, &sl->home) != HSA_STATUS_SUCCESS) sl->home.handle = 0;
+    b.lds_bytes = AM_LDS_BUDGET;       // k_doc takes what k_doc_fast leaves, in either mode
+    b.max_hot_v = ~0ull;
+    b.fast_lds = c.fast_lds;
+  }
+  if (err) err->code = 0;
+  return p;
+}
+
+// the D2H copies of a batch whose kernels have been enqueued: waits for its compute chain, then
+// queues the copies of its summaries and arenas on the output stream
+// The agent that owns an allocation (ROCr's pointer info); false for memory ROCr does not know
+// (pageable host memory)
+static bool hsa_owner(const void* ptr, hsa_agent_t& agent) {
+  hsa_amd_pointer_info_t info;
+  std::memset(&info, 0, sizeof info);
+  info.size = sizeof info;
+  if (!ptr || hsa_amd_pointer_info(ptr, &info, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS) return false;
+  if (info.type == HSA_EXT_POINTER_TYPE_UNKNOWN) return false;
+  agent = info.agentOwner;
+  return true;
+}
+// device view of a caller buffer in mapped pinned host memory (am_host_alloc), or null
+static void* mapped(void* host) {
+  void* d = nullptr;
+  if (!host || hipHostGetDevicePointer(&d, host, 0) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+  return d;
+}
+
+// Queues the copies home of a batch whose kernels have been enqueued, once its compute chain is
+// done (the host needs the arena sizes). The copies go to the SDMA engines when the destinations
+// are pinned: a device-to-host copy issued from the CUs (the runtime's blit kernel, or our own)
+// keeps the L2's path to the host full for as long as the link is busy, and the next batch's
+// kernels then wait on their own memory traffic (k_chunks ran 6x slower under it).
+static bool pipe_finalize(am_pipe* p, PipeSlot* sl) {
+  if (sl->finalized) return true;
+  if (hipEventSynchronize(sl->ev_comp) != hipSuccess) return false;
+  const uint64_t to = sl->h_totals[0], tp = sl->h_totals[1];
+  const uint32_t nd = sl->b.ndocs;
+  const uint64_t ns = sizeof(am_doc_summary) * (uint64_t)nd;
+  const uint64_t no = std::min<uint64_t>(std::min<uint64_t>(to, p->caps.out_bytes), sl->h_out_cap);
+  const uint64_t np = std::min<uint64_t>(std::min<uint64_t>(tp, p->caps.patch_bytes), sl->h_patch_cap);
+  struct { void* dst; const void* src; uint64_t n; } cp[3] = {{sl->h_summ, sl->summ.p, ns}, {sl->h_out, sl->dout.p, no},
+                                                             {sl->h_patch, sl->dpatch.p, np}};
+  hsa_agent_t gpu, host;
+  bool sdma = sl->home.handle && hsa_owner(sl->summ.p, gpu);
+  for (auto& c : cp) sdma = sdma && (!c.n || hsa_owner(c.dst, host));
+  sl->home_sdma = false;
+  if (sdma) {
+    uint32_t n = 0;
+    for (auto& c : cp) n += c.n ? 1 : 0;
+    hsa_signal_store_screlease(sl->home, n);
+    for (auto& c : cp) {
+      if (!c.n) continue;
+      if (hsa_amd_memory_async_copy(c.dst, host, c.src, gpu, c.n, 0, nullptr, sl->home) != HSA_STATUS_SUCCESS) {
+        hsa_signal_subtract_screlease(sl->home, 1);  // this one is not in flight
+        sdma = false;
+      }
+    }
+    sl->home_sdma = true;
+    if (!sdma) {  // a copy was refused: wait for the others, then copy everything the HIP way
+      hsa_signal_wait_scacquire(sl->home, HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+      sl->home_sdma = false;
+    }
+  }
+  if (!sl->home_sdma) {
+    void *ds = mapped(sl->h_summ), *dout = mapped(sl->h_out), *dpat = mapped(sl->h_patch);
+    if (ds && (dout || !no) && (dpat || !np) && no % 16 == 0 && np % 16 == 0) {
+      am_launch_copy_home(sl->summ.p, ds, ns, sl->dout.p, dout, no, sl->dpatch.p, dpat, np, 64, p->s_out);
+    } else {
+      for (auto& c : cp)
+        if (c.n && hipMemcpyAsync(c.dst, c.src, c.n, hipMemcpyDeviceToHost, p->s_out) != hipSuccess) return false;
+    }
+    if (hipEventRecord(sl->ev_out, p->s_out) != hipSuccess) return false;
+  }
+  p->totals.push_back(to);
+  p->totals.push_back(tp);
+  sl->finalized = true;
+  return true;
+}
+
+// the copies home of a finalized batch are complete (host wait)
+static bool pipe_wait_home(PipeSlot* sl) {
+  if (sl->home_sdma) {
+    hsa_signal_wait_scacquire(sl->home, HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+    sl->home_sdma = false;
+    return true;
+  }
+  return hipEventSynchronize(sl->ev_out) == hipSuccess;
+}
+
+// A slot reused by a new batch: the previous batch's copies home are queued (finalize) and its
+// kernel times are read (its compute chain is complete); the new batch's H2D waits for that compute
+// chain on the device and its kernels wait for the copies home -- no host wait on the copies.
+// wait_home: the host also waits for the copies (drain).
+static bool pipe_retire(am_pipe* p, PipeSlot* sl, bool wait_home) {
+  if (!sl->busy) return true;
+  if (!pipe_finalize(p, sl)) return false;
+  float a = 0.f, d = 0.f;
+  (void)hipEventElapsedTime(&a, sl->ev_c0, sl->ev_comp);
+  (void)hipEventElapsedTime(&d, sl->ev_d0, sl->ev_d1);
+  p->ms_comp += a;
+  p->ms_doc += d;
+  p->nms++;
+  if (wait_home || sl->home_sdma) {
+    // SDMA copies are not ordered with the HIP streams: the host waits before the slot is reused
+    if (!pipe_wait_home(sl)) return false;
+  } else if (hipStreamWaitEvent(p->s_c, sl->ev_out, 0) != hipSuccess) {
+    return false;
+  }
+  if (hipStreamWaitEvent(p->s_in, sl->ev_comp, 0) != hipSuccess) return false;
+  sl->busy = false;
+  return true;
+}
+
+extern "C" int am_pipe_submit(am_pipe* p, const uint8_t* arena, uint64_t arena_len, const am_chunk_desc* chunks,
+                              uint32_t nchunks, const am_doc_desc* docs, uint32_t ndocs, am_doc_summary* summary,
+                              uint8_t* out, uint64_t out_cap, uint8_t* patches, uint64_t patch_cap, uint64_t* ticket,
+                              am_error* err) {
+  auto fail = [&](const char* m) { to_c(Err{AM_U_CAPACITY, false, m}, err); return 1; };
+  if (!set_device(p->eng)) return fail("automerge_amd: no device");
+  const am_pipe_caps& c = p->caps;
+  if (arena_len > c.arena_bytes || nchunks > c.chunks || ndocs > c.docs)
+    return fail("automerge_amd: batch exceeds the pipeline capacities");
+  PipeSlot* sl = p->slots[p->next % p->slots.size()];
+  if (!pipe_retire(p, sl, false)) return fail("automerge_amd: HIP error while retiring a batch");
+  am_batch& b = sl->b;
+  b.nchunks = nchunks;
+  b.ndocs = ndocs;
+  b.any_diff = false;
+  for (uint32_t d = 0; d < ndocs && !b.any_diff; d++) b.any_diff = (docs[d].flags & AM_DOC_WANT_DIFF) != 0;
+  // inputs
+  if (arena_len && hipMemcpyAsync(b.arena.p, arena, arena_len, hipMemcpyHostToDevice, p->s_in) != hipSuccess) return fail("automerge_amd: H2D failed");
+  if (nchunks && hipMemcpyAsync(b.chunks.p, chunks, sizeof(am_chunk_desc) * nchunks, hipMemcpyHostToDevice, p->s_in) != hipSuccess)
+    return fail("automerge_amd: H2D failed");
+  if (ndocs && hipMemcpyAsync(b.docs.p, docs, sizeof(am_doc_desc) * ndocs, hipMemcpyHostToDevice, p->s_in) != hipSuccess)
+    return fail("automerge_amd: H2D failed");
+  if (hipEventRecord(sl->ev_in, p->s_in) != hipSuccess || hipStreamWaitEvent(p->s_c, sl->ev_in, 0) != hipSuccess)
+    return fail("automerge_amd: stream ordering failed");
+  // the whole chain on the compute stream; no host round trip
+  BatchDev d = b.dev();
+  d.ws_cap = c.ws_bytes;
+  hipStream_t s = p->s_c;
+  (void)hipEventRecord(sl->ev_c0, s);
+  am_launch_chunks(d, s);
+  am_launch_bounds(d, s);
+  (void)hipEventRecord(sl->ev_d0, s);
+  am_launch_doc(d, s);
+  (void)hipEventRecord(sl->ev_d1, s);
+  am_launch_out_hash(d, s);
+  am_launch_pipe_compact(d, sl->olen.p, sl->ooff.p, sl->plen.p, sl->poff.p, sl->tmp.p, sl->totals.p, sl->dout.p, c.out_bytes,
+                         sl->dpatch.p, c.patch_bytes, sl->summ.p, s);
+  if (hipMemcpyAsync(sl->h_totals, sl->totals.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s) != hipSuccess)
+    return fail("automerge_amd: D2H failed");
+  if (hipEventRecord(sl->ev_comp, s) != hipSuccess || hipGetLastError() != hipSuccess) return fail("automerge_amd: kernel launch failed");
+  sl->busy = true;
+  sl->finalized = false;
+  sl->ticket = p->next;
+  sl->h_summ = summary;
+  sl->h_out = out;
+  sl->h_out_cap = out_cap;
+  sl->h_patch = patches;
+  sl->h_patch_cap = patch_cap;
+  if (ticket) *ticket = p->next;
+  // the previous batch: its kernels are ahead of ours on the compute stream; queue its copies home
+  if (p->next > 0) {
+    PipeSlot* prev = p->slots[(p->next - 1) % p->slots.size()];
+    if (prev->busy && !pipe_finalize(p, prev)) return fail("automerge_amd: HIP error while finishing a batch");
+  }
+  p->next++;
+  if (err) err->code = 0;
+  return 0;
+}
+
+extern "C" int am_pipe_drain(am_pipe* p, uint64_t* totals, uint32_t cap, am_error* err) {
+  if (!set_device(p->eng)) { to_c(Err{AM_U_CAPACITY, false, "automerge_amd: no device"}, err); return 1; }
+  const size_t S = p->slots.size();
+  // in submission order
+  for (uint64_t t = p->next >= S ? p->next - S : 0; t < p->next; t++) {
+    PipeSlot* sl = p->slots[t % S];
+    if (sl->busy && sl->ticket == t && !pipe_retire(p, sl, true)) {
+      to_c(Err{AM_U_CAPACITY, false, "automerge_amd: HIP error while draining the pipeline"}, err);
+      return 1;
+    }
+  }
+  for (uint32_t i = 0; totals && i < cap && 2 * i + 1 < p->totals.size(); i++) {
+    totals[2 * i] = p->totals[2 * i];
+    totals[2 * i + 1] = p->totals[2 * i + 1];
+  }
+  p->totals.clear();
+  if (err) err->code = 0;
+  return 0;
+}
+
+extern "C" int am_pipe_times(am_pipe* p, float* ms2, uint32_t* n) {
+  ms2[0] = p->ms_comp;
+  ms2[1] = p->ms_doc;
+  *n = p->nms;
+  p->ms_comp = p->ms_doc = 0.f;  // reset on read
+  p->nms = 0;
   return 0;
 }
 

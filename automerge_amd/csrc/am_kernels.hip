@@ -667,6 +667,108 @@ void am_launch_sha256(const uint8_t* arena, const am_chunk_desc* msgs, uint32_t 
   hipLaunchKernelGGL(k_sha256, dim3((n + 255) / 256), dim3(256), 0, s, arena, msgs, n, out);
 }
 
+// ------------------------------------------------------------------------------------------
+// Pipelined batches (am_pipe_*, am_capi.hip): the merged documents and patch logs of a batch are
+// gathered into two dense arenas (16-byte slots) so that one D2H copy each brings them home.
+// ------------------------------------------------------------------------------------------
+void am_launch_scan(const uint64_t* in, uint64_t* out, uint64_t* tmp, uint32_t n, uint64_t* total, hipStream_t s) {
+  if (!n) { (void)hipMemsetAsync(total, 0, sizeof(uint64_t), s); return; }
+  const uint32_t nblk = (n + SCAN_T - 1) / SCAN_T;
+  hipLaunchKernelGGL(k_scan_blocks, dim3(nblk), dim3(SCAN_T), 0, s, in, out, tmp, n);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, tmp, nblk, total);
+  hipLaunchKernelGGL(k_scan_add, dim3(nblk), dim3(SCAN_T), 0, s, out, tmp, n);
+}
+// per document: 16-byte-rounded lengths of its merged chunk and of its patch log (wire form)
+__global__ void __launch_bounds__(256) k_pipe_lens(const am_doc_result* __restrict__ res, const DocBounds* __restrict__ bounds,
+                                                   const uint8_t* __restrict__ ws, uint32_t ndocs, uint64_t* __restrict__ olen,
+                                                   uint64_t* __restrict__ plen) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= ndocs) return;
+  const am_doc_result r = res[d];
+  uint64_t o = 0, p = 0;
+  if (!r.status) {
+    o = (r.out_len + 15) & ~15ull;
+    const DocBounds b = bounds[d];
+    if (b.P) {
+      const WsLayout L = ws_layout(b);
+      const PatchHdr2* h = reinterpret_cast<const PatchHdr2*>(ws + r.ws_off + L.pwire);
+      if (h->magic == AM_PATCH_MAGIC && sizeof(PatchHdr2) + h->nbytes <= L.pwire_cap)
+        p = (sizeof(PatchHdr2) + h->nbytes + 15) & ~15ull;
+    }
+  }
+  olen[d] = o;
+  plen[d] = p;
+}
+// one wave per document: 16-byte copies of its chunk and its log into the dense arenas, and its
+// summary (documents whose slot does not fit the arenas report AM_U_CAPACITY)
+__global__ void __launch_bounds__(256) k_pipe_compact(const am_doc_result* __restrict__ res, const DocBounds* __restrict__ bounds,
+                                                      const uint8_t* __restrict__ ws, uint32_t ndocs,
+                                                      const uint64_t* __restrict__ olen, const uint64_t* __restrict__ ooff,
+                                                      const uint64_t* __restrict__ plen, const uint64_t* __restrict__ poff,
+                                                      uint8_t* __restrict__ dout, uint64_t out_cap, uint8_t* __restrict__ dpatch,
+                                                      uint64_t patch_cap, am_doc_summary* __restrict__ summary) {
+  const uint32_t d = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  if (d >= ndocs) return;
+  const am_doc_result r = res[d];
+  const uint64_t on = olen[d], oo = ooff[d], pn = plen[d], po = poff[d];
+  const bool ofit = oo + on <= out_cap, pfit = po + pn <= patch_cap;
+  if (on && ofit) {
+    const uint4* src = reinterpret_cast<const uint4*>(ws + r.out_off);
+    uint4* dst = reinterpret_cast<uint4*>(dout + oo);
+    for (uint64_t q = l; q < on / 16; q += 64) dst[q] = src[q];
+  }
+  if (pn && pfit) {
+    const WsLayout L = ws_layout(bounds[d]);
+    const uint4* src = reinterpret_cast<const uint4*>(ws + r.ws_off + L.pwire);
+    uint4* dst = reinterpret_cast<uint4*>(dpatch + po);
+    for (uint64_t q = l; q < pn / 16; q += 64) dst[q] = src[q];
+  }
+  if (l == 0) {
+    am_doc_summary sm;
+    sm.status = (!ofit || !pfit) && !r.status ? (uint32_t)AM_U_CAPACITY : r.status;
+    sm.nqueued = r.nqueued;
+    sm.out_len = sm.status ? 0u : (uint32_t)r.out_len;
+    uint32_t pl = 0;
+    if (!sm.status && pn) {
+      const WsLayout L = ws_layout(bounds[d]);
+      pl = (uint32_t)(sizeof(PatchHdr2) + reinterpret_cast<const PatchHdr2*>(ws + r.ws_off + L.pwire)->nbytes);
+    }
+    sm.patch_len = pl;
+    sm.out_off = oo;
+    sm.patch_off = po;
+    summary[d] = sm;
+  }
+}
+void am_launch_pipe_compact(const BatchDev& b, uint64_t* olen, uint64_t* ooff, uint64_t* plen, uint64_t* poff, uint64_t* tmp,
+                            uint64_t* totals, uint8_t* dout, uint64_t out_cap, uint8_t* dpatch, uint64_t patch_cap,
+                            am_doc_summary* summary, hipStream_t s) {
+  if (!b.ndocs) { (void)hipMemsetAsync(totals, 0, 2 * sizeof(uint64_t), s); return; }
+  hipLaunchKernelGGL(k_pipe_lens, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, b.results, b.bounds, b.ws, b.ndocs, olen, plen);
+  am_launch_scan(olen, ooff, tmp, b.ndocs, totals, s);
+  am_launch_scan(plen, poff, tmp, b.ndocs, totals + 1, s);
+  hipLaunchKernelGGL(k_pipe_compact, dim3((b.ndocs + 3) / 4), dim3(256), 0, s, b.results, b.bounds, b.ws, b.ndocs, olen, ooff,
+                     plen, poff, dout, out_cap, dpatch, patch_cap, summary);
+}
+
+// Copies home over the host link, written by a kernel of a few workgroups straight into mapped
+// pinned host memory: the runtime's own device-to-host path runs as a full-width blit kernel that
+// would take the CUs from the next batch's kernels for as long as the link is busy.
+struct CopySeg { const uint4* src; uint4* dst; uint64_t n16; };
+__global__ void __launch_bounds__(256) k_copy_home(CopySeg a, CopySeg b, CopySeg c) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t i = t; i < a.n16; i += stride) a.dst[i] = a.src[i];
+  for (uint64_t i = t; i < b.n16; i += stride) b.dst[i] = b.src[i];
+  for (uint64_t i = t; i < c.n16; i += stride) c.dst[i] = c.src[i];
+}
+void am_launch_copy_home(const void* s0, void* d0, uint64_t n0, const void* s1, void* d1, uint64_t n1, const void* s2, void* d2,
+                         uint64_t n2, uint32_t wgs, hipStream_t s) {
+  CopySeg a{reinterpret_cast<const uint4*>(s0), reinterpret_cast<uint4*>(d0), n0 / 16};
+  CopySeg b{reinterpret_cast<const uint4*>(s1), reinterpret_cast<uint4*>(d1), n1 / 16};
+  CopySeg c{reinterpret_cast<const uint4*>(s2), reinterpret_cast<uint4*>(d2), n2 / 16};
+  hipLaunchKernelGGL(k_copy_home, dim3(wgs), dim3(256), 0, s, a, b, c);
+}
+
 // Self-test of the DPP / permlane primitives (am_wave.h) on the device: one wave, the lane values
 // in[64] -> 16 result rows of 64 lanes (tests/test_gpu_wave.py checks them against numpy)
 __global__ void __launch_bounds__(64) k_wave_selftest(const uint64_t* __restrict__ in, uint64_t* __restrict__ out) {

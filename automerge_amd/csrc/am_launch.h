@@ -38,6 +38,16 @@ void am_launch_out_hash(const BatchDev& b, hipStream_t s);
 void am_launch_digest(const BatchDev& b, uint64_t first, uint64_t* d_out, hipStream_t s);
 void am_launch_sha256(const uint8_t* arena, const am_chunk_desc* msgs, uint32_t n, uint8_t* out, hipStream_t s);
 size_t am_scan_tmp_elems(uint32_t n);
+void am_launch_scan(const uint64_t* in, uint64_t* out, uint64_t* tmp, uint32_t n, uint64_t* total, hipStream_t s);
+// pipelined batches: dense arenas of merged documents / patch logs + per-document summaries;
+// totals[0..1] = bytes of the two arenas
+void am_launch_pipe_compact(const BatchDev& b, uint64_t* olen, uint64_t* ooff, uint64_t* plen, uint64_t* poff, uint64_t* tmp,
+                            uint64_t* totals, uint8_t* dout, uint64_t out_cap, uint8_t* dpatch, uint64_t patch_cap,
+                            am_doc_summary* summary, hipStream_t s);
+// 16-byte copies of three segments (sizes multiples of 16) by a grid of `wgs` workgroups; the
+// destinations are device pointers of mapped pinned host memory
+void am_launch_copy_home(const void* s0, void* d0, uint64_t n0, const void* s1, void* d1, uint64_t n1, const void* s2, void* d2,
+                         uint64_t n2, uint32_t wgs, hipStream_t s);
 // DEFLATE of compressed change chunks (am_inflate.hip): pass 1 sizes, pass 2 writes the new arena
 void am_launch_inflate_size(const uint8_t* arena, const am_chunk_desc* chunks, const uint32_t* zidx, uint32_t nz,
                             uint32_t* zlen, hipStream_t s);

@@ -1,0 +1,103 @@
+"""Pipelined batches (am_pipe_* in include/automerge_amd.h): a stream of batches of documents, each
+Backend.load + Backend.applyChanges per document, from host memory back to host memory. The H2D
+copy of the next batch and the D2H copy of the previous one overlap the kernels of the current one.
+
+    caps = pipe.caps_for(batch_staged_with_Batch, docs=..., ...)   # sizes from a representative batch
+    p = Pipeline(caps)
+    for arena, chunks, docs in batches:                            # pinned inputs (pinned())
+        p.submit(arena, chunks, docs, summary, out, patches)       # pinned outputs
+    totals = p.drain()                                             # every batch is home
+
+Each document's merged chunk is out[s.out_off : s.out_off + s.out_len] and its patch log (wire form,
+automerge_amd/patch.py) patches[s.patch_off : s.patch_off + s.patch_len] for its summary s.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _native as N
+from .batch import CHUNK_DT, DOC_DT
+
+SUMMARY_DT = np.dtype([("status", "<u4"), ("nqueued", "<u4"), ("out_len", "<u4"), ("patch_len", "<u4"),
+                       ("out_off", "<u8"), ("patch_off", "<u8")])
+assert SUMMARY_DT.itemsize == C.sizeof(N.DocSummary)
+
+
+class Pinned:
+    """A numpy view of pinned host memory (am_host_alloc)."""
+
+    def __init__(self, nbytes):
+        self.nbytes = max(int(nbytes), 1)
+        self.ptr = N.lib.am_host_alloc(self.nbytes)
+        if not self.ptr:
+            raise MemoryError("automerge_amd: pinned allocation of %d bytes failed" % self.nbytes)
+        self.u8 = np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def view(self, dtype, count=None, offset=0):
+        dtype = np.dtype(dtype)
+        if count is None:
+            count = (self.nbytes - offset) // dtype.itemsize
+        return self.u8[offset:offset + count * dtype.itemsize].view(dtype)
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            N.lib.am_host_free(self.ptr)
+            self.ptr = None
+
+
+def pinned_copy(arr):
+    """A Pinned buffer holding a copy of a numpy array; `.arr` is the copy (keep the buffer alive)."""
+    arr = np.ascontiguousarray(arr)
+    p = Pinned(arr.nbytes)
+    p.arr = p.view(arr.dtype, arr.size).reshape(arr.shape)
+    p.arr[...] = arr
+    return p
+
+
+class Pipeline:
+    def __init__(self, arena_bytes, chunks, docs, ws_bytes, out_bytes, patch_bytes, fast_lds, slots=3, device=0):
+        self._eng = N.engine(device)
+        self.caps = N.PipeCaps(int(arena_bytes), int(chunks), int(docs), int(ws_bytes), int(out_bytes), int(patch_bytes),
+                               int(fast_lds), int(slots))
+        err = N.Error()
+        self._p = N.lib.am_pipe_create(self._eng, C.byref(self.caps), C.byref(err))
+        if not self._p:
+            N.raise_for(err)
+        self._keep = {}
+
+    def __del__(self):
+        if getattr(self, "_p", None):
+            N.lib.am_pipe_destroy(self._p)
+            self._p = None
+
+    def submit(self, arena, chunks, docs, summary, out, patches):
+        """Enqueues one batch. All arrays should be pinned (pinned_copy / Pinned views) and must stay
+        alive until drain()."""
+        assert chunks.dtype == CHUNK_DT and docs.dtype == DOC_DT and summary.dtype == SUMMARY_DT
+        assert len(summary) >= len(docs)
+        t = C.c_uint64()
+        err = N.Error()
+        if N.lib.am_pipe_submit(self._p, arena.ctypes.data, arena.nbytes, chunks.ctypes.data, len(chunks), docs.ctypes.data,
+                                len(docs), summary.ctypes.data, out.ctypes.data, out.nbytes, patches.ctypes.data,
+                                patches.nbytes, C.byref(t), C.byref(err)):
+            N.raise_for(err)
+        self._keep[t.value] = (arena, chunks, docs, summary, out, patches)
+        return t.value
+
+    def drain(self, nbatches=0):
+        """Waits for every submitted batch; returns [(output bytes, patch bytes)] of the batches
+        finalized since the last drain (in submission order)."""
+        cap = max(int(nbatches), len(self._keep), 1)
+        tot = (C.c_uint64 * (2 * cap))()
+        err = N.Error()
+        if N.lib.am_pipe_drain(self._p, tot, cap, C.byref(err)):
+            N.raise_for(err)
+        self._keep.clear()
+        return [(int(tot[2 * i]), int(tot[2 * i + 1])) for i in range(cap)]
+
+    def times(self):
+        """(ms of the compute chains, ms of the document kernels, batches) retired since the last call."""
+        ms = (C.c_float * 2)()
+        n = C.c_uint32()
+        N.lib.am_pipe_times(self._p, ms, C.byref(n))
+        return float(ms[0]), float(ms[1]), int(n.value)

@@ -1,7 +1,9 @@
 """Document sharding across ranks: one process per GPU, documents are
-independent, so rank r merges documents [r*D, (r+1)*D) with no collective on the data path.
-The only exchange is one all-gather of a small per-rank digest after the timed region (RCCL over
-xGMI on the GPU box; gloo in the CPU tests)."""
+independent, so there is no collective on the data path. The C4 job is sharded by document hash
+(rank = first byte of the SHA-256 of the base document chunk, i.e. its container checksum
+columnar.js:659-686, mod N: workload.c4_shard); shard_range is the plain range split other
+workloads use. The only exchange is one all-gather of a small per-rank digest after the timed
+region (RCCL over xGMI on the GPU box; gloo in the CPU tests)."""
 
 DIGEST_FIELDS = ("docs", "ops", "errors", "out_bytes", "out_digest")
 
@@ -32,6 +34,31 @@ def doc_digest(index, status, out):
     chk = int.from_bytes(out[4:8], "little") if status == 0 and len(out) >= 8 else 0
     n = len(out) if status == 0 else 0
     return (_mix64(((index << 32) | chk) & M64) + n * 0x9E3779B97F4A7C15 + status) & M64
+
+
+def shard_of(doc_bytes, world):
+    """Rank of a document (the base document chunk): SHA-256(chunk)[0] mod world, read from the
+    container checksum (bytes 4..8 of the chunk are the first four bytes of that hash)."""
+    return doc_bytes[4] % world
+
+
+def doc_digest_np(index, status, out_len, chk):
+    """doc_digest over arrays (numpy uint64, wrapping arithmetic); returns the combined digest."""
+    import numpy as np
+    index = np.asarray(index, np.uint64)
+    status = np.asarray(status, np.uint64)
+    ok = status == 0
+    chk = np.where(ok, np.asarray(chk, np.uint64), np.uint64(0))
+    n = np.where(ok, np.asarray(out_len, np.uint64), np.uint64(0))
+    with np.errstate(over="ignore"):
+        x = (index << np.uint64(32)) | chk
+        x ^= x >> np.uint64(30)
+        x *= np.uint64(0xBF58476D1CE4E5B9)
+        x ^= x >> np.uint64(27)
+        x *= np.uint64(0x94D049BB133111EB)
+        x ^= x >> np.uint64(31)
+        t = x + n * np.uint64(0x9E3779B97F4A7C15) + status
+        return int(t.sum(dtype=np.uint64)) & 0x7FFFFFFFFFFFFFFF
 
 
 def combine(terms):

@@ -1,14 +1,22 @@
 #!/usr/bin/env python3
 """bench.py -- batched load + applyChanges on MI355X (BASELINE.json metric), one process per GPU.
 
-Workload (per GPU): D documents; each is a saved base document (change 0:
-makeList 'items' + 'title') loaded and merged with 12 concurrent changes from 4 actors (4 list
-inserts + 1 conflicting title set each): 13 changes, 62 ops per document, ~600 B saved.
-A step = the whole GPU pipeline over all D documents with inputs resident in HBM: SHA-256 of every
-chunk, header parse, causal queue, column decode, merge (sort/RGA/succ), canonical re-encode and
-the checksum of every merged document. Weak scaling: rank r merges documents [r*D, (r+1)*D).
+Workload: the 1M-document job. Document i is a saved base document (change 0:
+makeList 'items' + 'title') that is loaded and merged with 12 concurrent changes from 4 actors (4
+list inserts + 1 conflicting title set each): 13 changes, 60 ops merged, ~2.1 KB of input and a
+~720 B merged document. Documents are sharded over the ranks by the first byte of their base
+document's SHA-256 (the container checksum) mod N, so N GPUs split the same job (strong scaling).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--docs D]
+A step is the whole job of a rank from host memory back to host memory, as a caller of the engine
+sees it: every batch of its shard goes through am_pipe_* (include/automerge_amd.h) -- H2D of the
+encoded chunks, SHA-256 of every chunk, header parse, causal queue, column decode, merge
+(sort / RGA / succ), canonical re-encode, checksum, the patch Backend.applyChanges returns (wire
+form of am_patch.h), compaction, and D2H of the merged documents, patches and per-document
+summaries. Copies of batch k+1 / k-1 overlap the kernels of batch k. Materializing the patches as
+JS objects is the host's job and is not timed here (it is reported separately by tools/).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--docs D] [--batch B] [--slots S]
+  python bench.py --mode resident [--workload c4|c2] --docs D   # inputs resident in HBM (kernels only)
 """
 import argparse
 import json
@@ -21,39 +29,15 @@ sys.path.insert(0, ROOT)
 
 METRIC = "ops merged/sec (batched load+applyChanges) + decode GB/s at 1/2/4/8 GPUs"
 HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic_k_doc.json")
-
-
-def kernel_source_digest():
-    """SHA-256 (16 hex) of the HIP sources the engine is built from."""
-    import glob
-    import hashlib
-    h = hashlib.sha256()
-    csrc = os.path.join(ROOT, "automerge_amd", "csrc")
-    for f in sorted(glob.glob(os.path.join(csrc, "*.h")) + glob.glob(os.path.join(csrc, "*.hip"))):
-        h.update(os.path.basename(f).encode())
-        h.update(open(f, "rb").read())
-    return h.hexdigest()[:16]
-
-
-def measured_traffic(kernel):
-    """roofline.traffic: HBM bytes per launch from the rocprofv3 FETCH_SIZE/WRITE_SIZE passes
-    (tools/gpu_prof.sh -> tools/traffic.py), only when they were measured on these exact sources."""
-    try:
-        rec = json.load(open(TRAFFIC_JSON))
-    except (OSError, ValueError):
-        return None
-    if rec.get("kernel") != kernel or rec.get("src_digest") != kernel_source_digest():
-        return None
-    return rec["traffic_bytes"]
+CPU_REF_JSON = os.path.join(ROOT, "profiles", "cpu_reference_node.json")
 
 
 def cpu_baseline(arena, chunks, docs, seconds=12.0, ops_per_doc=60, name="C4"):
     """The oracle (CPU restatement of the reference algorithm, oracle/) timed on one host core over
-    a bounded sample of the same documents: ops merged per second (load + applyChanges)."""
+    a bounded sample of the same documents: ops merged per second (load + applyChanges + save)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as O
-    from automerge_amd import workload
+    import workload
     n = 0
     ops = 0
     t0 = time.perf_counter()
@@ -65,25 +49,56 @@ def cpu_baseline(arena, chunks, docs, seconds=12.0, ops_per_doc=60, name="C4"):
         ops += ops_per_doc
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": ops / dt, "unit": "ops/s", "cores": 1, "kind": "port",
+    return {"value": ops / dt, "unit": "ops/s", "cores": 1, "kind": "port", "host_cpus": os.cpu_count(),
             "sample": "%d %s documents (load + applyChanges + save) by oracle/liboracle.so, 1 thread, %.1f s" % (n, name, dt)}
+
+
+def cpu_reference():
+    """The reference JS backend under Node (measured in the build container by
+    tools/cpu_reference.js, which cannot run on the GPU box): per core and on all cores."""
+    try:
+        return json.load(open(CPU_REF_JSON))
+    except (OSError, ValueError):
+        return None
+
+
+def split_batches(arena, chunks, docs, batch):
+    """Per-batch (arena slice, rebased chunk descriptors, rebased document descriptors)."""
+    import numpy as np
+    out = []
+    for lo in range(0, len(docs), batch):
+        d = docs[lo:lo + batch].copy()
+        c0 = int(d["chg_begin"][0]) - (1 if d["base_chunk"][0] >= 0 else 0)
+        c1 = int(d["chg_begin"][-1] + d["chg_count"][-1])
+        c = chunks[c0:c1].copy()
+        a0 = int(c["off"][0])
+        a1 = int(c["off"][-1] + c["len"][-1])
+        c["off"] -= a0
+        d["chg_begin"] -= c0
+        d["base_chunk"] = np.where(d["base_chunk"] >= 0, d["base_chunk"] - c0, -1)
+        out.append((arena[a0:a1], c, d))
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--docs", type=int, default=131072, help="documents per GPU (8 GPUs x 131072 = the 1M-doc C4 job)")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--docs", type=int, default=1 << 20, help="documents of the whole job (sharded over the ranks)")
+    ap.add_argument("--batch", type=int, default=0, help="documents per pipeline batch (0: auto)")
+    ap.add_argument("--slots", type=int, default=3, help="batches in flight")
+    ap.add_argument("--mode", choices=["pipe", "resident"], default="pipe")
+    ap.add_argument("--workload", choices=["c4", "c2"], default="c4")
+    ap.add_argument("--no-patch", action="store_true", help="merge without the applyChanges patch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", type=int, default=32, help="documents verified against the oracle (rank 0)")
-    ap.add_argument("--workload", choices=["c4", "c2"], default="c4",
-                    help="c4 (default, the metric's config) or c2 (configs[1]: 10k-doc-class map/counter docs)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
     import torch
     dist = None
     if world > 1:
@@ -91,97 +106,198 @@ def main():
         dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
 
-    from automerge_amd import shard, workload
-    from automerge_amd.batch import Batch
+    from automerge_amd import shard
+    from automerge_amd.batch import WANT_DIFF, Batch
+    import workload
 
-    first, D = shard.shard_range(rank, world, args.docs)
     t_gen = time.perf_counter()
-    arena, chunks, docs, ops_per_rank = getattr(workload, args.workload)(first, D)
+    if args.workload == "c4":
+        ids = workload.c4_shard(0, args.docs, world, rank)
+        arena, chunks, docs, ops_rank = workload.c4_list(ids)
+        per_doc = 60
+    else:
+        first, n = rank * (args.docs // world), args.docs // world
+        ids = np.arange(first, first + n, dtype=np.uint64)
+        arena, chunks, docs, ops_rank = workload.c2(first, n)
+        per_doc = 14
+    if not args.no_patch:
+        docs["flags"] |= WANT_DIFF
     t_gen = time.perf_counter() - t_gen
-    b = Batch(device=local)
-    b.stage(arena, chunks, docs)  # H2D once: inputs resident in HBM before timing
+    D = len(docs)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        b.run()
-    b.sync()
-    barrier()
-    torch.cuda.synchronize()
-    stage_ms = [0.0, 0.0, 0.0, 0.0]
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        b.run()
+    extra = {}
+    if args.mode == "resident":
+        # inputs resident in HBM: the kernel-only rate (no H2D / D2H in the timed region)
+        b = Batch(device=local)
+        b.stage(arena, chunks, docs)
+        for _ in range(args.warmup):
+            b.run()
         b.sync()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            b.run()
+            b.sync()
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
         st = b.stage_times()
-        for i in range(4):
-            stage_ms[i] += st[i]
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        res = b.results()
+        statuses = res["status"]
+        out_bytes = int(res["out_len"].sum())
+        patch_bytes = 0
+        t_doc = st[2]
+        in_b = int(arena.nbytes)
+        alg_launch = in_b + out_bytes
+        extra["stage_ms"] = dict(zip(["k_chunks", "k_bounds+scan", "k_doc", "k_out_hash"], st))
+        extra["fast_docs"] = int(b.fast_flags().sum())
+        digest = b.digest(0) if args.workload == "c2" else None
+        workspace = int(b.workspace_bytes())
 
-    res = b.results()
-    nerr = int((res["status"] != 0).sum())
-    out_bytes = int(res["out_len"].sum())
-    in_bytes = int(arena.nbytes)
-    # per-shard digest exchanged with one RCCL all-gather (never inside the timed region)
-    tot, _ = shard.exchange(dist, [D, ops_per_rank, nerr, out_bytes, b.digest(first)], "cuda")
-    if rank != 0:
-        dist.destroy_process_group() if dist is not None else None
-        return
-    total_ops = tot[1]
-    ms_per_step = elapsed * 1000.0 / args.steps
-    value = total_ops / (elapsed / args.steps)
-    k = args.steps
-    t_chunks, t_bounds, t_doc, t_hash = [x / k for x in stage_ms]
-    # roofline of the dominant kernel; algorithmic bytes: every input chunk byte read once + every
-    # merged-document byte written once (SURVEY.md §8(d) B_merge), per launch over D documents
-    alg = {"k_doc": in_bytes + out_bytes, "k_chunks": in_bytes, "k_out_hash": 2 * out_bytes}
-    times = {"k_doc": t_doc, "k_chunks": t_chunks, "k_out_hash": t_hash}
-    dom = max(times, key=times.get)
-    achieved = alg[dom] / (times[dom] * 1e-3) / 1e9
-    chunk_gbps = in_bytes / (t_chunks * 1e-3) / 1e9 if t_chunks > 0 else None
-    # correctness spot check against the oracle (outside the timed region)
+        def check(i):
+            return b.doc_output(i, res[i]), (b.doc_patch(i) if not args.no_patch else None)
+    else:
+        from automerge_amd import pipe
+        batch = args.batch or max(16384, min(131072, -(-D // 4)))
+        parts = split_batches(arena, chunks, docs, batch)
+        # capacities from a representative batch (the largest one), staged the ordinary way
+        probe = Batch(device=local)
+        probe.stage(*max(parts, key=lambda p: len(p[0])))
+        ws_need = int(probe.workspace_bytes())
+        kinfo = probe.kernel_info()
+        del probe
+        arena_cap = max(len(p[0]) for p in parts)
+        ncap = max(len(p[2]) for p in parts)
+        ccap = max(len(p[1]) for p in parts)
+        out_cap = ncap * 1024 + (1 << 20)
+        patch_cap = ncap * 1024 + (1 << 20) if not args.no_patch else (1 << 20)
+        pl = pipe.Pipeline(arena_cap, ccap, ncap, ws_need + ws_need // 8 + (1 << 20), out_cap, patch_cap,
+                           kinfo["k_doc_fast_lds_per_doc"], slots=args.slots, device=local)
+        # pinned host memory: inputs, and one set of outputs per batch
+        pin_in = [(pipe.pinned_copy(a), pipe.pinned_copy(c), pipe.pinned_copy(d)) for a, c, d in parts]
+        pin_out = []
+        for a, c, d in parts:
+            s = pipe.Pinned(len(d) * pipe.SUMMARY_DT.itemsize)
+            pin_out.append((s, s.view(pipe.SUMMARY_DT, len(d)), pipe.Pinned(out_cap), pipe.Pinned(patch_cap)))
+
+        def step():
+            for (pa, pc, pd), (_, summ, po, pp) in zip(pin_in, pin_out):
+                pl.submit(pa.arr, pc.arr, pd.arr, summ, po.u8, pp.u8)
+            return pl.drain(len(parts))
+
+        for _ in range(args.warmup):
+            step()
+        pl.times()
+        # the host link on its own (pinned copies of the rank's input bytes, each way)
+        hb = torch.empty(min(int(arena.nbytes), 1 << 30), dtype=torch.uint8).pin_memory()
+        db = torch.empty_like(hb, device="cuda")
+        db.copy_(hb, non_blocking=True)
+        torch.cuda.synchronize()
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
+        db.copy_(hb, non_blocking=True)
+        e1.record()
+        hb.copy_(db, non_blocking=True)
+        e2.record()
+        torch.cuda.synchronize()
+        extra["pcie_GBps"] = {"h2d": hb.numel() / (e0.elapsed_time(e1) * 1e-3) / 1e9,
+                              "d2h": hb.numel() / (e1.elapsed_time(e2) * 1e-3) / 1e9}
+        del hb, db
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            totals = step()
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        ms_comp, ms_doc, nt = pl.times()
+        summ_all = np.concatenate([o[1] for o in pin_out])
+        statuses = summ_all["status"]
+        out_bytes = sum(t[0] for t in totals[:len(parts)])
+        patch_bytes = sum(t[1] for t in totals[:len(parts)])
+        in_b = int(arena.nbytes)
+        nb = len(parts)
+        t_doc = ms_doc / max(nt, 1)  # average document-kernel time per batch (one launch each)
+        alg_launch = (in_b + out_bytes + patch_bytes) / nb
+        extra["kernel_resident_ops_per_s"] = ops_rank * args.steps / (ms_comp * 1e-3) if ms_comp else None
+        extra["kernel_ms_per_step"] = ms_comp / args.steps
+        extra["batches"] = nb
+        extra["batch_docs"] = batch
+        extra["pcie_bytes_per_step_rank0"] = {"h2d": in_b + int(chunks.nbytes) + int(docs.nbytes),
+                                              "d2h": out_bytes + patch_bytes + D * pipe.SUMMARY_DT.itemsize}
+        workspace = int(ws_need)
+        # per-shard digest: container checksum, length and status of every merged document
+        chk = []
+        for _, s, po, _ in pin_out:
+            off = s["out_off"].astype(np.int64)
+            b4 = [po.u8[off + j].astype(np.uint64) for j in range(4, 8)]
+            chk.append(np.where(s["status"] == 0, b4[0] | (b4[1] << 8) | (b4[2] << 16) | (b4[3] << 24), 0))
+        digest = shard.doc_digest_np(ids, statuses, summ_all["out_len"], np.concatenate(chk).astype(np.uint64))
+        starts = np.cumsum([0] + [len(p[2]) for p in parts])
+
+        def check(i):
+            k = int(np.searchsorted(starts, i, side="right") - 1)
+            s = pin_out[k][1][i - starts[k]]
+            o = bytes(pin_out[k][2].u8[int(s["out_off"]):int(s["out_off"]) + int(s["out_len"])])
+            p = bytes(pin_out[k][3].u8[int(s["patch_off"]):int(s["patch_off"]) + int(s["patch_len"])])
+            return o, (p if not args.no_patch else None)
+
+    nerr = int((statuses != 0).sum())
+    tot, _ = shard.exchange(dist, [D, ops_rank, nerr, out_bytes, digest or 0], "cuda")
+    # correctness spot check against the oracle (outside the timed region): merged bytes and patch
     checked = 0
-    if args.check:
+    if args.check and rank == 0:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_ffi as O
+        from automerge_amd import patch as P
+        canon = lambda x: json.dumps(x, sort_keys=True, default=lambda v: bytes(v).hex())
         for i in range(min(args.check, D)):
             base, changes = workload.doc_chunks(arena, chunks, docs, i)
             ref = O.Doc.load(base) if base else O.Doc.init()
-            ref.apply(changes)
-            assert b.doc_output(i, res[i]) == ref.save(), "document %d differs from the oracle" % i
+            want = ref.apply_patch(changes) if not args.no_patch else None
+            got, log = check(i)
+            assert got == ref.save(), "document %d differs from the oracle" % i
+            if log is not None:
+                pat = P.materialize(log, want["deps"], want["pendingChanges"], want["maxOp"])
+                assert canon(pat) == canon(want), "patch of document %d differs from the oracle" % i
             checked += 1
-    per_doc = ops_per_rank // max(D, 1)
-    cpu = None if args.no_cpu_baseline else cpu_baseline(arena, chunks, docs, ops_per_doc=per_doc,
-                                                         name=args.workload.upper())
-    wl = {"c4": "C4: load base doc + applyChanges of 12 concurrent changes (4 actors x 3), 62 ops/doc",
+    if rank != 0:
+        dist.destroy_process_group() if dist is not None else None
+        return
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = tot[1] / (elapsed / args.steps)
+    achieved = alg_launch / (t_doc * 1e-3) / 1e9 if t_doc else None
+    cpu = None if args.no_cpu_baseline else cpu_baseline(arena, chunks, docs, ops_per_doc=per_doc, name=args.workload.upper())
+    wl = {"c4": "C4 1M-document job: load base doc + applyChanges of 12 concurrent changes (4 actors x 3), 60 ops/doc",
           "c2": "C2: applyChanges of 3 changes (10 map/counter/string sets + 2 concurrent inc/overwrite), 14 ops/doc"}
+    what = "H2D + merge + applyChanges patch + D2H (pipelined)" if args.mode == "pipe" else "kernels, inputs resident in HBM"
+    if args.no_patch:
+        what = what.replace(" + applyChanges patch", "")
     line = {
-        "metric": METRIC, "value": value, "unit": "ops/s", "n_gpus": world, "steps": k, "warmup": args.warmup,
-        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u8", "data": "synthetic (seeded %s generator, SURVEY.md 8(d); bytes pinned to the reference encoder)" % args.workload.upper(),
-        "config": {"workload": wl[args.workload],
-                   "docs_per_gpu": D, "total_docs": tot[0], "ops_per_doc_merged": per_doc,
+        "metric": METRIC, "value": value, "unit": "ops/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded %s generator, SURVEY.md 8(d); bytes pinned to the reference encoder)" % args.workload.upper(),
+        "config": {"workload": wl[args.workload] + "; " + what, "total_docs": tot[0], "docs_rank0": D,
+                   "ops_per_doc_merged": per_doc,
+                   "sharding": "SHA-256(base doc)[0] mod N" if args.workload == "c4" else "ranges",
                    "parallelism": "doc-sharded dp%d" % world},
-        "roofline": {"kernel": dom, "bound": "hbm", "limiter": "VALU issue of k_doc_fast (~16.6k VALU per document-wave, DESIGN.md 4); not HBM", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": measured_traffic(dom) if (args.workload, D) == ("c4", 131072) else None,
-                     "alg_bytes_per_launch": alg[dom], "avg_ms": times[dom]},
-        "stage_ms": {"k_chunks(sha256+parse)": t_chunks, "k_bounds+scan": t_bounds, "k_doc(plan+decode+merge+encode)": t_doc,
-                     "k_out_hash": t_hash},
-        "chunk_hash_parse_GBps": chunk_gbps,
-        "docs_per_sec": tot[0] / (elapsed / k),
-        "errors": tot[2], "verified_docs": checked, "input_bytes_per_gpu": in_bytes, "output_bytes_per_gpu": out_bytes,
-        "workspace_bytes_per_gpu": int(b.workspace_bytes()), "gen_s": t_gen,
-        "kernel_info": b.kernel_info(),
-        "cpu_baseline": cpu,
+        "roofline": {"kernel": "k_doc_fast (+ k_doc for the rest)", "bound": "hbm", "achieved": achieved,
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS if achieved else None,
+                     "traffic": None, "alg_bytes_per_launch": alg_launch, "avg_ms": t_doc,
+                     "limiter": "VALU issue of the one-wave-per-document merge (DESIGN.md 4); not HBM"},
+        "errors": tot[2], "verified_docs": checked, "input_bytes_rank0": in_b, "output_bytes_rank0": out_bytes,
+        "patch_bytes_rank0": patch_bytes, "workspace_bytes_per_batch": workspace, "gen_s": t_gen,
+        "docs_per_sec": tot[0] / (elapsed / args.steps), "digest": tot[4],
+        "cpu_baseline": cpu, "cpu_reference_node": cpu_reference(),
     }
+    line.update(extra)
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()

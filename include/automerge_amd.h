@@ -199,6 +199,49 @@ uint64_t am_batch_workspace_bytes(am_batch *b);
  * hot working set. Not part of the reference interface (bench/profiling only). */
 int am_batch_kernel_info(am_batch *b, uint64_t *out3);
 
+/* ---- pipelined batches: the whole job from host memory to host memory ----
+ * A stream of batches (each = many documents, one Backend.load + Backend.applyChanges per document,
+ * as am_batch_*) runs through `slots` device buffer sets: the H2D copy of batch k+1 and the D2H
+ * copy of batch k-1 overlap the kernels of batch k on separate HIP streams. Each batch's merged
+ * documents and patch logs (documents staged with AM_DOC_WANT_DIFF) come back densely packed in
+ * 16-byte slots, described by one am_doc_summary per document. Host buffers should come from
+ * am_host_alloc (pinned) for the copies to be asynchronous.
+ *   caps: per-batch capacities. ws_bytes: device workspace per batch (am_batch_workspace_bytes of a
+ *   representative batch, with headroom); fast_lds: k_doc_fast LDS slice per document
+ *   (am_batch_kernel_info out3[1]; 0 disables the small-document kernel). Documents that exceed a
+ *   capacity report AM_U_CAPACITY in their summary and can be rerun through am_batch_*.
+ * Change chunks must be uncompressed (type 1): DEFLATEd ones go through am_batch_stage. */
+typedef struct am_doc_summary {     /* 32 bytes per document */
+  uint32_t status;                  /* AM_* code (0 = applied / loaded) */
+  uint32_t nqueued;                 /* changes left in the queue (pendingChanges) */
+  uint32_t out_len, patch_len;      /* merged document chunk (uncompressed columns) / patch log bytes */
+  uint64_t out_off, patch_off;      /* their offsets in the batch's output arenas */
+} am_doc_summary;
+typedef struct am_pipe_caps {
+  uint64_t arena_bytes;             /* input bytes per batch */
+  uint32_t chunks, docs;            /* chunks / documents per batch */
+  uint64_t ws_bytes;                /* device workspace per batch */
+  uint64_t out_bytes, patch_bytes;  /* output arena capacities per batch */
+  uint32_t fast_lds;                /* k_doc_fast LDS bytes per document (0: off) */
+  uint32_t slots;                   /* batches in flight (>= 2) */
+} am_pipe_caps;
+typedef struct am_pipe am_pipe;
+void *am_host_alloc(size_t n);      /* pinned host memory (hipHostMalloc) */
+void am_host_free(void *p);
+am_pipe *am_pipe_create(am_engine *eng, const am_pipe_caps *caps, am_error *err);
+void am_pipe_destroy(am_pipe *p);
+/* Enqueues batch `ticket` (returned in *ticket): H2D, the pipeline of am_batch_run, compaction and
+ * D2H into summary[ndocs], out[..] and patches[..]. Blocks only while every slot is in flight. */
+int am_pipe_submit(am_pipe *p, const uint8_t *arena, uint64_t arena_len, const am_chunk_desc *chunks, uint32_t nchunks,
+                   const am_doc_desc *docs, uint32_t ndocs, am_doc_summary *summary, uint8_t *out, uint64_t out_cap,
+                   uint8_t *patches, uint64_t patch_cap, uint64_t *ticket, am_error *err);
+/* Waits until every submitted batch is home. totals (optional, 2 per batch in submission order
+ * since the last drain, up to cap batches): output / patch arena bytes. */
+int am_pipe_drain(am_pipe *p, uint64_t *totals, uint32_t cap, am_error *err);
+/* Device time (ms) of the batches retired since the last call (reset on read): [0] their whole
+ * compute chains summed, [1] their document kernels (k_doc_fast + k_doc) summed; n = batches. */
+int am_pipe_times(am_pipe *p, float *ms2, uint32_t *n);
+
 /* ---- per-document backend state (mirrors backend/backend.js over the batch path, n = 1) ---- */
 am_doc *am_doc_init(am_engine *eng);
 am_doc *am_doc_load(am_engine *eng, const uint8_t *data, size_t len, am_error *err);
@@ -266,24 +309,6 @@ int am_bloom_probe(am_engine *eng, const uint8_t *filters, const uint64_t *foff,
 int am_sync_select(am_engine *eng, uint32_t npairs, const uint64_t *coff, const uint8_t *hashes32, const uint64_t *doff,
                    const int32_t *didx, const uint64_t *pfoff, const uint8_t *filters, const uint64_t *foff,
                    uint8_t *send, am_error *err);
-
-/* ---- synthetic workloads (bench.py input preparation, host side) ----
- * C4: document i = base document (change 0 saved) + 12 concurrent changes (4 actors x 3), seeded
- * by i. Returns the arena bytes needed; fills arena/chunks (13 per doc)/docs when arena != NULL
- * and cap suffices. ops_out receives the number of ops in the 12 changes of all documents. */
-uint64_t am_workload_c4(uint64_t first_doc, uint32_t ndocs, uint8_t *arena, uint64_t cap, am_chunk_desc *chunks,
-                        am_doc_desc *docs, uint64_t *ops_out, int nthreads);
-/* C2 (configs[1]): document i = Backend.init() + 3 changes (10 map/counter/string sets by actor 0;
- * two concurrent changes incrementing the counter and overwriting k1), 3 chunks per document. */
-uint64_t am_workload_c2(uint64_t first_doc, uint32_t ndocs, uint8_t *arena, uint64_t cap, am_chunk_desc *chunks,
-                        am_doc_desc *docs, uint64_t *ops_out, int nthreads);
-/* Text editing histories (C1: cross_every 0, two actors concurrent from the same base; C3:
- * cross_every 10, interleaved): document i = Backend.init() + 1 + nchanges change chunks (change 0
- * = makeText), per_change ops each (1/5 deletes of live elements, otherwise one-character
- * inserts), chunks >= 256 B deflated as encodeChange does (columnar.js:738). */
-uint64_t am_workload_text(uint64_t first_doc, uint32_t ndocs, uint32_t nchanges, uint32_t per_change,
-                          uint32_t cross_every, uint8_t *arena, uint64_t cap, am_chunk_desc *chunks,
-                          am_doc_desc *docs, uint64_t *ops_out, int nthreads);
 
 #ifdef __cplusplus
 }

@@ -91,7 +91,7 @@ def test_apply_patch_one_batch_matches_reference(docs):
 def test_workload_apply_patch_matches_oracle(kind, first, n):
     import oracle_ffi as O
     from automerge_amd import patch as P
-    from automerge_amd import workload
+    import workload
     from automerge_amd.batch import WANT_DIFF, Batch
     arena, chunks, docs, _ = getattr(workload, kind)(first, n)
     docs = docs.copy()
@@ -117,7 +117,7 @@ def test_fast_and_general_patch_writers_agree(docs):
     equal, and the fast writer must take every C4 document (the bench's shape)."""
     import os
     from automerge_amd import patch as P
-    from automerge_amd import workload
+    import workload
     from automerge_amd.batch import WANT_DIFF, Batch
     items = [(base, ch) for base, ch, _ in _steps(docs)]
     nc4 = 600

@@ -73,7 +73,7 @@ def test_deflated_change_chunks_inflate_in_the_batch_stage():
     batch as they are: the stage inflates them on the GPU, the hashes and merged bytes equal the
     oracle's (which inflates with zlib)."""
     import oracle_ffi as O
-    from automerge_amd import workload as W
+    import workload as W
     from automerge_amd.batch import Batch
     arena, chunks, docs, _ = W.text(5, 6, 30, 60, 4)
     b = Batch()

@@ -172,7 +172,8 @@ def test_workload_batch_matches_oracle_and_digest(kind, first, n):
     the CPU oracle's save(), and the device digest (am_batch_digest) equals the host restatement
     (shard.doc_digest) over the oracle's bytes."""
     import oracle_ffi as O
-    from automerge_amd import shard, workload
+    from automerge_amd import shard
+    import workload
     from automerge_amd.batch import Batch
     arena, chunks, docs, _ = getattr(workload, kind)(first, n)
     b = Batch()
@@ -197,7 +198,7 @@ def test_fast_and_general_kernels_agree(docs):
     small-document kernel (k_doc_fast) and with it disabled (AM_FAST=0 at stage time, k_doc only).
     Outputs, heads and results must be identical, and the fast kernel must take the C4/C2 documents."""
     import os
-    from automerge_amd import workload
+    import workload
     from automerge_amd.batch import Batch
     items = []
     for sc in docs:

@@ -1,0 +1,91 @@
+"""Pipelined batches (am_pipe_*): the same documents through the pipeline and through am_batch_*
+give the same merged documents and patch logs; batches larger than the pipeline's capacities are
+refused; documents that outgrow the output arenas report AM_U_CAPACITY instead of a truncated
+result."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _parts(kind, first, n, batch, flags):
+    import bench
+    import workload
+    arena, chunks, docs, _ = getattr(workload, kind)(first, n)
+    docs = docs.copy()
+    docs["flags"] |= flags
+    return (arena, chunks, docs), bench.split_batches(arena, chunks, docs, batch)
+
+
+@pytest.mark.parametrize("kind", ["c4", "c2"])
+def test_pipeline_equals_batch_path(kind):
+    from automerge_amd import pipe
+    from automerge_amd.batch import WANT_DIFF, Batch
+    whole, parts = _parts(kind, 40, 2500, 700, WANT_DIFF)
+    ref = Batch()
+    ref.stage(*whole)
+    ref.run()
+    ref.sync()
+    rr = ref.results()
+    kinfo = ref.kernel_info()
+    ws = int(ref.workspace_bytes())
+    pl = pipe.Pipeline(max(len(p[0]) for p in parts), max(len(p[1]) for p in parts), 700, ws, 1 << 20, 4 << 20,
+                       kinfo["k_doc_fast_lds_per_doc"], slots=2)
+    outs = []
+    for _ in range(2):  # the second pass reuses every slot
+        keep = []
+        for a, c, d in parts:
+            pa, pc, pd = pipe.pinned_copy(a), pipe.pinned_copy(c), pipe.pinned_copy(d)
+            s = pipe.Pinned(len(d) * pipe.SUMMARY_DT.itemsize)
+            po, pp = pipe.Pinned(1 << 20), pipe.Pinned(4 << 20)
+            pl.submit(pa.arr, pc.arr, pd.arr, s.view(pipe.SUMMARY_DT, len(d)), po.u8, pp.u8)
+            keep.append((pa, pc, pd, s, po, pp, len(d)))
+        pl.drain(len(parts))
+        outs.append(keep)
+    for keep in outs:
+        i = 0
+        for pa, pc, pd, s, po, pp, n in keep:
+            sm = s.view(pipe.SUMMARY_DT, n)
+            for j in range(n):
+                assert int(sm[j]["status"]) == int(rr[i]["status"]) == 0
+                o = bytes(po.u8[int(sm[j]["out_off"]):int(sm[j]["out_off"]) + int(sm[j]["out_len"])])
+                assert o == ref.doc_output(i, rr[i]), i
+                p = bytes(pp.u8[int(sm[j]["patch_off"]):int(sm[j]["patch_off"]) + int(sm[j]["patch_len"])])
+                assert p == ref.doc_patch(i), i
+                assert int(sm[j]["nqueued"]) == int(rr[i]["nqueued"])
+                i += 1
+        assert i == 2500
+    ms_comp, ms_doc, nb = pl.times()
+    assert nb == 2 * len(parts) and ms_comp > ms_doc > 0
+
+
+def test_pipeline_capacities():
+    from automerge_amd import _native as N
+    from automerge_amd import pipe
+    from automerge_amd.batch import WANT_DIFF, Batch
+    _, parts = _parts("c4", 0, 300, 300, WANT_DIFF)
+    a, c, d = parts[0]
+    ref = Batch()
+    ref.stage(a, c, d)
+    kinfo = ref.kernel_info()
+    ws = int(ref.workspace_bytes())
+    # a batch above the capacities is refused
+    small = pipe.Pipeline(len(a), len(c), 100, ws, 1 << 20, 1 << 20, kinfo["k_doc_fast_lds_per_doc"], slots=2)
+    pa, pc, pd = pipe.pinned_copy(a), pipe.pinned_copy(c), pipe.pinned_copy(d)
+    s = pipe.Pinned(len(d) * pipe.SUMMARY_DT.itemsize)
+    po, pp = pipe.Pinned(1 << 20), pipe.Pinned(1 << 20)
+    with pytest.raises(N.AutomergeError, match="capacities"):
+        small.submit(pa.arr, pc.arr, pd.arr, s.view(pipe.SUMMARY_DT, len(d)), po.u8, pp.u8)
+    # output arenas that hold only part of the batch: the rest report AM_U_CAPACITY
+    tight = pipe.Pipeline(len(a), len(c), len(d), ws, 100 * 1024, 1 << 20, kinfo["k_doc_fast_lds_per_doc"], slots=2)
+    sm = s.view(pipe.SUMMARY_DT, len(d))
+    tight.submit(pa.arr, pc.arr, pd.arr, sm, po.u8, pp.u8)
+    tight.drain(1)
+    st = sm["status"]
+    assert (st == 0).sum() > 50 and (st == 106).sum() > 50 and set(np.unique(st)) <= {0, 106}
+    # too little workspace: the documents beyond it report AM_U_CAPACITY, the others merge
+    short = pipe.Pipeline(len(a), len(c), len(d), ws // 2, 1 << 20, 1 << 20, kinfo["k_doc_fast_lds_per_doc"], slots=2)
+    short.submit(pa.arr, pc.arr, pd.arr, sm, po.u8, pp.u8)
+    short.drain(1)
+    st = sm["status"]
+    assert (st == 0).sum() > 50 and (st == 106).sum() > 50

@@ -51,7 +51,7 @@ def _run(docs, flags):
 @pytest.mark.parametrize("cs", CASES, ids=[c["name"] for c in CASES])
 def test_text_history_matches_reference(cs):
     from automerge_amd import patch as P
-    from automerge_amd import workload as W
+    import workload as W
     from automerge_amd.batch import WANT_DIFF, WANT_PATCH
     arena, chunks, docs, _ = W.text(cs["first"], cs["n"], cs["nchanges"], cs["per_change"], cs["cross_every"])
     chg = [W.doc_chunks(arena, chunks, docs, i)[1] for i in range(cs["n"])]

@@ -55,7 +55,7 @@ def test_apply_change_depending_on_history_of_loaded_document():
     knows its heads, so applyChanges computes the hash graph and retries (new.js:1826-1832)."""
     import oracle_ffi as O
     from automerge_amd import backend as B
-    from automerge_amd import workload as W
+    import workload as W
     arena, chunks, docs, _ = W.text(3, 1, 6, 5, 0)  # two actors that never meet: B's deps = [change 0]
     _, chg = W.doc_chunks(arena, chunks, docs, 0)
     ref = O.Doc.init()
@@ -79,7 +79,7 @@ def test_backend_hash_graph_queries():
     """getChanges(haveDeps) / getChangesAdded / getMissingDeps of the Python mirror (new.js:1913-2020)
     on two concurrent chains, loaded from save() (history reconstructed) and freshly applied."""
     from automerge_amd import backend as B
-    from automerge_amd import workload as W
+    import workload as W
     arena, chunks, docs, _ = W.text(9, 1, 8, 4, 0)  # change 0, then A and B alternate, never meeting
     _, chg = W.doc_chunks(arena, chunks, docs, 0)
     hashes = B.changeHashes(chg)

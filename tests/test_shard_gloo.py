@@ -1,7 +1,8 @@
-"""N>1 path of bench.py on CPU: two ranks (gloo, 127.0.0.1) shard the C4 documents, merge their
-shard (here with the CPU checker; on the GPU box with the engine) and exchange the per-rank
-digest with one all-gather. The gathered totals must equal one process over all documents, and
-the shards must be disjoint and cover the range."""
+"""N>1 path of bench.py on CPU: two ranks (gloo, 127.0.0.1) shard the C4 job with bench.py's own
+partition (SHA-256 of the base document, first byte mod N: workload.c4_shard), merge their shard
+(here with the CPU checker; on the GPU box with the engine) and exchange the per-rank digest with
+one all-gather. The gathered totals must equal one process over all documents, and the shards
+must be disjoint and cover the job."""
 import os
 import socket
 import sys
@@ -11,7 +12,7 @@ import pytest
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DOCS_PER_RANK = 5
+TOTAL_DOCS = 12
 
 
 def _free_port():
@@ -22,21 +23,24 @@ def _free_port():
     return port
 
 
-def _merge_shard(first, n):
+def _merge_shard(world, rank):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as O
-    from automerge_amd import shard, workload
-    arena, chunks, docs, ops = workload.c4(first, n)
+    from automerge_amd import shard
+    import workload
+    ids = workload.c4_shard(0, TOTAL_DOCS, world, rank)
+    arena, chunks, docs, ops = workload.c4_list(ids)
     lens, terms = [], []
-    for i in range(n):
+    for i, gi in enumerate(ids):
         base, changes = workload.doc_chunks(arena, chunks, docs, i)
+        assert shard.shard_of(base, world) == rank
         d = O.Doc.load(base)
         d.apply(changes)
         out = d.save()
         lens.append(len(out))
-        terms.append(shard.doc_digest(first + i, 0, out))
-    return [n, ops, 0, sum(lens), shard.combine(terms)], lens
+        terms.append(shard.doc_digest(int(gi), 0, out))
+    return [len(ids), ops, 0, sum(lens), shard.combine(terms)], [int(x) for x in ids]
 
 
 def _worker(rank, world, port, outdir):
@@ -45,10 +49,9 @@ def _worker(rank, world, port, outdir):
     sys.path.insert(0, ROOT)
     from automerge_amd import shard
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    first, n = shard.shard_range(rank, world, DOCS_PER_RANK)
-    digest, lens = _merge_shard(first, n)
+    digest, ids = _merge_shard(world, rank)
     tot, rows = shard.exchange(dist, digest, "cpu")
-    np.save(os.path.join(outdir, "rank%d.npy" % rank), np.array(tot + [first, n], dtype=np.int64))
+    np.save(os.path.join(outdir, "rank%d.npy" % rank), np.array(tot + ids, dtype=np.int64))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -67,9 +70,10 @@ def test_two_rank_gloo_digest_matches_single_process(tmp_path):
                        start_method="spawn")
     got = [np.load(os.path.join(tmp_path, "rank%d.npy" % r)).tolist() for r in range(world)]
     assert got[0][:5] == got[1][:5]  # every rank sees the same gathered totals
-    firsts = sorted((g[5], g[6]) for g in got)
-    assert firsts == [(0, DOCS_PER_RANK), (DOCS_PER_RANK, DOCS_PER_RANK)]  # disjoint, covering
-    single, _ = _merge_shard(0, world * DOCS_PER_RANK)
+    ids = sorted(got[0][5:] + got[1][5:])
+    assert ids == list(range(TOTAL_DOCS))  # disjoint, covering
+    assert got[0][5:] and got[1][5:]
+    single, _ = _merge_shard(1, 0)
     assert got[0][:4] == single[:4]
     assert got[0][4] == single[4]
 

@@ -9,7 +9,7 @@ import os
 import pytest
 
 import oracle_ffi as O
-from automerge_amd import workload as W
+import workload as W
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CASES = json.load(open(os.path.join(HERE, "golden", "text.json")))

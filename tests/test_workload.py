@@ -10,7 +10,7 @@ def sha(b):
 
 
 def test_c4_generator_matches_reference_encoder():
-    from automerge_amd import workload
+    import workload
     w = golden("workload.json")["c4"]
     arena, chunks, docs, ops = workload.c4(0, len(w))
     assert ops == 60 * len(w)
@@ -21,7 +21,7 @@ def test_c4_generator_matches_reference_encoder():
 
 
 def test_c4_generator_is_deterministic_across_ranges():
-    from automerge_amd import workload
+    import workload
     a1, c1, d1, _ = workload.c4(100, 8, nthreads=1)
     a2, c2, d2, _ = workload.c4(96, 16, nthreads=4)
     for i in range(8):
@@ -30,7 +30,7 @@ def test_c4_generator_is_deterministic_across_ranges():
 
 def test_c4_oracle_merge_of_generated_docs():
     import oracle_ffi as O
-    from automerge_amd import workload
+    import workload
     w = golden("workload.json")["c4"]
     arena, chunks, docs, _ = workload.c4(0, 16)
     for i in range(16):
@@ -42,7 +42,7 @@ def test_c4_oracle_merge_of_generated_docs():
 
 
 def test_c2_generator_matches_reference_encoder():
-    from automerge_amd import workload
+    import workload
     w = golden("workload.json")["c2"]
     arena, chunks, docs, ops = workload.c2(0, len(w))
     assert ops == 14 * len(w)
@@ -57,7 +57,7 @@ def test_c2_oracle_merge_and_getpatch_of_generated_docs():
     getPatch (documentPatch) the oracle reproduces."""
     import json
     import oracle_ffi as O
-    from automerge_amd import workload
+    import workload
     w = golden("workload.json")["c2"]
     arena, chunks, docs, _ = workload.c2(0, 16)
     for i in range(16):

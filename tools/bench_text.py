@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-baseline", action="store_true", help="time the oracle on document 0 (load + apply)")
     args = ap.parse_args()
-    from automerge_amd import workload as W
+    import workload as W
     from automerge_amd.batch import Batch, pack
 
     t0 = time.perf_counter()

@@ -5,7 +5,7 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from automerge_amd import patch as P  # noqa: E402
-from automerge_amd import workload as W  # noqa: E402
+import workload as W  # noqa: E402
 from automerge_amd.batch import WANT_DIFF, WANT_PATCH, Batch, pack  # noqa: E402
 
 T0 = time.time()

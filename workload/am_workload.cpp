@@ -1,5 +1,6 @@
 // am_workload.cpp -- synthetic workloads of SURVEY.md §8(d) for bench.py (host-side data
-// preparation, runs before any timed region). Documents are generated from a seeded LCG
+// preparation, runs before any timed region; built as workload/libam_workload.so, outside the
+// product library). Documents are generated from a seeded LCG
 // (s = s*1664525 + 1013904223 mod 2^32, seed = document index) and encoded in the Automerge
 // binary change format (columnar.js encodeChange/encodeContainer). The bytes are pinned by the
 // SHA-256 digests in tests/golden/workload.json, which the reference's own encoder produced for
@@ -15,8 +16,8 @@
 
 #include <zlib.h>
 
-#include "../../include/automerge_amd.h"
-#include "am_host_codec.h"
+#include "am_workload.h"
+#include "../automerge_amd/csrc/am_host_codec.h"
 
 namespace {
 
@@ -164,18 +165,28 @@ struct DocOut {
 };
 
 // C4: 4 actors x 3 concurrent changes of 4 list inserts + 1 conflicting title set.
-void gen_c4(uint32_t doc_index, DocOut& out) {
-  uint32_t s = doc_index;
-  std::vector<Actor> actors;
+// The base document (change 0 saved) of document doc_index; s / actors / h0 continue the sequence.
+Bytes c4_base_from(uint32_t& s, std::vector<Actor>& actors, uint8_t h0[32]) {
   make_actors(s, 4, actors);
-  const int A0 = 0;
   std::vector<Op> ops0 = {
       {-1, 0, "items", -1, 0, false, 2, 0, 0, "", {}},
       {-1, 0, "title", -1, 0, false, 1, 6, 0, "untitled", {}},
   };
+  Bytes change0 = encode_change(actors, 0, 1, 1, {}, ops0, h0);
+  return c4_base_doc(actors[0], h0, change0);
+}
+Bytes c4_base(uint32_t doc_index) {
+  uint32_t s = doc_index;
+  std::vector<Actor> actors;
   uint8_t h0[32];
-  Bytes change0 = encode_change(actors, A0, 1, 1, {}, ops0, h0);
-  out.base = c4_base_doc(actors[0], h0, change0);
+  return c4_base_from(s, actors, h0);
+}
+void gen_c4(uint32_t doc_index, DocOut& out) {
+  uint32_t s = doc_index;
+  std::vector<Actor> actors;
+  const int A0 = 0;
+  uint8_t h0[32];
+  out.base = c4_base_from(s, actors, h0);
   std::vector<std::vector<Bytes>> ch(4);
   for (int i = 0; i < 4; i++) {
     std::vector<uint8_t> last(h0, h0 + 32);
@@ -400,18 +411,44 @@ uint64_t layout(std::vector<DocOut>& outs, uint8_t* arena, uint64_t cap, am_chun
   return total;
 }
 
+// Generated documents of the last size query, reused by the fill call that follows it
+struct Cache {
+  uint64_t key = ~0ull;
+  std::vector<DocOut> outs;
+};
+Cache g_cache;
+
 template <class Gen>
-uint64_t generate(Gen gen, uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks,
+uint64_t generate_ids(Gen gen, uint64_t key, const uint64_t* ids, uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap,
+                      am_chunk_desc* chunks, am_doc_desc* docs, uint64_t* ops_out, int nthreads) {
+  if (g_cache.key != key || g_cache.outs.size() != n) {
+    std::vector<DocOut> outs(n);
+    if (nthreads < 1) nthreads = 1;
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; t++)
+      th.emplace_back([&, t]() {
+        for (uint32_t d = t; d < n; d += nthreads) gen((uint32_t)(ids ? ids[d] : first + d), outs[d]);
+      });
+    for (auto& x : th) x.join();
+    g_cache.outs.swap(outs);
+    g_cache.key = key;
+  }
+  const uint64_t need = layout(g_cache.outs, arena, cap, chunks, docs, ops_out);
+  if (arena && cap >= need) {  // filled: release
+    g_cache.key = ~0ull;
+    std::vector<DocOut>().swap(g_cache.outs);
+  }
+  return need;
+}
+uint64_t mix_key(uint64_t kind, uint64_t a, uint64_t b, uint64_t c) {
+  uint64_t h = kind * 0x9E3779B97F4A7C15ull;
+  for (uint64_t v : {a, b, c}) h = (h ^ v) * 0xff51afd7ed558ccdull + 0x632be59bd9b4e5f1ull;
+  return h;
+}
+template <class Gen>
+uint64_t generate(Gen gen, uint64_t kind, uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks,
                   am_doc_desc* docs, uint64_t* ops_out, int nthreads) {
-  std::vector<DocOut> outs(n);
-  if (nthreads < 1) nthreads = 1;
-  std::vector<std::thread> th;
-  for (int t = 0; t < nthreads; t++)
-    th.emplace_back([&, t]() {
-      for (uint32_t d = t; d < n; d += nthreads) gen((uint32_t)(first + d), outs[d]);
-    });
-  for (auto& x : th) x.join();
-  return layout(outs, arena, cap, chunks, docs, ops_out);
+  return generate_ids(gen, mix_key(kind, first, n, 0), nullptr, first, n, arena, cap, chunks, docs, ops_out, nthreads);
 }
 
 }  // namespace
@@ -423,13 +460,13 @@ extern "C" {
  * cap suffices. chunks: n * 13 entries; docs: n entries. ops_out: total ops in the changes. */
 uint64_t am_workload_c4(uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks, am_doc_desc* docs,
                         uint64_t* ops_out, int nthreads) {
-  return generate(gen_c4, first, n, arena, cap, chunks, docs, ops_out, nthreads);
+  return generate(gen_c4, 4, first, n, arena, cap, chunks, docs, ops_out, nthreads);
 }
 
 /* C2: documents [first, first + n), each = Backend.init() + 3 change chunks (no base chunk). */
 uint64_t am_workload_c2(uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks, am_doc_desc* docs,
                         uint64_t* ops_out, int nthreads) {
-  return generate(gen_c2, first, n, arena, cap, chunks, docs, ops_out, nthreads);
+  return generate(gen_c2, 2, first, n, arena, cap, chunks, docs, ops_out, nthreads);
 }
 
 /* Text editing histories (gen_text above; C1: cross_every 0, C3: cross_every 10): documents
@@ -439,7 +476,40 @@ uint64_t am_workload_text(uint64_t first, uint32_t n, uint32_t nchanges, uint32_
                           uint8_t* arena, uint64_t cap, am_chunk_desc* chunks, am_doc_desc* docs, uint64_t* ops_out,
                           int nthreads) {
   auto gen = [=](uint32_t d, DocOut& o) { gen_text(d, nchanges, per_change, cross_every, o); };
-  return generate(gen, first, n, arena, cap, chunks, docs, ops_out, nthreads);
+  return generate(gen, mix_key(10, nchanges, per_change, cross_every), first, n, arena, cap, chunks, docs, ops_out, nthreads);
+}
+
+/* Document sharding of the C4 job: the documents of [first, first + n) whose
+ * base document's SHA-256 (its container checksum, columnar.js:659-686) has first byte % world ==
+ * rank, in index order. Writes up to cap indexes; returns how many belong to the shard. */
+uint64_t am_workload_c4_shard(uint64_t first, uint64_t n, uint32_t world, uint32_t rank, uint64_t* ids, uint64_t cap,
+                              int nthreads) {
+  if (world == 0) return 0;
+  if (nthreads < 1) nthreads = 1;
+  std::vector<uint8_t> mine(n, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; t++)
+    th.emplace_back([&, t]() {
+      for (uint64_t d = t; d < n; d += nthreads) {
+        const Bytes base = c4_base((uint32_t)(first + d));
+        mine[d] = base.size() > 4 && base[4] % world == rank;
+      }
+    });
+  for (auto& x : th) x.join();
+  uint64_t k = 0;
+  for (uint64_t d = 0; d < n; d++)
+    if (mine[d]) {
+      if (ids && k < cap) ids[k] = first + d;
+      k++;
+    }
+  return k;
+}
+
+/* C4 documents with the given indexes (am_workload_c4 over a list, e.g. one shard). */
+uint64_t am_workload_c4_list(const uint64_t* ids, uint32_t n, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks,
+                             am_doc_desc* docs, uint64_t* ops_out, int nthreads) {
+  const uint64_t key = mix_key(40, n ? ids[0] : 0, n, n ? ids[n - 1] : 0);
+  return generate_ids(gen_c4, key, ids, 0, n, arena, cap, chunks, docs, ops_out, nthreads);
 }
 
 }  // extern "C"
