@@ -7,7 +7,7 @@
 'use strict'
 const fs = require('fs')
 const path = require('path')
-const REF = process.argv[2] || '/root/reference'
+const REF = process.env.AM_REF || (require.main === module && process.argv[2]) || '/root/reference'
 const OUT = path.join(__dirname, '..')
 
 const Automerge = require(path.join(REF, 'src/automerge'))
@@ -618,4 +618,5 @@ function main() {
   write('bloom_edge.json', bloomEdgeVectors())
 }
 
-main()
+if (require.main === module) main()
+else module.exports = {c4Doc, c2Doc, lcg}
