@@ -51,6 +51,10 @@ class PipeCaps(C.Structure):
                 ("out_bytes", C.c_uint64), ("patch_bytes", C.c_uint64), ("fast_lds", C.c_uint32), ("slots", C.c_uint32)]
 
 
+class Span(C.Structure):
+    _fields_ = [("off", C.c_uint64), ("len", C.c_uint64)]
+
+
 class Error(C.Structure):
     _fields_ = [("code", C.c_uint32), ("is_type_error", C.c_int32), ("message", C.c_char * 480)]
 
@@ -106,6 +110,29 @@ _sigs = {
     "am_stage_change": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
     "am_stage_document": (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t),
                                     C.POINTER(C.c_int), C.POINTER(Error)]),
+    "am_doc_get_changes": (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.c_size_t),
+                                     C.POINTER(Error)]),
+    "am_doc_get_changes_added": (C.c_int, [P, P, C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(C.c_size_t),
+                                           C.POINTER(Error)]),
+    "am_doc_change_index": (C.c_int64, [P, C.c_char_p]),
+    "am_doc_get_missing_deps": (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t),
+                                          C.POINTER(Error)]),
+    "am_doc_clock": (C.c_int64, [P, C.c_char_p]),
+    "am_doc_actor_hash": (C.c_int, [P, C.c_char_p, C.c_int64, P]),
+    "am_doc_change_deps": (C.c_int, [P, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t)]),
+    "am_doc_engine": (P, [P]),
+    "am_encode_change": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), P, C.POINTER(Error)]),
+    "am_doc_apply_local_change": (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t),
+                                            C.POINTER(u8p), C.POINTER(C.c_size_t), P, P, C.POINTER(C.c_int),
+                                            C.POINTER(Error)]),
+    "am_bloom_check": (C.c_int, [C.c_char_p, C.c_uint64, C.POINTER(Error)]),
+    "am_sync_generate": (C.c_int, [C.c_size_t, P, P, P, P, P, P, P, P]),
+    "am_sync_receive": (C.c_int, [P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(u8p),
+                                  C.POINTER(C.c_size_t), C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
+    "am_sync_encode_message": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
+    "am_sync_decode_messages": (C.c_int, [C.c_size_t, P, P, C.POINTER(C.POINTER(Span)), P, P, P]),
+    "am_sync_encode_state": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
+    "am_sync_decode_state": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
     "am_host_alloc": (P, [C.c_size_t]),
     "am_host_free": (None, [P]),
     "am_pipe_create": (P, [P, C.POINTER(PipeCaps), C.POINTER(Error)]),
@@ -163,6 +190,13 @@ def buf_array(bufs):
     arr = (C.c_char_p * max(n, 1))(*[bytes(b) for b in bufs])
     lens = (C.c_size_t * max(n, 1))(*[len(b) for b in bufs])
     return arr, lens, n
+
+
+def take(ptr, n):
+    """bytes of a malloc'd engine result, then am_free."""
+    b = C.string_at(ptr, n) if n else b""
+    lib.am_free(ptr)
+    return b
 
 
 def stage_change(data):

@@ -6,6 +6,8 @@ MI355X pipeline of libautomerge_amd.so (there is no CPU path). A backend state i
 further use raises the reference's error (backend/util.js:1-10).
 """
 import ctypes as C
+import json
+import re
 
 from . import _native as N
 
@@ -154,39 +156,6 @@ def _hash_graph(s):
         N.raise_for(err)
 
 
-def getAllChanges(backend):
-    """Backend.getAllChanges() (backend/backend.js:142-144 -> getChanges(backend, [])): the whole
-    history; a loaded document first reconstructs it from save() (computeHashGraph)."""
-    s = _backend_state(backend)
-    _hash_graph(s)
-    out = []
-    i = 0
-    while True:
-        p = N.u8p()
-        n = C.c_size_t()
-        if N.lib.am_doc_change(s.ptr, i, C.byref(p), C.byref(n), None):
-            break
-        out.append(C.string_at(p, n.value))
-        i += 1
-    return out
-
-
-def getChangeByHash(backend, hash_hex):
-    """Backend.getChangeByHash() (backend/backend.js:166-168)."""
-    s = _backend_state(backend)
-    _hash_graph(s)
-    i = 0
-    h = (C.c_uint8 * 32)()
-    while True:
-        p = N.u8p()
-        n = C.c_size_t()
-        if N.lib.am_doc_change(s.ptr, i, C.byref(p), C.byref(n), h):
-            return None
-        if bytes(h).hex() == hash_hex:
-            return C.string_at(p, n.value)
-        i += 1
-
-
 def changeHashes(changes, device=0):
     """decodeChangeMeta(change, true).hash for each change (columnar.js:783), on the GPU."""
     arr, lens, n = N.buf_array(changes)
@@ -198,45 +167,32 @@ def changeHashes(changes, device=0):
     return [raw[32 * i:32 * i + 32].hex() for i in range(n)]
 
 
-# ---- hash-graph queries (new.js:1913-2020), host traversals over the change history ----
-def _uleb(b, o):
-    v = sh = 0
-    while True:
-        c = b[o]
-        o += 1
-        v |= (c & 0x7F) << sh
-        sh += 7
-        if not c & 0x80:
-            return v, o
+# ---- hash-graph queries (new.js:1913-2020): the traversals run in the engine (am_graph.cpp) ----
+_HEX64 = re.compile(r"^[0-9a-f]{64}$")
 
 
-def _change_deps(data):
-    """deps (hex) of a binary change (decodeChangeMeta, columnar.js:783-793)."""
-    b = N.stage_change(data)
-    _, o = _uleb(b, 9)
-    n, o = _uleb(b, o)
-    return [b[o + 32 * i:o + 32 * i + 32].hex() for i in range(n)]
+def _flat_hashes(hashes):
+    """One flat bytes of 32-byte hashes; a string that is not a hash travels as a sentinel the
+    engine cannot know (0xff x 28 + its index), mapped back where a result or error names it."""
+    out, odd = [], {}
+    for i, h in enumerate(hashes):
+        if isinstance(h, str) and _HEX64.match(h):
+            out.append(bytes.fromhex(h))
+        else:
+            b = b"\xff" * 28 + i.to_bytes(4, "big")
+            odd[b.hex()] = h
+            out.append(b)
+    return b"".join(out), odd
 
 
-def _graph(s):
-    _hash_graph(s)
-    changes = []
-    i = 0
-    h = (C.c_uint8 * 32)()
-    while True:
-        p = N.u8p()
-        n = C.c_size_t()
-        if N.lib.am_doc_change(s.ptr, i, C.byref(p), C.byref(n), h):
-            break
-        changes.append((bytes(h).hex(), C.string_at(p, n.value)))
-        i += 1
-    index = {hh: k for k, (hh, _) in enumerate(changes)}
-    deps_of = {hh: _change_deps(b) for hh, b in changes}
-    dependents = {hh: [] for hh, _ in changes}
-    for hh, _ in changes:
-        for d in deps_of[hh]:
-            dependents.setdefault(d, []).append(hh)
-    return changes, index, deps_of, dependents
+def _changes_at(s, idx, n):
+    res = []
+    for k in range(n):
+        p, ln = N.u8p(), C.c_size_t()
+        if N.lib.am_doc_change(s.ptr, idx[k], C.byref(p), C.byref(ln), None):
+            raise N.AutomergeError("automerge_amd: change index out of range")
+        res.append(C.string_at(p, ln.value))
+    return res
 
 
 def getChanges(backend, haveDeps):
@@ -244,64 +200,344 @@ def getChanges(backend, haveDeps):
     if not isinstance(haveDeps, list):
         raise TypeError("Pass an array of hashes to Backend.getChanges()")
     s = _backend_state(backend)
-    changes, index, deps_of, dependents = _graph(s)
-    if not haveDeps:
-        return [b for _, b in changes]
-    stack, seen, to_return = [], set(), []
-    for h in haveDeps:
-        seen.add(h)
-        if h not in dependents:
-            raise N.AutomergeError("hash not found: %s" % h, 0, "RangeError")
-        stack += dependents[h]
-    while stack:
-        h = stack.pop()
-        seen.add(h)
-        to_return.append(h)
-        if not all(d in seen for d in deps_of[h]):
-            break
-        stack += dependents[h]
-    if not stack and all(h in seen for h in backend.heads):
-        return [changes[index[h]][1] for h in to_return]
-    stack, seen = list(haveDeps), set()
-    while stack:
-        h = stack.pop()
-        if h not in seen:
-            if h not in deps_of:
-                raise N.AutomergeError("hash not found: %s" % h, 0, "RangeError")
-            stack += deps_of[h]
-            seen.add(h)
-    return [b for h, b in changes if h not in seen]
+    flat, odd = _flat_hashes(haveDeps)
+    idx, n, err = C.POINTER(C.c_uint64)(), C.c_size_t(), N.Error()
+    if N.lib.am_doc_get_changes(s.ptr, flat or None, len(haveDeps), C.byref(idx), C.byref(n), C.byref(err)):
+        msg = err.message.decode("utf-8", "replace")
+        for k, v in odd.items():
+            msg = msg.replace(k, str(v))
+        raise N.AutomergeError(msg, err.code, "TypeError" if err.is_type_error else "RangeError")
+    try:
+        return _changes_at(s, idx, n.value)
+    finally:
+        N.lib.am_free(idx)
+
+
+def getAllChanges(backend):
+    """Backend.getAllChanges() (backend/backend.js:142-144 -> getChanges(backend, []))."""
+    return getChanges(backend, [])
 
 
 def getChangesAdded(backend1, backend2):
     """Backend.getChangesAdded() (new.js:1971-1988): changes in backend2 that backend1 lacks."""
-    _, other, _, _ = _graph(_backend_state(backend1))
-    changes, index, deps_of, _ = _graph(_backend_state(backend2))
-    stack, seen, to_return = list(backend2.heads), set(), []
-    while stack:
-        h = stack.pop()
-        if h not in seen and h not in other:
-            seen.add(h)
-            to_return.append(h)
-            stack += deps_of[h]
-    return [changes[index[h]][1] for h in reversed(to_return)]
+    s1, s2 = _backend_state(backend1), _backend_state(backend2)
+    idx, n, err = C.POINTER(C.c_uint64)(), C.c_size_t(), N.Error()
+    if N.lib.am_doc_get_changes_added(s1.ptr, s2.ptr, C.byref(idx), C.byref(n), C.byref(err)):
+        N.raise_for(err)
+    try:
+        return _changes_at(s2, idx, n.value)
+    finally:
+        N.lib.am_free(idx)
+
+
+def getChangeByHash(backend, hash_hex):
+    """Backend.getChangeByHash() (backend/backend.js:166-168, new.js:1990-1993); None when unknown."""
+    s = _backend_state(backend)
+    if not (isinstance(hash_hex, str) and _HEX64.match(hash_hex)):
+        return None
+    i = N.lib.am_doc_change_index(s.ptr, bytes.fromhex(hash_hex))
+    if i == -2:
+        raise N.AutomergeError("automerge_amd: the document history could not be reconstructed")
+    return None if i < 0 else _changes_at(s, [i], 1)[0]
 
 
 def getMissingDeps(backend, heads=None):
     """Backend.getMissingDeps() (new.js:2005-2020)."""
     s = _backend_state(backend)
-    _, index, _, _ = _graph(s)
-    all_deps, in_queue = set(heads or []), set()
-    queued = []
-    i = 0
+    heads = list(heads or [])
+    flat, odd = _flat_hashes(heads)
+    out, n, err = N.u8p(), C.c_size_t(), N.Error()
+    if N.lib.am_doc_get_missing_deps(s.ptr, flat or None, len(heads), C.byref(out), C.byref(n), C.byref(err)):
+        N.raise_for(err)
+    raw = N.take(out, 32 * n.value)
+    res = [odd.get(raw[i:i + 32].hex(), raw[i:i + 32].hex()) for i in range(0, len(raw), 32)]
+    return sorted(res) if odd else res
+
+
+# ---- applyLocalChange (backend.js:54-91): encodeChange + applyChanges(isLocal) in the engine ----
+def _json_default(o):
+    if isinstance(o, (bytes, bytearray, memoryview)):
+        return {"__bytes": bytes(o).hex()}
+    raise TypeError("not JSON serializable: %r" % (o,))
+
+
+def _nonfinite(x):
+    if isinstance(x, float) and (x != x or x in (float("inf"), float("-inf"))):
+        return {"__f64": "NaN" if x != x else ("Infinity" if x > 0 else "-Infinity")}
+    if isinstance(x, dict):
+        return {k: _nonfinite(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_nonfinite(v) for v in x]
+    return x
+
+
+def request_json(obj):
+    """A change request / sync message as the JSON text the C ABI reads (include/automerge_amd.h)."""
+    return json.dumps(_nonfinite(obj), default=_json_default, allow_nan=False).encode()
+
+
+def encodeChange(change):
+    """encodeChange (columnar.js:710-739) in the engine library (am_encode_change, host code)."""
+    js = request_json(change)
+    out, n, err = N.u8p(), C.c_size_t(), N.Error()
+    if N.lib.am_encode_change(js, len(js), C.byref(out), C.byref(n), None, C.byref(err)):
+        N.raise_for(err)
+    return N.take(out, n.value)
+
+
+def applyLocalChange(backend, change):
+    """Backend.applyLocalChange() (backend/backend.js:54-91). Returns (state, patch, binaryChange);
+    like the reference, the request's deps gain the local actor's previous change."""
+    from . import patch as P
+    s = _backend_state(backend)
+    js = request_json(change)
+    ch, cl, pa, pl = N.u8p(), C.c_size_t(), N.u8p(), C.c_size_t()
+    nh, lh, has_last, err = (C.c_uint8 * 32)(), (C.c_uint8 * 32)(), C.c_int(), N.Error()
+    rc = N.lib.am_doc_apply_local_change(s.ptr, js, len(js), C.byref(ch), C.byref(cl), C.byref(pa), C.byref(pl), nh,
+                                         lh, C.byref(has_last), C.byref(err))
+    if rc:
+        if rc == 2:
+            backend.frozen = True
+        N.raise_for(err)
+    if has_last.value:
+        deps = {bytes(lh).hex(): True}
+        for h in change["deps"]:
+            deps[h] = True
+        change["deps"] = sorted(deps)
+    binary, log = N.take(ch, cl.value), N.take(pa, pl.value)
+    backend.frozen = True
+    new = BackendState(s, s.heads())
+    patch = P.materialize(log, [h for h in new.heads if h != bytes(nh).hex()], N.lib.am_doc_pending(s.ptr),
+                          N.lib.am_doc_max_op(s.ptr))
+    patch["actor"] = change["actor"]
+    patch["seq"] = change["seq"]
+    return new, patch, binary
+
+
+# ---- sync protocol (backend/sync.js) in the engine (am_sync_proto.cpp); SyncState dicts cross as
+# the flat state blob of include/automerge_amd.h ----
+def _checked_hash(h):
+    if not isinstance(h, str):
+        raise N.AutomergeError("value is not a string", kind="TypeError")
+    if not re.match(r"^([0-9a-f][0-9a-f])*$", h):
+        raise N.AutomergeError("value is not hexadecimal")
+    if len(h) != 64:
+        raise N.AutomergeError("heads hashes must be 256 bits", kind="TypeError")
+    return bytes.fromhex(h)
+
+
+def _uleb(v):
+    out = bytearray()
     while True:
-        p = N.u8p()
-        n = C.c_size_t()
-        if N.lib.am_doc_queued(s.ptr, i, C.byref(p), C.byref(n)):
-            break
-        queued.append(C.string_at(p, n.value))
-        i += 1
-    for b, h in zip(queued, changeHashes(queued) if queued else []):
-        in_queue.add(h)
-        all_deps.update(_change_deps(b))
-    return sorted(h for h in all_deps if h not in index and h not in in_queue)
+        b = v & 0x7F
+        v >>= 7
+        out.append(b | (0x80 if v else 0))
+        if not v:
+            return bytes(out)
+
+
+def _pack_state(st):
+    def hashes(lst):
+        if not isinstance(lst, list):
+            raise N.AutomergeError("hashes must be an array", kind="TypeError")
+        return _uleb(len(lst)) + b"".join(_checked_hash(h) for h in lst)
+    sent = st.get("sentHashes")
+    keys = [k for k in sent if _HEX64.match(k)] if isinstance(sent, dict) else []
+    flags = ((1 if st.get("theirHeads") is not None else 0) | (2 if st.get("theirNeed") is not None else 0) |
+             (4 if st.get("theirHave") is not None else 0) | (8 if isinstance(sent, list) else 0))
+    out = bytes([0x53, flags]) + hashes(st["sharedHeads"]) + hashes(st["lastSentHeads"])
+    if flags & 1:
+        out += hashes(st["theirHeads"])
+    if flags & 2:
+        out += hashes(st["theirNeed"])
+    if flags & 4:
+        out += _uleb(len(st["theirHave"]))
+        for h in st["theirHave"]:
+            b = bytes(h["bloom"])
+            out += hashes(h["lastSync"]) + _uleb(len(b)) + b
+    return out + _uleb(len(keys)) + b"".join(bytes.fromhex(k) for k in keys)
+
+
+def _unpack_state(b):
+    o = [2]
+
+    def u():
+        v = sh = 0
+        while True:
+            x = b[o[0]]
+            o[0] += 1
+            v |= (x & 0x7F) << sh
+            sh += 7
+            if not x & 0x80:
+                return v
+
+    def hashes():
+        n = u()
+        r = [b[o[0] + 32 * i:o[0] + 32 * i + 32].hex() for i in range(n)]
+        o[0] += 32 * n
+        return r
+    flags = b[1]
+    st = {"sharedHeads": hashes(), "lastSentHeads": hashes(), "theirHeads": None, "theirNeed": None, "theirHave": None}
+    if flags & 1:
+        st["theirHeads"] = hashes()
+    if flags & 2:
+        st["theirNeed"] = hashes()
+    if flags & 4:
+        st["theirHave"] = []
+        for _ in range(u()):
+            ls = hashes()
+            ln = u()
+            st["theirHave"].append({"lastSync": ls, "bloom": bytes(b[o[0]:o[0] + ln])})
+            o[0] += ln
+    sent = hashes()
+    st["sentHashes"] = [] if flags & 8 else {h: True for h in sent}
+    return st
+
+
+def initSyncState():
+    """initSyncState() (sync.js:308-317)."""
+    return {"sharedHeads": [], "lastSentHeads": [], "theirHeads": None, "theirNeed": None, "theirHave": None,
+            "sentHashes": {}}
+
+
+def encodeSyncMessage(message):
+    """encodeSyncMessage (sync.js:157-171)."""
+    js = request_json(message)
+    out, n, err = N.u8p(), C.c_size_t(), N.Error()
+    if N.lib.am_sync_encode_message(js, len(js), C.byref(out), C.byref(n), C.byref(err)):
+        N.raise_for(err)
+    return N.take(out, n.value)
+
+
+def decodeSyncMessages(messages):
+    """decodeSyncMessage (sync.js:177-199) over many messages in one call (am_sync_decode_messages):
+    a list of message dicts, or the AutomergeError of a malformed one in its place."""
+    n = len(messages)
+    bufs = [bytes(m) for m in messages]
+    arr = (C.c_char_p * max(n, 1))(*bufs)
+    lens = (C.c_size_t * max(n, 1))(*[len(b) for b in bufs])
+    spans = C.POINTER(N.Span)()
+    soff = (C.c_uint64 * (n + 1))()
+    counts = (C.c_uint32 * (4 * max(n, 1)))()
+    errs = (N.Error * max(n, 1))()
+    N.lib.am_sync_decode_messages(n, arr, lens, C.byref(spans), soff, counts, errs)
+    out = []
+    for i, m in enumerate(bufs):
+        if errs[i].code:
+            e = errs[i]
+            out.append(N.AutomergeError(e.message.decode("utf-8", "replace"), e.code,
+                                        "TypeError" if e.is_type_error else "RangeError"))
+            continue
+        k = int(soff[i])
+
+        def hl(sp):
+            return [m[sp.off + 32 * j:sp.off + 32 * j + 32].hex() for j in range(sp.len)]
+        msg = {"heads": hl(spans[k]), "need": hl(spans[k + 1]), "have": [], "changes": []}
+        k += 2
+        for _ in range(counts[4 * i + 2]):
+            msg["have"].append({"lastSync": hl(spans[k]), "bloom": m[spans[k + 1].off:spans[k + 1].off + spans[k + 1].len]})
+            k += 2
+        for _ in range(counts[4 * i + 3]):
+            msg["changes"].append(m[spans[k].off:spans[k].off + spans[k].len])
+            k += 1
+        out.append(msg)
+    N.lib.am_free(spans)
+    return out
+
+
+def decodeSyncMessage(data):
+    """decodeSyncMessage (sync.js:177-199)."""
+    r = decodeSyncMessages([data])[0]
+    if isinstance(r, Exception):
+        raise r
+    return r
+
+
+def encodeSyncState(sync_state):
+    """encodeSyncState (sync.js:206-211)."""
+    blob = _pack_state({"sharedHeads": sync_state["sharedHeads"], "lastSentHeads": []})
+    out, n, err = N.u8p(), C.c_size_t(), N.Error()
+    if N.lib.am_sync_encode_state(blob, len(blob), C.byref(out), C.byref(n), C.byref(err)):
+        N.raise_for(err)
+    return N.take(out, n.value)
+
+
+def decodeSyncState(data):
+    """decodeSyncState (sync.js:217-225)."""
+    out, n, err = N.u8p(), C.c_size_t(), N.Error()
+    if N.lib.am_sync_decode_state(bytes(data), len(data), C.byref(out), C.byref(n), C.byref(err)):
+        N.raise_for(err)
+    return _unpack_state(N.take(out, n.value))
+
+
+def generateSyncMessages(backends, sync_states):
+    """generateSyncMessage for many documents in one call (am_sync_generate): their Bloom filters
+    are built in one k_bloom_build launch and their change selections run in one k_sync_select
+    launch. Returns [(state, message or None) or AutomergeError]."""
+    n = len(backends)
+    ptrs = (C.c_void_p * max(n, 1))(*[_backend_state(b).ptr for b in backends])
+    packed = [_pack_state(s) for s in sync_states]
+    st = (C.c_char_p * max(n, 1))(*packed)
+    sl = (C.c_size_t * max(n, 1))(*[len(p) for p in packed])
+    ost, osl = (N.u8p * max(n, 1))(), (C.c_size_t * max(n, 1))()
+    msg, ml = (N.u8p * max(n, 1))(), (C.c_size_t * max(n, 1))()
+    errs = (N.Error * max(n, 1))()
+    N.lib.am_sync_generate(n, ptrs, st, sl, ost, osl, msg, ml, errs)
+    out = []
+    for i in range(n):
+        if errs[i].code:
+            e = errs[i]
+            out.append(N.AutomergeError(e.message.decode("utf-8", "replace"), e.code,
+                                        "TypeError" if e.is_type_error else "RangeError"))
+            continue
+        blob = N.take(ost[i], osl[i])
+        m = N.take(msg[i], ml[i]) if msg[i] else None
+        if m is None or blob == packed[i]:
+            out.append((sync_states[i], m))
+        else:
+            nxt = _unpack_state(blob)
+            out.append((dict(sync_states[i], lastSentHeads=nxt["lastSentHeads"], sentHashes=nxt["sentHashes"]), m))
+    return out
+
+
+def generateSyncMessage(backend, sync_state):
+    """generateSyncMessage (sync.js:327-400): (syncState, message or None)."""
+    if not backend:
+        raise N.AutomergeError("generateSyncMessage called with no Automerge document", kind="Error")
+    if not sync_state:
+        raise N.AutomergeError("generateSyncMessage requires a syncState, which can be created with initSyncState()",
+                               kind="Error")
+    r = generateSyncMessages([backend], [sync_state])[0]
+    if isinstance(r, Exception):
+        raise r
+    return r
+
+
+def receiveSyncMessage(backend, old_sync_state, message):
+    """receiveSyncMessage (sync.js:420-474): (backend, syncState, patch or None)."""
+    from . import patch as P
+    if not backend:
+        raise N.AutomergeError("generateSyncMessage called with no Automerge document", kind="Error")
+    if not old_sync_state:
+        raise N.AutomergeError("generateSyncMessage requires a syncState, which can be created with initSyncState()",
+                               kind="Error")
+    msg = decodeSyncMessage(message)
+    s = _backend_state(backend) if (msg["changes"] or msg["heads"]) else backend.state
+    blob = _pack_state(old_sync_state)
+    ost, osl, pa, pl, err = N.u8p(), C.c_size_t(), N.u8p(), C.c_size_t(), N.Error()
+    rc = N.lib.am_sync_receive(s.ptr, blob, len(blob), bytes(message), len(message), C.byref(ost), C.byref(osl),
+                               C.byref(pa), C.byref(pl), C.byref(err))
+    if rc:
+        if rc == 2:
+            backend.frozen = True
+        N.raise_for(err)
+    st = _unpack_state(N.take(ost, osl.value))
+    patch = None
+    log = N.take(pa, pl.value) if pa else None
+    if msg["changes"]:
+        backend.frozen = True
+        backend = BackendState(s, s.heads())
+        patch = P.materialize(log, backend.heads, N.lib.am_doc_pending(s.ptr), N.lib.am_doc_max_op(s.ptr))
+    sent = st["sentHashes"] if isinstance(st["sentHashes"], list) else old_sync_state.get("sentHashes")
+    return backend, {"sharedHeads": st["sharedHeads"], "lastSentHeads": st["lastSentHeads"], "theirHave": msg["have"],
+                     "theirHeads": msg["heads"], "theirNeed": msg["need"], "sentHashes": sent}, patch

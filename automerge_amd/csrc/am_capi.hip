@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <array>
+#include <functional>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -17,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "am_graph.h"
 #include "am_launch.h"
 #include "am_patch.h"
 
@@ -1000,7 +1002,10 @@ struct am_doc {
   std::vector<std::vector<uint8_t>> changes;           // applied change buffers (this.changes)
   std::vector<std::array<uint8_t, 32>> hashes;         // their hashes
   std::vector<std::vector<uint8_t>> queue;             // enqueued change buffers (this.queue)
+  std::vector<std::array<uint8_t, 32>> queue_hashes;   // their hashes
   std::vector<std::array<uint8_t, 32>> heads;
+  std::vector<std::array<uint8_t, 32>> load_heads;     // changeIndexByHash of a loaded document without its graph
+  HashGraph graph;                                     // over changes[0, graph.size()) (am_graph.h)
   int64_t max_op = 0;
   size_t nchanges = 0;
 };
@@ -1238,6 +1243,7 @@ extern "C" am_doc* am_doc_load(am_engine* eng, const uint8_t* data, size_t len, 
   d->has_binary = true;
   d->have_hash_graph = false;
   d->heads = res.heads;
+  d->load_heads = res.heads;
   d->nchanges = res.r.nchanges;
   // maxOp of a loaded document: the largest op counter in ids and succs (documentPatch,
   // new.js:1627-1630, 1749) -- reduced by k_doc over the base rows
@@ -1323,16 +1329,18 @@ static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* le
   const size_t base = d->state.empty() ? 0 : 1;
   std::vector<size_t> applied(res.r.napplied);
   std::vector<std::vector<uint8_t>> newq;
+  std::vector<std::array<uint8_t, 32>> newqh;
   for (size_t i = 0; i < orig.size(); i++) {
     int32_t st = res.chg_state[base + i];
     if (st >= 0) applied[(size_t)st] = i;
-    else if (st == CHG_QUEUED) newq.push_back(orig[i]);
+    else if (st == CHG_QUEUED) { newq.push_back(orig[i]); newqh.push_back(res.hashes[base + i]); }
   }
   for (size_t k = 0; k < applied.size(); k++) {
     d->changes.push_back(orig[applied[k]]);
     d->hashes.push_back(res.hashes[base + applied[k]]);
   }
   d->queue = std::move(newq);
+  d->queue_hashes = std::move(newqh);
   d->state = std::move(res.out);
   d->heads = res.heads;
   d->has_binary = false;
@@ -1458,6 +1466,7 @@ extern "C" int am_doc_compute_hash_graph(am_doc* d, am_error* err) {
   if (am_document_changes(d->state.data(), d->state.size(), &out, &offs, &hs, &n, err)) return 1;
   d->changes.clear();
   d->hashes.clear();
+  d->graph.clear();
   for (size_t i = 0; i < n; i++) {
     d->changes.emplace_back(out + offs[i], out + offs[i + 1]);
     std::array<uint8_t, 32> h;
@@ -1517,6 +1526,131 @@ extern "C" int am_doc_queued(const am_doc* d, size_t i, const uint8_t** data, si
   *len = d->queue[i].size();
   return 0;
 }
+
+// ---- hash-graph queries of BackendDoc (new.js:1913-2020) over the graph kept with the document ----
+static Hash32 h32(const uint8_t* p) {
+  Hash32 h;
+  std::memcpy(h.b, p, 32);
+  return h;
+}
+// computeHashGraph on first use, then index the changes committed since
+static bool ensure_graph(am_doc* d, am_error* err) {
+  if (!d->have_hash_graph && am_doc_compute_hash_graph(d, err)) return false;
+  for (size_t i = d->graph.size(); i < d->changes.size(); i++) {
+    ChangeMeta m;
+    if (!am_change_meta(d->changes[i].data(), d->changes[i].size(), m)) {
+      to_c(Err{AM_U_VALUE, false, "automerge_amd: unreadable change header in the document history"}, err);
+      return false;
+    }
+    d->graph.add(h32(d->hashes[i].data()), m);
+  }
+  if (err) err->code = 0;
+  return true;
+}
+static std::vector<Hash32> heads_of(const am_doc* d) {
+  std::vector<Hash32> h;
+  for (auto& x : d->heads) h.push_back(h32(x.data()));
+  return h;
+}
+static int out_indexes(const std::vector<size_t>& v, uint64_t** idx, size_t* n, am_error* err) {
+  *n = v.size();
+  *idx = static_cast<uint64_t*>(std::malloc(sizeof(uint64_t) * (v.size() ? v.size() : 1)));
+  if (!*idx) { to_c(Err{AM_U_CAPACITY, false, "automerge_amd: out of host memory"}, err); return 1; }
+  for (size_t i = 0; i < v.size(); i++) (*idx)[i] = v[i];
+  if (err) err->code = 0;
+  return 0;
+}
+
+extern "C" int am_doc_get_changes(am_doc* d, const uint8_t* have32, size_t nhave, uint64_t** idx, size_t* n, am_error* err) {
+  if (!ensure_graph(d, err)) return 1;
+  std::vector<Hash32> have;
+  for (size_t i = 0; i < nhave; i++) have.push_back(h32(have32 + 32 * i));
+  std::vector<size_t> out;
+  Hash32 missing;
+  if (!d->graph.changes_since(have, heads_of(d), out, missing)) {
+    to_c(Err{AM_E_HISTORY, false, "hash not found: " + hexs(missing.b, 32)}, err);
+    return 1;
+  }
+  return out_indexes(out, idx, n, err);
+}
+
+extern "C" int am_doc_get_changes_added(am_doc* d1, am_doc* d2, uint64_t** idx, size_t* n, am_error* err) {
+  if (!ensure_graph(d2, err)) return 1;
+  // d1's changeIndexByHash: every change once its graph exists, else the loaded heads and the
+  // changes applied since the load (new.js:1729-1739, 1820-1822)
+  std::function<bool(const Hash32&)> known;
+  std::vector<Hash32> extra;
+  if (d1->have_hash_graph) {
+    if (!ensure_graph(d1, err)) return 1;
+    known = [d1](const Hash32& h) { return d1->graph.find(h) >= 0; };
+  } else {
+    for (auto& x : d1->load_heads) extra.push_back(h32(x.data()));
+    for (auto& x : d1->hashes) extra.push_back(h32(x.data()));
+    known = [&extra](const Hash32& h) { return std::find(extra.begin(), extra.end(), h) != extra.end(); };
+  }
+  std::vector<size_t> out;
+  d2->graph.added_since(known, heads_of(d2), out);
+  return out_indexes(out, idx, n, err);
+}
+
+extern "C" int64_t am_doc_change_index(am_doc* d, const uint8_t* hash32) {
+  if (!ensure_graph(d, nullptr)) return -2;
+  return d->graph.find(h32(hash32));
+}
+
+extern "C" int am_doc_get_missing_deps(am_doc* d, const uint8_t* heads32, size_t nheads, uint8_t** out32, size_t* n,
+                                       am_error* err) {
+  if (!ensure_graph(d, err)) return 1;
+  std::vector<Hash32> all, inq;
+  for (size_t i = 0; i < nheads; i++) all.push_back(h32(heads32 + 32 * i));
+  for (size_t q = 0; q < d->queue.size(); q++) {
+    inq.push_back(h32(d->queue_hashes[q].data()));
+    ChangeMeta m;
+    if (!am_change_meta(d->queue[q].data(), d->queue[q].size(), m)) {
+      to_c(Err{AM_U_VALUE, false, "automerge_amd: unreadable queued change"}, err);
+      return 1;
+    }
+    all.insert(all.end(), m.deps.begin(), m.deps.end());
+  }
+  std::vector<Hash32> missing;
+  for (const Hash32& h : all)
+    if (d->graph.find(h) < 0 && std::find(inq.begin(), inq.end(), h) == inq.end() &&
+        std::find(missing.begin(), missing.end(), h) == missing.end())
+      missing.push_back(h);
+  std::sort(missing.begin(), missing.end());
+  *n = missing.size();
+  *out32 = static_cast<uint8_t*>(std::malloc(32 * (missing.size() ? missing.size() : 1)));
+  if (!*out32) { to_c(Err{AM_U_CAPACITY, false, "automerge_amd: out of host memory"}, err); return 1; }
+  for (size_t i = 0; i < missing.size(); i++) std::memcpy(*out32 + 32 * i, missing[i].b, 32);
+  if (err) err->code = 0;
+  return 0;
+}
+
+// clock[actor] (new.js:1857) and hashesByActor[actor][seq - 1] (new.js:1840-1841), read by
+// applyLocalChange (backend.js:54-91); a loaded document computes its hash graph first
+extern "C" int64_t am_doc_clock(am_doc* d, const char* actor_hex) {
+  if (!ensure_graph(d, nullptr)) return -1;
+  auto it = d->graph.clock.find(actor_hex);
+  return it == d->graph.clock.end() ? 0 : it->second;
+}
+extern "C" int am_doc_actor_hash(am_doc* d, const char* actor_hex, int64_t seq, uint8_t* hash32) {
+  if (!ensure_graph(d, nullptr)) return 2;
+  auto it = d->graph.by_actor.find(actor_hex);
+  if (it == d->graph.by_actor.end() || seq < 1 || (uint64_t)seq > it->second.size()) return 1;
+  static const Hash32 zero{};
+  const Hash32& h = it->second[(size_t)seq - 1];
+  if (h == zero) return 1;  // a hole (the document misses that change)
+  std::memcpy(hash32, h.b, 32);
+  return 0;
+}
+extern "C" int am_doc_change_deps(am_doc* d, size_t i, const uint8_t** deps32, size_t* n) {
+  if (!ensure_graph(d, nullptr) || i >= d->graph.meta.size()) return 1;
+  const std::vector<Hash32>& v = d->graph.meta[i].deps;
+  *deps32 = v.empty() ? nullptr : v[0].b;
+  *n = v.size();
+  return 0;
+}
+extern "C" am_engine* am_doc_engine(const am_doc* d) { return d->eng; }
 
 extern "C" int am_change_hashes(am_engine* eng, const uint8_t* const* bufs, const size_t* lens, size_t n, uint8_t* out32,
                                 am_error* err) {

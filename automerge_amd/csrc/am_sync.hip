@@ -277,6 +277,18 @@ bool gpu_ok(am_error* err, hipError_t e, const char* what) {
 }  // namespace
 
 extern "C" uint64_t am_bloom_encoded_size(uint64_t nhashes) { return bloom_size(nhashes); }
+// new BloomFilter(bytes) header check on the host (sync.js:47-58): 0 when well formed, else the
+// RangeError the reference raises (the sync protocol decodes every `have` filter before it
+// selects changes, sync.js:252-256)
+extern "C" int am_bloom_check(const uint8_t* f, uint64_t len, am_error* err) {
+  if (err) err->code = 0;
+  uint64_t pos, nbytes;
+  uint32_t ne, np;
+  uint8_t e = bloom_header(f, len, pos, ne, np, nbytes);
+  if (!e && ne && nbytes && np > BLOOM_MAX_PROBES) e = BP_TOO_MANY;
+  return probe_error(e, err) ? 1 : 0;
+}
+
 
 void am_launch_bloom_build(const uint8_t* d_hashes, const uint64_t* d_hoff, uint32_t nfilt, uint8_t* d_out,
                            const uint64_t* d_foff, hipStream_t s) {

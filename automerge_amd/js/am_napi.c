@@ -354,6 +354,311 @@ static napi_value js_change_hashes(napi_env env, napi_callback_info info) {
   return v;
 }
 
+// ---- hash-graph queries, local changes and sync (include/automerge_amd.h) ----
+#define ARGS(n)                                                  \
+  size_t argc = (n);                                             \
+  napi_value argv[(n) > 0 ? (n) : 1];                            \
+  NAPI_OK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+
+// throws the engine error; `applied` marks an error raised after the document changed
+static napi_value throw_am2(napi_env env, const am_error* e, int applied) {
+  napi_value msg, err, t;
+  NAPI_OK(napi_create_string_utf8(env, e->message, NAPI_AUTO_LENGTH, &msg));
+  if (e->is_type_error) NAPI_OK(napi_create_type_error(env, NULL, msg, &err));
+  else NAPI_OK(napi_create_range_error(env, NULL, msg, &err));
+  if (applied) {
+    NAPI_OK(napi_get_boolean(env, true, &t));
+    NAPI_OK(napi_set_named_property(env, err, "applied", t));
+  }
+  napi_throw(env, err);
+  return NULL;
+}
+
+static char* get_string(napi_env env, napi_value v, size_t* len) {
+  if (napi_get_value_string_utf8(env, v, NULL, 0, len) != napi_ok) {
+    napi_throw_type_error(env, NULL, "automerge_amd: expected a string");
+    return NULL;
+  }
+  char* s = (char*)malloc(*len + 1);
+  napi_get_value_string_utf8(env, v, s, *len + 1, len);
+  return s;
+}
+
+static int arg_bytes(napi_env env, napi_value v, const uint8_t** p, size_t* n) {
+  if (!get_bytes(env, v, p, n)) {
+    napi_throw_type_error(env, NULL, "automerge_amd: expected a Uint8Array");
+    return 0;
+  }
+  return 1;
+}
+
+static napi_value change_list(napi_env env, am_doc* d, const uint64_t* idx, size_t n) {
+  napi_value arr;
+  NAPI_OK(napi_create_array_with_length(env, n, &arr));
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t* data;
+    size_t len;
+    if (am_doc_change(d, (size_t)idx[i], &data, &len, NULL)) {
+      napi_throw_range_error(env, NULL, "automerge_amd: change index out of range");
+      return NULL;
+    }
+    NAPI_OK(napi_set_element(env, arr, (uint32_t)i, new_u8(env, data, len)));
+  }
+  return arr;
+}
+
+// getChanges(handle, flatHaveHashes) -> [Uint8Array]
+static napi_value js_doc_get_changes(napi_env env, napi_callback_info info) {
+  ARGS(2)
+  DocBox* b = get_box(env, argv[0]);
+  const uint8_t* h;
+  size_t hl;
+  if (!b || !arg_bytes(env, argv[1], &h, &hl)) return NULL;
+  uint64_t* idx = NULL;
+  size_t n = 0;
+  am_error err;
+  if (am_doc_get_changes(b->doc, h, hl / 32, &idx, &n, &err)) return throw_am(env, &err);
+  napi_value v = change_list(env, b->doc, idx, n);
+  am_free(idx);
+  return v;
+}
+
+// getChangesAdded(handle1, handle2) -> [Uint8Array]
+static napi_value js_doc_get_changes_added(napi_env env, napi_callback_info info) {
+  ARGS(2)
+  DocBox* b1 = get_box(env, argv[0]);
+  DocBox* b2 = b1 ? get_box(env, argv[1]) : NULL;
+  if (!b2) return NULL;
+  uint64_t* idx = NULL;
+  size_t n = 0;
+  am_error err;
+  if (am_doc_get_changes_added(b1->doc, b2->doc, &idx, &n, &err)) return throw_am(env, &err);
+  napi_value v = change_list(env, b2->doc, idx, n);
+  am_free(idx);
+  return v;
+}
+
+// changeByHash(handle, hash32) -> Uint8Array | undefined
+static napi_value js_doc_change_by_hash(napi_env env, napi_callback_info info) {
+  ARGS(2)
+  DocBox* b = get_box(env, argv[0]);
+  const uint8_t* h;
+  size_t hl;
+  if (!b || !arg_bytes(env, argv[1], &h, &hl)) return NULL;
+  napi_value undef;
+  NAPI_OK(napi_get_undefined(env, &undef));
+  if (hl != 32) return undef;
+  const int64_t i = am_doc_change_index(b->doc, h);
+  if (i == -2) {
+    napi_throw_range_error(env, NULL, "automerge_amd: the document history could not be reconstructed");
+    return NULL;
+  }
+  if (i < 0) return undef;
+  uint64_t one = (uint64_t)i;
+  napi_value arr = change_list(env, b->doc, &one, 1), el;
+  if (!arr) return NULL;
+  NAPI_OK(napi_get_element(env, arr, 0, &el));
+  return el;
+}
+
+// missingDeps(handle, flatHeads) -> Uint8Array (sorted 32-byte hashes)
+static napi_value js_doc_missing_deps(napi_env env, napi_callback_info info) {
+  ARGS(2)
+  DocBox* b = get_box(env, argv[0]);
+  const uint8_t* h;
+  size_t hl;
+  if (!b || !arg_bytes(env, argv[1], &h, &hl)) return NULL;
+  uint8_t* out = NULL;
+  size_t n = 0;
+  am_error err;
+  if (am_doc_get_missing_deps(b->doc, h, hl / 32, &out, &n, &err)) return throw_am(env, &err);
+  napi_value v = new_u8(env, out, 32 * n);
+  am_free(out);
+  return v;
+}
+
+// applyLocal(handle, json) -> {change, patch, newHash, lastHash|null}
+static napi_value js_doc_apply_local(napi_env env, napi_callback_info info) {
+  ARGS(2)
+  DocBox* b = get_box(env, argv[0]);
+  if (!b) return NULL;
+  size_t jl;
+  char* js = get_string(env, argv[1], &jl);
+  if (!js) return NULL;
+  uint8_t *change = NULL, *patch = NULL, nh[32], lh[32];
+  size_t cl = 0, pl = 0;
+  int has_last = 0;
+  am_error err;
+  const int rc = am_doc_apply_local_change(b->doc, js, jl, &change, &cl, &patch, &pl, nh, lh, &has_last, &err);
+  free(js);
+  if (rc) return throw_am2(env, &err, rc == 2);
+  napi_value o, nul;
+  NAPI_OK(napi_create_object(env, &o));
+  NAPI_OK(napi_get_null(env, &nul));
+  NAPI_OK(napi_set_named_property(env, o, "change", new_u8(env, change, cl)));
+  NAPI_OK(napi_set_named_property(env, o, "patch", new_u8(env, patch, pl)));
+  NAPI_OK(napi_set_named_property(env, o, "newHash", hex_list(env, nh, 1)));
+  NAPI_OK(napi_set_named_property(env, o, "lastHash", has_last ? hex_list(env, lh, 1) : nul));
+  am_free(change);
+  am_free(patch);
+  return o;
+}
+
+// encodeChange(json) -> Uint8Array
+static napi_value js_encode_change(napi_env env, napi_callback_info info) {
+  ARGS(1)
+  size_t jl;
+  char* js = get_string(env, argv[0], &jl);
+  if (!js) return NULL;
+  uint8_t* out = NULL;
+  size_t n = 0;
+  am_error err;
+  const int rc = am_encode_change(js, jl, &out, &n, NULL, &err);
+  free(js);
+  if (rc) return throw_am(env, &err);
+  napi_value v = new_u8(env, out, n);
+  am_free(out);
+  return v;
+}
+
+// syncGenerate([handle...], [stateBlob...]) -> [[stateBlob, message|null] | Error]
+static napi_value js_sync_generate(napi_env env, napi_callback_info info) {
+  ARGS(2)
+  uint32_t n = 0;
+  NAPI_OK(napi_get_array_length(env, argv[0], &n));
+  am_doc** docs = (am_doc**)calloc(n ? n : 1, sizeof(am_doc*));
+  const uint8_t** st = (const uint8_t**)calloc(n ? n : 1, sizeof(uint8_t*));
+  size_t* sl = (size_t*)calloc(n ? n : 1, sizeof(size_t));
+  uint8_t** ost = (uint8_t**)calloc(n ? n : 1, sizeof(uint8_t*));
+  size_t* osl = (size_t*)calloc(n ? n : 1, sizeof(size_t));
+  uint8_t** msg = (uint8_t**)calloc(n ? n : 1, sizeof(uint8_t*));
+  size_t* ml = (size_t*)calloc(n ? n : 1, sizeof(size_t));
+  am_error* errs = (am_error*)calloc(n ? n : 1, sizeof(am_error));
+  napi_value res = NULL;
+  int ok = 1;
+  for (uint32_t i = 0; i < n && ok; i++) {
+    napi_value hv, sv;
+    DocBox* b;
+    ok = napi_get_element(env, argv[0], i, &hv) == napi_ok && (b = get_box(env, hv)) != NULL &&
+         napi_get_element(env, argv[1], i, &sv) == napi_ok && arg_bytes(env, sv, &st[i], &sl[i]);
+    if (ok) docs[i] = b->doc;
+  }
+  if (ok) {
+    am_sync_generate(n, docs, st, sl, ost, osl, msg, ml, errs);
+    napi_create_array_with_length(env, n, &res);
+    for (uint32_t i = 0; i < n; i++) {
+      napi_value el;
+      if (errs[i].code) {
+        napi_value m;
+        napi_create_string_utf8(env, errs[i].message, NAPI_AUTO_LENGTH, &m);
+        if (errs[i].is_type_error) napi_create_type_error(env, NULL, m, &el);
+        else napi_create_range_error(env, NULL, m, &el);
+      } else {
+        napi_value nul;
+        napi_get_null(env, &nul);
+        napi_create_array_with_length(env, 2, &el);
+        napi_set_element(env, el, 0, new_u8(env, ost[i], osl[i]));
+        napi_set_element(env, el, 1, msg[i] ? new_u8(env, msg[i], ml[i]) : nul);
+      }
+      napi_set_element(env, res, i, el);
+      am_free(ost[i]);
+      am_free(msg[i]);
+    }
+  }
+  free(docs); free(st); free(sl); free(ost); free(osl); free(msg); free(ml); free(errs);
+  return res;
+}
+
+// syncReceive(handle, stateBlob, message) -> [stateBlob, patch|null]
+static napi_value js_sync_receive(napi_env env, napi_callback_info info) {
+  ARGS(3)
+  DocBox* b = get_box(env, argv[0]);
+  const uint8_t *st, *m;
+  size_t sl, ml;
+  if (!b || !arg_bytes(env, argv[1], &st, &sl) || !arg_bytes(env, argv[2], &m, &ml)) return NULL;
+  uint8_t *ost = NULL, *patch = NULL;
+  size_t osl = 0, pl = 0;
+  am_error err;
+  const int rc = am_sync_receive(b->doc, st, sl, m, ml, &ost, &osl, &patch, &pl, &err);
+  if (rc) return throw_am2(env, &err, rc == 2);
+  napi_value o, nul;
+  NAPI_OK(napi_get_null(env, &nul));
+  NAPI_OK(napi_create_array_with_length(env, 2, &o));
+  NAPI_OK(napi_set_element(env, o, 0, new_u8(env, ost, osl)));
+  NAPI_OK(napi_set_element(env, o, 1, patch ? new_u8(env, patch, pl) : nul));
+  am_free(ost);
+  am_free(patch);
+  return o;
+}
+
+static napi_value js_sync_encode_message(napi_env env, napi_callback_info info) {
+  ARGS(1)
+  size_t jl;
+  char* js = get_string(env, argv[0], &jl);
+  if (!js) return NULL;
+  uint8_t* out = NULL;
+  size_t n = 0;
+  am_error err;
+  const int rc = am_sync_encode_message(js, jl, &out, &n, &err);
+  free(js);
+  if (rc) return throw_am(env, &err);
+  napi_value v = new_u8(env, out, n);
+  am_free(out);
+  return v;
+}
+
+// syncDecodeMessage(bytes) -> {heads: flat, need: flat, have: [{lastSync: flat, bloom}], changes: [u8]}
+static napi_value js_sync_decode_message(napi_env env, napi_callback_info info) {
+  ARGS(1)
+  const uint8_t* m;
+  size_t ml;
+  if (!arg_bytes(env, argv[0], &m, &ml)) return NULL;
+  am_span* sp = NULL;
+  uint64_t off[2];
+  uint32_t cnt[4];
+  am_error err;
+  if (am_sync_decode_messages(1, &m, &ml, &sp, off, cnt, &err)) {
+    am_free(sp);
+    return throw_am(env, &err);
+  }
+  napi_value o, have, changes;
+  NAPI_OK(napi_create_object(env, &o));
+  size_t k = 0;
+  NAPI_OK(napi_set_named_property(env, o, "heads", new_u8(env, m + sp[k].off, 32 * sp[k].len))); k++;
+  NAPI_OK(napi_set_named_property(env, o, "need", new_u8(env, m + sp[k].off, 32 * sp[k].len))); k++;
+  NAPI_OK(napi_create_array_with_length(env, cnt[2], &have));
+  for (uint32_t i = 0; i < cnt[2]; i++, k += 2) {
+    napi_value h;
+    NAPI_OK(napi_create_object(env, &h));
+    NAPI_OK(napi_set_named_property(env, h, "lastSync", new_u8(env, m + sp[k].off, 32 * sp[k].len)));
+    NAPI_OK(napi_set_named_property(env, h, "bloom", new_u8(env, m + sp[k + 1].off, sp[k + 1].len)));
+    NAPI_OK(napi_set_element(env, have, i, h));
+  }
+  NAPI_OK(napi_create_array_with_length(env, cnt[3], &changes));
+  for (uint32_t i = 0; i < cnt[3]; i++, k++) NAPI_OK(napi_set_element(env, changes, i, new_u8(env, m + sp[k].off, sp[k].len)));
+  NAPI_OK(napi_set_named_property(env, o, "have", have));
+  NAPI_OK(napi_set_named_property(env, o, "changes", changes));
+  am_free(sp);
+  return o;
+}
+
+static napi_value js_sync_state_conv(napi_env env, napi_callback_info info, int encode) {
+  ARGS(1)
+  const uint8_t* p;
+  size_t n;
+  if (!arg_bytes(env, argv[0], &p, &n)) return NULL;
+  uint8_t* out = NULL;
+  size_t on = 0;
+  am_error err;
+  if (encode ? am_sync_encode_state(p, n, &out, &on, &err) : am_sync_decode_state(p, n, &out, &on, &err))
+    return throw_am(env, &err);
+  napi_value v = new_u8(env, out, on);
+  am_free(out);
+  return v;
+}
+static napi_value js_sync_encode_state(napi_env env, napi_callback_info info) { return js_sync_state_conv(env, info, 1); }
+static napi_value js_sync_decode_state(napi_env env, napi_callback_info info) { return js_sync_state_conv(env, info, 0); }
+
 static napi_value js_version(napi_env env, napi_callback_info info) {
   (void)info;
   napi_value v;
@@ -375,6 +680,18 @@ static napi_value init_module(napi_env env, napi_value exports) {
       {"docPatch", 0, js_doc_patch, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
       {"docQueued", 0, js_doc_queued, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
       {"changeHashes", 0, js_change_hashes, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docGetChanges", 0, js_doc_get_changes, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docGetChangesAdded", 0, js_doc_get_changes_added, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docChangeByHash", 0, js_doc_change_by_hash, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docMissingDeps", 0, js_doc_missing_deps, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docApplyLocal", 0, js_doc_apply_local, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"encodeChange", 0, js_encode_change, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"syncGenerate", 0, js_sync_generate, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"syncReceive", 0, js_sync_receive, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"syncEncodeMessage", 0, js_sync_encode_message, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"syncDecodeMessage", 0, js_sync_decode_message, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"syncEncodeState", 0, js_sync_encode_state, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"syncDecodeState", 0, js_sync_decode_state, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
       {"version", 0, js_version, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
   };
   if (napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props) != napi_ok) return NULL;

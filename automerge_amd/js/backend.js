@@ -9,16 +9,17 @@
  * is reached through the N-API addon am_napi.node (am_napi.c); there is no JS or CPU fallback:
  * if the addon or the HIP device is missing, require() or the first call throws.
  *
- * Hash-graph queries (getChanges, getChangesAdded, getChangeByHash, getMissingDeps) are host
- * traversals over the applied change buffers, as in new.js:1913-2020.
+ * Hash-graph queries (getChanges, getChangesAdded, getChangeByHash, getMissingDeps) run in the
+ * engine over the document's change graph (am_graph.cpp, new.js:1913-2020); applyLocalChange
+ * encodes the request (am_local.cpp, columnar.js:710-739) and applies it on the GPU; the seven sync
+ * functions of backend/index.js run the protocol of sync.js in the engine (am_sync_proto.cpp), with
+ * Bloom filters and change selection in HIP kernels (am_sync.hip).
  * getPatch runs documentPatch on the GPU, applyChanges replays the patch of the call on the GPU
  * (k_doc phase P8, am_diff.h); both logs are materialized here.
  * The change history of a loaded document is reconstructed from save() on first use
  * (computeHashGraph, new.js:1879-1904; am_document_changes, 8(f) row 2).
- * Not on the GPU path yet: applyLocalChange (8(f) row 3); it throws.
  */
 const path = require('path')
-const zlib = require('zlib')
 const native = require(process.env.AM_NAPI_PATH || path.join(__dirname, 'am_napi.node'))
 
 const FROZEN_MESSAGE =
@@ -54,11 +55,6 @@ function applyChanges(backend, changes) {
   const heads = native.docHeads(state)
   const c = native.docCounts(state)
   return [{state, heads}, materializePatch(log, heads, c.pending, c.maxOp)]
-}
-
-function applyLocalChange(backend) {
-  backendState(backend)
-  throw new RangeError('automerge_amd: applyLocalChange is not implemented by this backend')
 }
 
 function save(backend) {
@@ -183,137 +179,236 @@ function getHeads(backend) {
   return backend.heads
 }
 
-// ---- hash graph (host side) ----
-function readUleb(buf, pos) {
-  let v = 0, mul = 1, b
-  do {
-    b = buf[pos++]
-    v += (b & 0x7f) * mul
-    mul *= 128
-  } while (b & 0x80)
-  return [v, pos]
-}
-
 function toHex(bytes) {
   return Buffer.from(bytes.buffer, bytes.byteOffset, bytes.byteLength).toString('hex')
 }
 
-// dependency hashes of a change chunk (decodeChangeMeta, columnar.js:768-811)
-function changeDeps(bytes) {
-  const type = bytes[8]
-  let [len, pos] = readUleb(bytes, 9)
-  let body = bytes.subarray(pos, pos + len)
-  if (type === 2) body = zlib.inflateRawSync(body)
-  let [n, q] = readUleb(body, 0)
-  const deps = []
-  for (let i = 0; i < n; i++, q += 32) deps.push(toHex(body.subarray(q, q + 32)))
-  return deps
-}
-
-function hashGraph(state) {
-  const changes = native.docChanges(state)
-  const index = {}, depsOf = {}, dependents = {}
-  changes.forEach((c, i) => {
-    index[c.hash] = i
-    depsOf[c.hash] = changeDeps(c.bytes)
-    dependents[c.hash] = []
-  })
-  for (const c of changes) {
-    for (const d of depsOf[c.hash]) {
-      if (!dependents[d]) dependents[d] = []
-      dependents[d].push(c.hash)
+// ---- hashes across the addon: hex strings <-> one flat Uint8Array of 32-byte hashes ----
+const HASH_RE = /^[0-9a-f]{64}$/
+// A string that is not a hash can never be found; it travels as a sentinel the engine does not
+// know (0xff x 28 + its index) and is mapped back where a result or an error names it.
+function flatHashes(list) {
+  const out = new Uint8Array(32 * list.length), odd = new Map()
+  list.forEach((h, i) => {
+    if (typeof h === 'string' && HASH_RE.test(h)) out.set(Buffer.from(h, 'hex'), 32 * i)
+    else {
+      out.fill(0xff, 32 * i, 32 * i + 28)
+      new DataView(out.buffer).setUint32(32 * i + 28, i)
+      odd.set(toHex(out.subarray(32 * i, 32 * i + 32)), h)
     }
-  }
-  return {changes, index, depsOf, dependents, heads: native.docHeads(state)}
+  })
+  return [out, odd]
+}
+const hexList = flat => { const r = []; for (let i = 0; i < flat.length; i += 32) r.push(toHex(flat.subarray(i, i + 32))); return r }
+function rethrowNamed(e, odd) {
+  for (const [k, v] of odd) if (e.message.includes(k)) e.message = e.message.replace(k, String(v))
+  throw e
 }
 
-// BackendDoc.getChanges (new.js:1913-1966)
+// BackendDoc.getChanges (new.js:1913-1966): the traversal runs in the engine (am_doc_get_changes)
 function getChanges(backend, haveDeps) {
   if (!Array.isArray(haveDeps)) {
     throw new TypeError('Pass an array of hashes to Backend.getChanges()')
   }
-  const g = hashGraph(backendState(backend))
-  if (haveDeps.length === 0) return g.changes.map(c => c.bytes)
-
-  let stack = [], seen = {}, toReturn = []
-  for (const hash of haveDeps) {
-    seen[hash] = true
-    const succ = g.dependents[hash]
-    if (!succ) throw new RangeError(`hash not found: ${hash}`)
-    stack.push(...succ)
-  }
-  while (stack.length > 0) {
-    const hash = stack.pop()
-    seen[hash] = true
-    toReturn.push(hash)
-    if (!g.depsOf[hash].every(dep => seen[dep])) break
-    stack.push(...g.dependents[hash])
-  }
-  if (stack.length === 0 && g.heads.every(head => seen[head])) {
-    return toReturn.map(hash => g.changes[g.index[hash]].bytes)
-  }
-  stack = haveDeps.slice()
-  seen = {}
-  while (stack.length > 0) {
-    const hash = stack.pop()
-    if (!seen[hash]) {
-      const deps = g.depsOf[hash]
-      if (!deps) throw new RangeError(`hash not found: ${hash}`)
-      stack.push(...deps)
-      seen[hash] = true
-    }
-  }
-  return g.changes.filter(c => !seen[c.hash]).map(c => c.bytes)
+  const [flat, odd] = flatHashes(haveDeps)
+  try { return native.docGetChanges(backendState(backend), flat) } catch (e) { rethrowNamed(e, odd) }
 }
 
 function getAllChanges(backend) {
   return getChanges(backend, [])
 }
 
-// BackendDoc.getChangesAdded (new.js:1971-1988)
+// BackendDoc.getChangesAdded (new.js:1971-1988): changes of backend2 that backend1 lacks
 function getChangesAdded(backend1, backend2) {
-  const other = hashGraph(backendState(backend1))
-  const g = hashGraph(backendState(backend2))
-  let stack = g.heads.slice(), seen = {}, toReturn = []
-  while (stack.length > 0) {
-    const hash = stack.pop()
-    if (!seen[hash] && other.index[hash] === undefined) {
-      seen[hash] = true
-      toReturn.push(hash)
-      stack.push(...g.depsOf[hash])
-    }
-  }
-  return toReturn.reverse().map(hash => g.changes[g.index[hash]].bytes)
+  return native.docGetChangesAdded(backendState(backend1), backendState(backend2))
 }
 
 // BackendDoc.getChangeByHash (new.js:1990-1993)
 function getChangeByHash(backend, hash) {
-  const g = hashGraph(backendState(backend))
-  const i = g.index[hash]
-  return i === undefined ? undefined : g.changes[i].bytes
+  const state = backendState(backend)
+  if (typeof hash !== 'string' || !HASH_RE.test(hash)) return undefined
+  return native.docChangeByHash(state, Buffer.from(hash, 'hex'))
 }
 
 // BackendDoc.getMissingDeps (new.js:2005-2020)
 function getMissingDeps(backend, heads = []) {
   const state = backendState(backend)
-  const g = hashGraph(state)
-  const queued = native.docQueued(state)
-  const qhashes = queued.length ? native.changeHashes(queued) : []
-  const allDeps = new Set(heads), inQueue = new Set()
-  queued.forEach((bytes, i) => {
-    inQueue.add(qhashes[i])
-    for (const dep of changeDeps(bytes)) allDeps.add(dep)
+  const [flat, odd] = flatHashes(Array.from(heads))
+  const missing = hexList(native.docMissingDeps(state, flat)).map(h => odd.has(h) ? odd.get(h) : h)
+  return odd.size ? missing.sort() : missing
+}
+
+// ---- applyLocalChange (backend.js:54-91): encodeChange + applyChanges(isLocal) in the engine ----
+// Uint8Array values and non-finite numbers cross as {__bytes} / {__f64} (include/automerge_amd.h)
+function requestJSON(change) {
+  return JSON.stringify(change, function (key, value) {
+    const raw = this[key]
+    // encodeValue takes the whole buffer of a value view (columnar.js:269-271); other bytes are the view
+    if (ArrayBuffer.isView(raw)) {
+      return {__bytes: toHex(key === 'value' ? new Uint8Array(raw.buffer) : new Uint8Array(raw.buffer, raw.byteOffset, raw.byteLength))}
+    }
+    if (typeof raw === 'number' && !Number.isFinite(raw)) return {__f64: String(raw)}
+    return value
   })
-  const missing = []
-  for (const hash of allDeps) {
-    if (g.index[hash] === undefined && !inQueue.has(hash)) missing.push(hash)
+}
+
+function applyLocalChange(backend, change) {
+  const state = backendState(backend)
+  let r
+  try {
+    r = native.docApplyLocal(state, requestJSON(change))
+  } catch (e) {
+    if (e.applied) backend.frozen = true
+    throw e
   }
-  return missing.sort()
+  // the request's deps gain the local actor's previous change, as in the reference (backend.js:80)
+  if (r.lastHash) {
+    const deps = {[r.lastHash[0]]: true}
+    for (const hash of change.deps) deps[hash] = true
+    change.deps = Object.keys(deps).sort()
+  }
+  backend.frozen = true
+  const heads = native.docHeads(state)
+  const c = native.docCounts(state)
+  const patch = materializePatch(r.patch, heads, c.pending, c.maxOp)
+  patch.actor = change.actor
+  patch.seq = change.seq
+  patch.deps = patch.deps.filter(head => head !== r.newHash[0])
+  return [{state, heads}, patch, r.change]
+}
+
+// ---- sync protocol (backend/sync.js) in the engine (am_sync_*); SyncState objects cross as the
+// flat state blob of include/automerge_amd.h ----
+function bytesOf(x) {
+  if (x instanceof Uint8Array) return x
+  throw new TypeError(`Not a byte array: ${x}`)
+}
+function checkedHash(h) {  // hexStringToBytes + the 256-bit check of encodeHashes (sync.js:130-139)
+  if (typeof h !== 'string') throw new TypeError('value is not a string')
+  if (!/^([0-9a-f][0-9a-f])*$/.test(h)) throw new RangeError('value is not hexadecimal')
+  if (h.length !== 64) throw new TypeError('heads hashes must be 256 bits')
+  return Buffer.from(h, 'hex')
+}
+function packState(s) {
+  const out = []
+  const uleb = v => { do { let b = v % 128; v = Math.floor(v / 128); out.push(v ? b | 0x80 : b) } while (v) }
+  const hashes = list => {
+    if (!Array.isArray(list)) throw new TypeError('hashes must be an array')
+    uleb(list.length)
+    for (const h of list) out.push(...checkedHash(h))
+  }
+  const sent = s.sentHashes
+  const sentKeys = sent && typeof sent === 'object' ? Object.keys(sent).filter(k => HASH_RE.test(k)) : []
+  const flags = (s.theirHeads ? 1 : 0) | (s.theirNeed ? 2 : 0) | (s.theirHave ? 4 : 0) | (Array.isArray(sent) ? 8 : 0)
+  out.push(0x53, flags)
+  hashes(s.sharedHeads)
+  hashes(s.lastSentHeads)
+  if (s.theirHeads) hashes(s.theirHeads)
+  if (s.theirNeed) hashes(s.theirNeed)
+  if (s.theirHave) {
+    uleb(s.theirHave.length)
+    for (const h of s.theirHave) {
+      hashes(h.lastSync)
+      const b = bytesOf(h.bloom)
+      uleb(b.byteLength)
+      for (const x of b) out.push(x)
+    }
+  }
+  uleb(sentKeys.length)
+  for (const h of sentKeys) out.push(...Buffer.from(h, 'hex'))
+  return Uint8Array.from(out)
+}
+function unpackState(b) {
+  let o = 2
+  const u = () => { let v = 0, mul = 1, x; do { x = b[o++]; v += (x & 0x7f) * mul; mul *= 128 } while (x & 0x80); return v }
+  const hashes = () => { const n = u(), r = []; for (let i = 0; i < n; i++, o += 32) r.push(toHex(b.subarray(o, o + 32))); return r }
+  const flags = b[1]
+  const s = {sharedHeads: hashes(), lastSentHeads: hashes(), theirHeads: null, theirNeed: null, theirHave: null}
+  if (flags & 1) s.theirHeads = hashes()
+  if (flags & 2) s.theirNeed = hashes()
+  if (flags & 4) {
+    s.theirHave = []
+    for (let n = u(), i = 0; i < n; i++) {
+      const lastSync = hashes(), len = u()
+      s.theirHave.push({lastSync, bloom: b.slice(o, o + len)})
+      o += len
+    }
+  }
+  const sent = hashes()
+  if (flags & 8) s.sentHashes = []
+  else { s.sentHashes = {}; for (const h of sent) s.sentHashes[h] = true }
+  return s
+}
+
+function initSyncState() {
+  return {sharedHeads: [], lastSentHeads: [], theirHeads: null, theirNeed: null, theirHave: null, sentHashes: {}}
+}
+
+function encodeSyncMessage(message) {
+  if (message === undefined || message === null) throw new TypeError(`Cannot read property 'heads' of ${message}`)
+  return native.syncEncodeMessage(requestJSON(message))
+}
+
+function decodeSyncMessage(bytes) {
+  const m = native.syncDecodeMessage(bytesOf(bytes))
+  return {heads: hexList(m.heads), need: hexList(m.need),
+          have: m.have.map(h => ({lastSync: hexList(h.lastSync), bloom: h.bloom})), changes: m.changes}
+}
+
+function encodeSyncState(syncState) {
+  return native.syncEncodeState(packState({sharedHeads: syncState.sharedHeads, lastSentHeads: []}))
+}
+
+function decodeSyncState(bytes) {
+  return unpackState(native.syncDecodeState(bytesOf(bytes)))
+}
+
+function generateSyncMessage(backend, syncState) {
+  if (!backend) throw new Error('generateSyncMessage called with no Automerge document')
+  if (!syncState) throw new Error('generateSyncMessage requires a syncState, which can be created with initSyncState()')
+  const packed = packState(syncState)
+  const [r] = native.syncGenerate([backendState(backend)], [packed])
+  if (r instanceof Error) throw r
+  const [blob, message] = r
+  if (message === null || Buffer.compare(Buffer.from(blob), Buffer.from(packed)) === 0) return [syncState, message]
+  const next = unpackState(blob)
+  return [Object.assign({}, syncState, {lastSentHeads: next.lastSentHeads, sentHashes: next.sentHashes}), message]
+}
+
+function receiveSyncMessage(backend, oldSyncState, binaryMessage) {
+  if (!backend) throw new Error('generateSyncMessage called with no Automerge document')
+  if (!oldSyncState) throw new Error('generateSyncMessage requires a syncState, which can be created with initSyncState()')
+  const message = decodeSyncMessage(binaryMessage)
+  // the reference reaches backendState() through applyChanges / getChangeByHash
+  const state = (message.changes.length > 0 || message.heads.length > 0) ? backendState(backend) : backend.state
+  let r
+  try {
+    r = native.syncReceive(state, packState(oldSyncState), binaryMessage)
+  } catch (e) {
+    if (e.applied) backend.frozen = true
+    throw e
+  }
+  let patch = null
+  if (message.changes.length > 0) {
+    backend.frozen = true
+    backend = {state, heads: native.docHeads(state)}
+    const c = native.docCounts(state)
+    patch = materializePatch(r[1], backend.heads, c.pending, c.maxOp)
+  }
+  const s = unpackState(r[0])
+  const syncState = {sharedHeads: s.sharedHeads, lastSentHeads: s.lastSentHeads, theirHave: message.have,
+                     theirHeads: message.heads, theirNeed: message.need, sentHashes: s.sentHashes}
+  // receiveSyncMessage keeps sentHashes unless the peer reset (sync.js:455-458)
+  if (!Array.isArray(s.sentHashes)) syncState.sentHashes = oldSyncState.sentHashes
+  return [backend, syncState, patch]
 }
 
 module.exports = {
   init, clone, free, applyChanges, applyLocalChange, save, load, loadChanges, getPatch,
   getHeads, getAllChanges, getChanges, getChangesAdded, getChangeByHash, getMissingDeps,
+  receiveSyncMessage, generateSyncMessage, encodeSyncMessage, decodeSyncMessage, encodeSyncState, decodeSyncState,
+  initSyncState,
+  encodeChange: change => native.encodeChange(requestJSON(change)),  // columnar.js encodeChange (tests)
   engineVersion: native.version,
   _materializePatch: materializePatch  // host stage of getPatch (exported for tests)
 }

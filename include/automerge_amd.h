@@ -68,6 +68,7 @@ enum am_status {
   AM_E_FLOAT_LEN = 31,      // Invalid length for floating point number: %a0 (getPatch)
   AM_E_UNKNOWN_COUNTER = 32,// increment operation %a0@%s for unknown counter (getPatch)
   AM_E_HISTORY = 33,        // RangeError of decodeDocument / groupChangeOps / decodeDocumentChanges (message as given)
+  AM_E_LOCAL = 34,          // error of encodeChange / applyLocalChange / the sync functions (class + message as given)
   AM_U_HASH_GRAPH = 100,    // needs the deferred hash graph of a loaded document (new.js:1826-1832)
   AM_U_UNKNOWN_COLUMN,      // column id outside DOC_OPS_COLUMNS / CHANGE_COLUMNS (new.js:1387-1425)
   AM_U_NONCAUSAL,           // opId counters violate Lamport order (insert after a later element, ...)
@@ -270,6 +271,75 @@ int am_doc_change(const am_doc *doc, size_t i, const uint8_t **data, size_t *len
 int am_doc_get_patch(am_doc *doc, uint8_t **out, size_t *len, am_error *err);
 /* i-th enqueued change (this.queue, new.js:1796-1871: changes waiting for missing deps), as given */
 int am_doc_queued(const am_doc *doc, size_t i, const uint8_t **data, size_t *len);
+/* ---- hash-graph queries (BackendDoc, new.js:1913-2020); the graph of a loaded document is
+ * computed on first use (computeHashGraph, new.js:1879-1904). Change indexes refer to
+ * am_doc_change; arrays are malloc'd (am_free). ----
+ * am_doc_get_changes       <- getChanges(haveDeps)        new.js:1913-1966 ("hash not found: <hex>")
+ * am_doc_get_changes_added <- getChangesAdded(doc1, doc2) new.js:1971-1988 (indexes into doc2)
+ * am_doc_change_index      <- getChangeByHash             new.js:1990-1993 (-1: unknown, -2: error)
+ * am_doc_get_missing_deps  <- getMissingDeps(heads)       new.js:2005-2020 (sorted hashes) */
+int am_doc_get_changes(am_doc *doc, const uint8_t *have32, size_t nhave, uint64_t **idx, size_t *n, am_error *err);
+int am_doc_get_changes_added(am_doc *doc1, am_doc *doc2, uint64_t **idx, size_t *n, am_error *err);
+int64_t am_doc_change_index(am_doc *doc, const uint8_t *hash32);
+int am_doc_get_missing_deps(am_doc *doc, const uint8_t *heads32, size_t nheads, uint8_t **out32, size_t *n, am_error *err);
+/* ---- per-actor state of a document (read by applyLocalChange) ----
+ * am_doc_clock       <- state.clock[actor]                 new.js:1857 (0: no entry; -1: error)
+ * am_doc_actor_hash  <- state.hashesByActor[actor][seq-1]  new.js:1840-1841 (0 ok, 1 unknown)
+ * am_doc_change_deps <- dependenciesByHash of change i      new.js:1843 (pointer valid until the next call)
+ * am_doc_engine      -- the engine a document runs on */
+int64_t am_doc_clock(am_doc *doc, const char *actor_hex);
+int am_doc_actor_hash(am_doc *doc, const char *actor_hex, int64_t seq, uint8_t *hash32);
+int am_doc_change_deps(am_doc *doc, size_t i, const uint8_t **deps32, size_t *n);
+am_engine *am_doc_engine(const am_doc *doc);
+
+/* ---- local changes ----
+ * Requests are the frontend's change objects as JSON text; a Uint8Array travels as
+ * {"__bytes":"<hex>"} and a non-finite number as {"__f64":"NaN"|"Infinity"|"-Infinity"}.
+ * am_encode_change          <- encodeChange(change)               columnar.js:710-739
+ *     out: the binary change (DEFLATE'd when >= 256 B, malloc'd); hash32: its hash
+ * am_doc_apply_local_change <- Backend.applyLocalChange(backend, change)  backend.js:54-91
+ *     out: the binary change, the patch log (wire form, am_patch.h), new_hash32 = the hash the
+ *     patch's deps omit, last_hash32 (*has_last) = the local actor's previous change that joined
+ *     the request's deps. Returns 0; 1 on an error before the document changed; 2 on the error
+ *     the reference raises after applying (the caller's handle must be treated as updated). */
+int am_encode_change(const char *json, size_t len, uint8_t **out, size_t *out_len, uint8_t *hash32, am_error *err);
+int am_doc_apply_local_change(am_doc *doc, const char *json, size_t len, uint8_t **change, size_t *change_len,
+                              uint8_t **patch, size_t *patch_len, uint8_t *new_hash32, uint8_t *last_hash32,
+                              int *has_last, am_error *err);
+
+/* ---- sync protocol (backend/sync.js) ----
+ * A SyncState object {sharedHeads, lastSentHeads, theirHeads, theirNeed, theirHave, sentHashes}
+ * (sync.js:262-271) crosses the ABI in this flat form ("state blob"):
+ *   u8 0x53 | u8 flags (1 theirHeads, 2 theirNeed, 4 theirHave present; 8 sentHashes is the empty
+ *   array receiveSyncMessage resets it to) | H sharedHeads | H lastSentHeads | [H theirHeads]
+ *   | [H theirNeed] | [uleb n, n x (H lastSync, uleb len, bloom bytes)] | H sentHashes
+ * where H = uleb count + count x 32-byte hash (sentHashes in insertion order).
+ * am_sync_generate       <- generateSyncMessage(backend, state)  sync.js:281-344, for n documents
+ *     at once: their Bloom filters are built in one k_bloom_build launch and their change
+ *     selections run in one k_sync_select launch. Per document: out state blob, message (NULL
+ *     when none is due) and error; returns the number of documents that failed.
+ * am_sync_receive        <- receiveSyncMessage(backend, state, msg) sync.js:381-438; *patch is the
+ *     applyChanges patch log when the message carried changes (else NULL). Returns 0, 1 (error,
+ *     document unchanged) or 2 (error after the changes were applied).
+ * am_sync_encode_message <- encodeSyncMessage(message)  sync.js:153-170 (message as JSON)
+ * am_sync_decode_messages<- decodeSyncMessage(bytes)    sync.js:175-198, n messages: spans of
+ *     message i are spans[span_off[i] .. span_off[i+1]): heads (off, count), need (off, count),
+ *     per have: lastSync (off, count) and bloom (off, len), per change (off, len); offsets into
+ *     the message, counts[4i..4i+3] = heads, need, have, changes. Returns the number failed.
+ * am_sync_encode_state   <- encodeSyncState(state)      sync.js:205-210 (from a state blob)
+ * am_sync_decode_state   <- decodeSyncState(bytes)      sync.js:216-224 (to a state blob) */
+typedef struct { uint64_t off, len; } am_span;
+int am_bloom_check(const uint8_t *filter, uint64_t len, am_error *err);
+int am_sync_generate(size_t n, am_doc *const *docs, const uint8_t *const *states, const size_t *state_lens,
+                     uint8_t **out_states, size_t *out_state_lens, uint8_t **msgs, size_t *msg_lens, am_error *errs);
+int am_sync_receive(am_doc *doc, const uint8_t *state, size_t state_len, const uint8_t *msg, size_t msg_len,
+                    uint8_t **out_state, size_t *out_state_len, uint8_t **patch, size_t *patch_len, am_error *err);
+int am_sync_encode_message(const char *json, size_t len, uint8_t **out, size_t *out_len, am_error *err);
+int am_sync_decode_messages(size_t n, const uint8_t *const *msgs, const size_t *lens, am_span **spans,
+                            uint64_t *span_off, uint32_t *counts, am_error *errs);
+int am_sync_encode_state(const uint8_t *state, size_t len, uint8_t **out, size_t *out_len, am_error *err);
+int am_sync_decode_state(const uint8_t *bytes, size_t len, uint8_t **state, size_t *state_len, am_error *err);
+
 void am_free(void *p);
 
 /* ---- host stage for batch callers (DEFLATE, columnar.js:798-823, 1052-1067) ----

@@ -1,0 +1,128 @@
+"""Replay of the backend-boundary logs recorded from the reference's own test files
+(tests/golden/backend_log_*.json, tests/golden/gen/make_backend_log.js) against the Python host
+(automerge_amd.backend). Each entry is one call of a backend/index.js export with its arguments and
+the reference's result or error; handles are matched by identity as the reference returned them."""
+import json
+import os
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FILES = ["sync", "backend", "test", "text", "table"]
+PURE = {"encodeSyncMessage", "decodeSyncMessage", "encodeSyncState", "decodeSyncState", "initSyncState"}
+UNDEF = object()
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, "backend_log_%s.json" % name)) as f:
+        return json.load(f)
+
+
+def _special(r):
+    return isinstance(r, dict) and len(r) == 1 and next(iter(r)) in ("__bytes", "__f64", "__undef", "__view", "$h")
+
+
+def decode(r, handles):
+    if isinstance(r, list):
+        return [decode(v, handles) for v in r]
+    if isinstance(r, dict):
+        if _special(r):
+            k, v = next(iter(r.items()))
+            if k == "$h":
+                return handles[v]
+            if k in ("__bytes", "__view"):
+                return bytes.fromhex(v)
+            if k == "__undef":
+                return UNDEF
+            return -0.0 if v == "-0" else float(v)
+        return {k: decode(v, handles) for k, v in r.items()}
+    return r
+
+
+def canon(x):
+    if x is UNDEF:
+        return {"__undef": 1}
+    if isinstance(x, bool) or x is None or isinstance(x, str):
+        return x
+    if isinstance(x, float):
+        if x != x or x in (float("inf"), float("-inf")):
+            return {"__f64": "NaN" if x != x else ("Infinity" if x > 0 else "-Infinity")}
+        if x == 0 and str(x).startswith("-"):
+            return {"__f64": "-0"}
+        return int(x) if x.is_integer() and abs(x) < 2 ** 63 else x
+    if isinstance(x, int):
+        return x
+    if isinstance(x, (bytes, bytearray, memoryview)):
+        return {"__bytes": bytes(x).hex()}
+    if isinstance(x, (list, tuple)):
+        return [canon(v) for v in x]
+    if isinstance(x, dict):
+        return {k: canon(x[k]) for k in sorted(x)}
+    raise TypeError("cannot canonicalize %r" % (x,))
+
+
+def _is_handle(x):
+    return hasattr(x, "state") and hasattr(x, "heads") and hasattr(x, "frozen")
+
+
+def match(rec, x, handles):
+    if _special(rec) and "$h" in rec:
+        if not _is_handle(x):
+            return False
+        if rec["$h"] in handles:
+            return handles[rec["$h"]] is x
+        handles[rec["$h"]] = x
+        return True
+    if isinstance(rec, list):
+        return isinstance(x, (list, tuple)) and len(x) == len(rec) and all(match(a, b, handles) for a, b in zip(rec, x))
+    if isinstance(rec, dict) and not _special(rec):
+        return isinstance(x, dict) and sorted(rec) == sorted(x) and all(match(rec[k], x[k], handles) for k in rec)
+    if rec == {"__undef": 1} and x is None:
+        return True
+    return json.dumps(canon(x), sort_keys=True) == json.dumps(rec, sort_keys=True)
+
+
+def _err_name(e):
+    from automerge_amd import _native as N
+    if isinstance(e, N.AutomergeError):
+        return e.kind
+    if isinstance(e, TypeError):
+        return "TypeError"
+    return "Error"
+
+
+def _args(fn, args):
+    # JS `undefined` arguments are absent in Python (defaults apply)
+    while args and args[-1] is UNDEF:
+        args = args[:-1]
+    return args
+
+
+def replay(B, files=FILES, only=None, stop_at=40):
+    """Replays the logs through backend module B; returns (calls, scenarios, bad)."""
+    bad, calls, scen = [], 0, 0
+    for f in files:
+        for sc in load(f)["scenarios"]:
+            handles = {}
+            if only is not None and not any(e["fn"] in only for e in sc["log"]):
+                continue
+            scen += 1
+            for i, e in enumerate(sc["log"]):
+                if only is not None and e["fn"] not in only:
+                    continue
+                calls += 1
+                try:
+                    res, err = getattr(B, e["fn"])(*_args(e["fn"], decode(e["args"], handles))), None
+                except Exception as x:  # noqa: BLE001 -- the error is the result being compared
+                    res, err = None, {"name": _err_name(x), "message": str(x)}
+                if "error" in e:
+                    if err is None or err["message"] != e["error"]["message"] or err["name"] != e["error"]["name"]:
+                        bad.append((f, sc["name"], i, e["fn"], e["error"], err))
+                    continue
+                if err is not None:
+                    bad.append((f, sc["name"], i, e["fn"], "unexpected", err))
+                    break
+                if not match(e["result"], res, handles):
+                    bad.append((f, sc["name"], i, e["fn"], json.dumps(e["result"])[:400], json.dumps(canon(res))[:400]))
+                    break
+                if len(bad) >= stop_at:
+                    return calls, scen, bad
+    return calls, scen, bad

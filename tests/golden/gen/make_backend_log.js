@@ -1,0 +1,140 @@
+// Backend-boundary recorder. Runs test files of the reference (test/sync_test.js, backend_test.js,
+// test.js, text_test.js, table_test.js) under a minimal describe/it harness with the reference's
+// Backend module replaced by a recorder that forwards every call to the real reference backend and
+// logs (function, arguments, result or error). The logs are the golden vectors for the 22
+// Backend exports of backend/index.js: tests/js/backend_log_replay.js replays each call against
+// automerge_amd/js/backend.js and compares every result.
+//   NODE_PATH=tests/golden/gen/node_modules node tests/golden/gen/make_backend_log.js
+// Clock and randomness are pinned (Date without arguments = epoch, seeded randomBytes and
+// Math.random), so a re-run reproduces the committed tests/golden/backend_log_*.json byte for byte.
+'use strict'
+const fs = require('fs')
+const path = require('path')
+const crypto = require('crypto')
+const assert = require('assert')
+const REF = process.env.AM_REF || '/root/reference'
+const OUT = path.join(__dirname, '..')
+
+// ---- pinned clock and randomness ----
+let seed = 0x2545f491
+crypto.randomBytes = n => {
+  const b = Buffer.alloc(n)
+  for (let i = 0; i < n; i++) { seed = (Math.imul(seed, 1664525) + 1013904223) >>> 0; b[i] = seed >>> 24 }
+  return b
+}
+let mseed = 0x9e3779b9
+Math.random = () => { mseed = (Math.imul(mseed, 1664525) + 1013904223) >>> 0; return mseed / 4294967296 }
+const RealDate = Date
+global.Date = class extends RealDate {
+  constructor(...a) { if (a.length) super(...a); else super(0) }
+  static now() { return 0 }
+}
+
+// ---- value encoding shared with the replay (canonical JSON) ----
+function canon(x, handleId) {
+  if (x === undefined) return {__undef: 1}
+  if (typeof x === 'number') {
+    if (!Number.isFinite(x) || Object.is(x, -0)) return {__f64: Object.is(x, -0) ? '-0' : String(x)}
+    return x
+  }
+  if (x instanceof Uint8Array) return {__bytes: Buffer.from(x.buffer, x.byteOffset, x.byteLength).toString('hex')}
+  if (ArrayBuffer.isView(x)) return {__view: Buffer.from(x.buffer).toString('hex')}
+  if (Array.isArray(x)) return x.map(v => canon(v, handleId))
+  if (x && typeof x === 'object') {
+    if (handleId) { const id = handleId(x); if (id !== null) return {$h: id} }
+    const o = {}
+    for (const k of Object.keys(x).sort()) o[k] = canon(x[k], handleId)
+    return o
+  }
+  return x
+}
+
+// ---- the recorder ----
+const realPath = require.resolve(path.join(REF, 'backend'))
+const Real = require(realPath)
+let handles = new Map(), nextHandle = 0, log = null, calls = 0
+const isHandle = x => x && typeof x === 'object' && 'state' in x && ('heads' in x)
+const handleId = x => {
+  if (!isHandle(x)) return null
+  if (!handles.has(x)) handles.set(x, nextHandle++)
+  return handles.get(x)
+}
+const recorder = {}
+for (const name of Object.keys(Real)) {
+  recorder[name] = function (...args) {
+    const entry = {fn: name, args: canon(args, handleId)}
+    if (log) log.push(entry)
+    calls++
+    try {
+      const r = Real[name](...args)
+      entry.result = canon(r, handleId)
+      return r
+    } catch (e) {
+      entry.error = {name: e.constructor.name, message: e.message}
+      throw e
+    }
+  }
+}
+require.cache[realPath].exports = recorder
+
+const Automerge = require(path.join(REF, 'src/automerge'))
+assert.strictEqual(Automerge.Backend, recorder)
+
+// ---- a minimal describe/it harness ----
+function harness(file) {
+  const tests = []
+  const stack = [{name: '', beforeEach: [], afterEach: []}]
+  const g = global
+  g.describe = (name, fn) => {
+    stack.push({name, beforeEach: [], afterEach: []})
+    fn()
+    stack.pop()
+  }
+  g.describe.skip = () => {}
+  g.describe.only = g.describe
+  g.context = g.describe
+  g.it = (name, fn) => tests.push({name: stack.map(s => s.name).filter(Boolean).concat(name).join(' / '),
+                                    fn, before: stack.flatMap(s => s.beforeEach), after: stack.flatMap(s => s.afterEach)})
+  g.it.skip = () => {}
+  g.it.only = g.it
+  g.beforeEach = fn => stack[stack.length - 1].beforeEach.push(fn)
+  g.afterEach = fn => stack[stack.length - 1].afterEach.push(fn)
+  g.before = fn => fn()
+  g.after = () => {}
+  require(path.join(REF, 'test', file))
+  return tests
+}
+
+const MAX_ENTRIES = +(process.env.AM_LOG_MAX || 400)
+function run(file) {
+  const scenarios = []
+  let passed = 0, failed = 0, skipped = 0
+  for (const t of harness(file)) {
+    if (t.fn.length > 0) { skipped++; continue }  // callback-style tests
+    handles = new Map()
+    nextHandle = 0
+    log = []
+    let ok = true
+    try {
+      for (const b of t.before) b()
+      const r = t.fn()
+      if (r && typeof r.then === 'function') { skipped++; log = null; continue }
+      for (const a of t.after) a()
+    } catch (e) {
+      ok = false
+    }
+    if (ok) passed++; else failed++
+    if (ok && log.length > 0 && log.length <= MAX_ENTRIES) scenarios.push({name: t.name, log})
+    log = null
+  }
+  return {file, passed, failed, skipped, scenarios}
+}
+
+const files = (process.env.AM_LOG_FILES || 'sync_test.js,backend_test.js,test.js,text_test.js,table_test.js').split(',')
+for (const f of files) {
+  const r = run(f)
+  const name = 'backend_log_' + f.replace(/_test\.js$|\.js$/, '') + '.json'
+  fs.writeFileSync(path.join(OUT, name), JSON.stringify(r) + '\n')
+  const n = r.scenarios.reduce((a, s) => a + s.log.length, 0)
+  console.log(`${f}: ${r.passed} passed, ${r.failed} failed, ${r.skipped} skipped; ${r.scenarios.length} scenarios, ${n} calls -> ${name}`)
+}

@@ -1,0 +1,97 @@
+'use strict'
+// Replays the backend-boundary logs recorded from the reference's own test files
+// (tests/golden/backend_log_*.json, made by tests/golden/gen/make_backend_log.js) against
+// automerge_amd/js/backend.js: every call of the 22 Backend exports with the recorded arguments,
+// every result (patches, binary changes, saved documents, heads, sync messages and sync states,
+// handle identity) and every thrown error class and message compared. Prints one JSON line.
+const fs = require('fs')
+const path = require('path')
+const B = require(path.join(__dirname, '..', '..', 'automerge_amd', 'js', 'backend.js'))
+const GOLDEN = path.join(__dirname, '..', 'golden')
+
+const isHandle = x => x && typeof x === 'object' && 'state' in x && 'heads' in x
+function canon(x) {
+  if (x === undefined) return {__undef: 1}
+  if (typeof x === 'number') {
+    if (!Number.isFinite(x) || Object.is(x, -0)) return {__f64: Object.is(x, -0) ? '-0' : String(x)}
+    return x
+  }
+  if (x instanceof Uint8Array) return {__bytes: Buffer.from(x.buffer, x.byteOffset, x.byteLength).toString('hex')}
+  if (ArrayBuffer.isView(x)) return {__view: Buffer.from(x.buffer).toString('hex')}
+  if (Array.isArray(x)) return x.map(canon)
+  if (x && typeof x === 'object') {
+    const o = {}
+    for (const k of Object.keys(x).sort()) o[k] = canon(x[k])
+    return o
+  }
+  return x
+}
+const special = r => r && typeof r === 'object' && !Array.isArray(r) &&
+  ['__bytes', '__f64', '__undef', '__view', '$h'].some(k => k in r) && Object.keys(r).length === 1
+function decode(r, h) {
+  if (Array.isArray(r)) return r.map(v => decode(v, h))
+  if (r && typeof r === 'object') {
+    if (special(r)) {
+      if ('$h' in r) return h.get(r.$h)
+      if ('__bytes' in r) return new Uint8Array(Buffer.from(r.__bytes, 'hex'))
+      if ('__view' in r) return new Uint8Array(Buffer.from(r.__view, 'hex'))
+      if ('__undef' in r) return undefined
+      return r.__f64 === '-0' ? -0 : Number(r.__f64)
+    }
+    const o = {}
+    for (const k of Object.keys(r)) o[k] = decode(r[k], h)
+    return o
+  }
+  return r
+}
+function match(rec, x, h) {
+  if (special(rec) && '$h' in rec) {
+    if (!isHandle(x)) return false
+    if (h.has(rec.$h)) return h.get(rec.$h) === x
+    h.set(rec.$h, x)
+    return true
+  }
+  if (Array.isArray(rec)) return Array.isArray(x) && x.length === rec.length && rec.every((v, i) => match(v, x[i], h))
+  if (rec && typeof rec === 'object' && !special(rec)) {
+    if (!x || typeof x !== 'object' || Array.isArray(x) || x instanceof Uint8Array) return false
+    const ks = Object.keys(rec)
+    if (JSON.stringify(ks) !== JSON.stringify(Object.keys(x).sort())) return false
+    return ks.every(k => match(rec[k], x[k], h))
+  }
+  return JSON.stringify(canon(x)) === JSON.stringify(rec)
+}
+
+const files = (process.argv[2] || 'sync,backend,test,text,table').split(',')
+const bad = [], perFn = {}
+let calls = 0, scenarios = 0
+for (const f of files) {
+  const data = JSON.parse(fs.readFileSync(path.join(GOLDEN, `backend_log_${f}.json`)))
+  for (const sc of data.scenarios) {
+    scenarios++
+    const h = new Map()
+    for (let i = 0; i < sc.log.length; i++) {
+      const e = sc.log[i]
+      calls++
+      perFn[e.fn] = (perFn[e.fn] || 0) + 1
+      let res, err = null
+      try {
+        res = B[e.fn](...decode(e.args, h))
+      } catch (x) {
+        err = {name: x.constructor.name, message: x.message}
+      }
+      if (e.error) {
+        if (!err || err.message !== e.error.message || err.name !== e.error.name) {
+          bad.push({file: f, scenario: sc.name, i, fn: e.fn, want: e.error, got: err || 'no error'})
+        }
+        continue
+      }
+      if (err) { bad.push({file: f, scenario: sc.name, i, fn: e.fn, unexpected: err}); break }
+      if (!match(e.result, res, h)) {
+        bad.push({file: f, scenario: sc.name, i, fn: e.fn, want: JSON.stringify(e.result).slice(0, 600),
+                  got: JSON.stringify(canon(res)).slice(0, 600)})
+        break
+      }
+    }
+  }
+}
+console.log(JSON.stringify({files, scenarios, calls, perFn, nbad: bad.length, bad: bad.slice(0, 40)}))
