@@ -44,19 +44,22 @@ function decode(r, h) {
   }
   return r
 }
-function match(rec, x, h) {
+let where = ''
+function match(rec, x, h, p = '') {
+  where = p
   if (special(rec) && '$h' in rec) {
     if (!isHandle(x)) return false
     if (h.has(rec.$h)) return h.get(rec.$h) === x
     h.set(rec.$h, x)
     return true
   }
-  if (Array.isArray(rec)) return Array.isArray(x) && x.length === rec.length && rec.every((v, i) => match(v, x[i], h))
+  if (Array.isArray(rec)) return Array.isArray(x) && x.length === rec.length && rec.every((v, i) => match(v, x[i], h, p + '/' + i))
   if (rec && typeof rec === 'object' && !special(rec)) {
     if (!x || typeof x !== 'object' || Array.isArray(x) || x instanceof Uint8Array) return false
     const ks = Object.keys(rec)
-    if (JSON.stringify(ks) !== JSON.stringify(Object.keys(x).sort())) return false
-    return ks.every(k => match(rec[k], x[k], h))
+    // integer-like keys (actor ids such as '76543210') come first in Object.keys: compare sorted
+    if (JSON.stringify(ks.slice().sort()) !== JSON.stringify(Object.keys(x).sort())) return false
+    return ks.every(k => match(rec[k], x[k], h, p + '/' + k))
   }
   return JSON.stringify(canon(x)) === JSON.stringify(rec)
 }
@@ -87,7 +90,7 @@ for (const f of files) {
       }
       if (err) { bad.push({file: f, scenario: sc.name, i, fn: e.fn, unexpected: err}); break }
       if (!match(e.result, res, h)) {
-        bad.push({file: f, scenario: sc.name, i, fn: e.fn, want: JSON.stringify(e.result).slice(0, 600),
+        bad.push({file: f, scenario: sc.name, i, fn: e.fn, where, want: JSON.stringify(e.result).slice(0, 600),
                   got: JSON.stringify(canon(res)).slice(0, 600)})
         break
       }
