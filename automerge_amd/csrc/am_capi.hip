@@ -393,6 +393,7 @@ static bool inflate_stage(am_batch* b, const uint8_t* arena, uint64_t arena_len,
   HIPCHECK(hipMemcpyAsync(d_zidx.p, zidx.data(), 4ull * nz, hipMemcpyHostToDevice, s));
   (void)hipEventRecord(b->eng->ev[0], s);
   am_launch_inflate_size(b->arena.p, b->chunks.p, d_zidx.p, nz, d_zlen.p, s);
+  HIPCHECK(hipGetLastError());  // sizes below come from this launch
   (void)hipEventRecord(b->eng->ev[1], s);
   std::vector<uint32_t> zlen(nz);
   HIPCHECK(hipMemcpyAsync(zlen.data(), d_zlen.p, 4ull * nz, hipMemcpyDeviceToHost, s));
@@ -645,7 +646,7 @@ extern "C" int am_inflate_raw(am_engine* eng, const uint8_t* const* bufs, const 
              hipMemcpyAsync(d_zidx.p, zidx.data(), 4 * n, hipMemcpyHostToDevice, s) == hipSuccess;
   if (okc) {
     am_launch_inflate_size(d_arena.p, d_ch.p, d_zidx.p, (uint32_t)n, d_zlen.p, s);
-    okc = hipMemcpyAsync(zlen.data(), d_zlen.p, 4 * n, hipMemcpyDeviceToHost, s) == hipSuccess &&
+    okc = hipGetLastError() == hipSuccess && hipMemcpyAsync(zlen.data(), d_zlen.p, 4 * n, hipMemcpyDeviceToHost, s) == hipSuccess &&
           hipStreamSynchronize(s) == hipSuccess;
   }
   if (!okc) return fail("automerge_amd: inflate pass 1 failed");
@@ -1054,7 +1055,7 @@ struct OneResult {
 // Runs one document (optional base chunk + change list) through the GPU pipeline.
 bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified, const std::vector<std::vector<uint8_t>>& chg,
              const std::vector<am_known_hash>& known, bool have_graph, OneResult& res, std::vector<uint8_t>& arena, Err& err,
-             int patch_mode = 0) {
+             int patch_mode = 0, uint32_t extra_flags = 0) {
   arena.clear();
   std::vector<am_chunk_desc> cds;
   am_doc_desc dd{};
@@ -1072,14 +1073,20 @@ bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified,
   }
   dd.known_begin = 0;
   dd.known_count = (uint32_t)known.size();
-  dd.flags = (have_graph ? 1u : 0u) | (patch_mode == 1 ? AM_DOC_WANT_PATCH : 0u) | (patch_mode == 2 ? AM_DOC_WANT_DIFF : 0u);
+  dd.flags = (have_graph ? 1u : 0u) | (patch_mode == 1 ? AM_DOC_WANT_PATCH : 0u) | (patch_mode == 2 ? AM_DOC_WANT_DIFF : 0u) |
+             extra_flags;
   am_batch* b = scratch_batch(e);
   am_error ce;
-  if (am_batch_stage(b, arena.data(), arena.size(), cds.data(), (uint32_t)cds.size(), &dd, 1, known.data(),
-                     (uint32_t)known.size(), &ce) ||
-      am_batch_run(b) || am_batch_sync(b, &ce) || am_batch_results(b, &res.r)) {
-    err = {AM_U_CAPACITY, false, std::string("automerge_amd: GPU pipeline failed: ") + ce.message};
-    return false;
+  for (;;) {
+    if (am_batch_stage(b, arena.data(), arena.size(), cds.data(), (uint32_t)cds.size(), &dd, 1, known.data(),
+                       (uint32_t)known.size(), &ce) ||
+        am_batch_run(b) || am_batch_sync(b, &ce) || am_batch_results(b, &res.r)) {
+      err = {AM_U_CAPACITY, false, std::string("automerge_amd: GPU pipeline failed: ") + ce.message};
+      return false;
+    }
+    // invalid UTF-8 in a key or message: run again with room for the U+FFFD replacements
+    if (res.r.status != AM_U_UTF8 || (dd.flags & AM_DOC_FIX_UTF8)) break;
+    dd.flags |= AM_DOC_FIX_UTF8;
   }
   res.chg_state.assign(cds.size(), 0);
   std::vector<uint8_t> hs(32 * cds.size());
@@ -1136,7 +1143,8 @@ bool gpu_sha256(am_engine* e, const std::vector<const std::vector<uint8_t>*>& ms
   DevBuf<uint8_t> da;
   DevBuf<am_chunk_desc> dd;
   DevBuf<uint8_t> dout;
-  if (!da.ensure(arena.size()) || !dd.ensure(d.size()) || !dout.ensure(32 * d.size())) return false;
+  // +16: sha256_words loads whole words past a message's last byte
+  if (!da.ensure(arena.size() + 16) || !dd.ensure(d.size()) || !dout.ensure(32 * d.size())) return false;
   hipStream_t s = e->stream;
   if (!arena.empty()) HIPCHECK(hipMemcpyAsync(da.p, arena.data(), arena.size(), hipMemcpyHostToDevice, s));
   HIPCHECK(hipMemcpyAsync(dd.p, d.data(), sizeof(am_chunk_desc) * d.size(), hipMemcpyHostToDevice, s));
@@ -1316,6 +1324,17 @@ static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* le
     fill_known();
     e = Err{};
     if (!run_one(d->eng, &d->state, false, staged, known, true, res, arena, e, patch ? 2 : 0)) {
+      to_c(e, err);
+      return 1;
+    }
+  }
+  // a patch larger than the pools sized from the row counts: run again with 8x pools (the engine's
+  // limit, not a reference error; the reference would return the patch)
+  if (patch && res.patch.size() >= sizeof(PatchHdr2)) {
+    PatchHdr2 ph;
+    std::memcpy(&ph, res.patch.data(), sizeof ph);
+    if (ph.status == AM_U_CAPACITY && !run_one(d->eng, d->state.empty() ? nullptr : &d->state, false, staged, known,
+                                               d->have_hash_graph, res, arena, e, 2, AM_DOC_PATCH_ROOM)) {
       to_c(e, err);
       return 1;
     }

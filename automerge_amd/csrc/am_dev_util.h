@@ -441,6 +441,41 @@ __device__ __forceinline__ static bool utf8_valid_dev(const uint8_t* s, uint32_t
   }
   return true;
 }
+// TextDecoder('utf-8').decode + TextEncoder.encode (encoding.js:11-17): every maximal subpart of an
+// ill-formed sequence becomes U+FFFD (EF BF BD), per the WHATWG UTF-8 decoder. Returns the output
+// length; `out` null only measures.
+__device__ static uint32_t utf8_sanitize_dev(const uint8_t* in, uint32_t n, uint8_t* out) {
+  uint32_t o = 0, i = 0;
+  while (i < n) {
+    const uint8_t b = in[i];
+    if (b < 0x80) { if (out) out[o] = b; o++; i++; continue; }
+    uint32_t need;
+    uint8_t lo = 0x80, hi = 0xbf;
+    if (b >= 0xc2 && b <= 0xdf) need = 1;
+    else if (b >= 0xe0 && b <= 0xef) { need = 2; if (b == 0xe0) lo = 0xa0; if (b == 0xed) hi = 0x9f; }
+    else if (b >= 0xf0 && b <= 0xf4) { need = 3; if (b == 0xf0) lo = 0x90; if (b == 0xf4) hi = 0x8f; }
+    else need = 0;
+    uint32_t k = 1;
+    if (need) {
+      for (; k <= need; k++) {
+        if (i + k >= n) break;
+        const uint8_t c = in[i + k];
+        if (c < lo || c > hi) break;
+        lo = 0x80; hi = 0xbf;
+      }
+    }
+    if (need && k > need) {
+      if (out) for (uint32_t q = 0; q <= need; q++) out[o + q] = in[i + q];
+      o += need + 1;
+      i += need + 1;
+    } else {  // the bytes read so far are one maximal subpart; the offending byte is read again
+      if (out) { out[o] = 0xef; out[o + 1] = 0xbf; out[o + 2] = 0xbd; }
+      o += 3;
+      i += k;
+    }
+  }
+  return o;
+}
 // JS string `<` on valid UTF-8: compares UTF-16 code units (new.js:84,1159).
 __device__ __forceinline__ uint32_t utf8_cp(const uint8_t* s, uint32_t& i) {
   uint8_t b = s[i];

@@ -88,21 +88,22 @@ AM_PHD inline uint64_t diff_hash_cap(uint64_t R) {
   while (h < 2 * R + 2) h <<= 1;
   return h;
 }
-AM_PHD inline void diff_caps(uint64_t R, uint64_t E, uint64_t caps[DIFF_NCAPS]) {
+// pools with heuristic sizes (kv, pe, ed, mv, tmp) scale by `ps` (8 on a rerun after PATCH_U_CAPACITY)
+AM_PHD inline void diff_caps(uint64_t R, uint64_t E, uint64_t caps[DIFF_NCAPS], uint64_t ps = 1) {
   caps[0] = R + 2;          // obj
   caps[1] = R + 2;          // kid
-  caps[2] = 4 * R + 64;     // kv
+  caps[2] = ps * (4 * R + 64);     // kv
   caps[3] = R + 2;          // prop
-  caps[4] = 4 * R + 64;     // pe
-  caps[5] = 4 * R + 64;     // ed
-  caps[6] = 4 * R + 64;     // mv
+  caps[4] = ps * (4 * R + 64);     // pe
+  caps[5] = ps * (4 * R + 64);     // ed
+  caps[6] = ps * (4 * R + 64);     // mv
   caps[7] = R + 2;          // pst
   caps[8] = 2 * R + 4;      // vis
   caps[9] = R + 2;          // cs
   caps[10] = E + 2;         // cm
   caps[11] = R + 2;         // fpos
   caps[12] = R + 2;         // oids
-  caps[13] = 8 * R + 128;   // tmp
+  caps[13] = ps * (8 * R + 128);   // tmp
   caps[14] = R + 2;         // cops (+ seen_off)
   caps[15] = E + 2;         // seen
   caps[16] = R + 2;         // bitp
@@ -114,9 +115,9 @@ AM_PHD inline void diff_caps(uint64_t R, uint64_t E, uint64_t caps[DIFF_NCAPS]) 
   caps[22] = R + 2;         // ev_off
   caps[23] = E + 2;         // ev
 }
-AM_PHD inline uint64_t diff_scratch_bytes(uint64_t R, uint64_t E) {
+AM_PHD inline uint64_t diff_scratch_bytes(uint64_t R, uint64_t E, uint64_t ps = 1) {
   uint64_t c[DIFF_NCAPS];
-  diff_caps(R, E, c);
+  diff_caps(R, E, c, ps);
   const uint64_t sz[DIFF_NCAPS] = {sizeof(DObj), sizeof(DKid), sizeof(DKV), sizeof(DProp), sizeof(DPE), sizeof(DEdit),
                                    sizeof(DMV), sizeof(DPst), sizeof(DVis), sizeof(DCs), sizeof(DCm), 4, 4, 4, 8, 1,
                                    4, 4, 4, 4, 4, 4, 4, 4};
@@ -124,9 +125,9 @@ AM_PHD inline uint64_t diff_scratch_bytes(uint64_t R, uint64_t E) {
   for (int i = 0; i < DIFF_NCAPS; i++) t += (c[i] * sz[i] + 15) & ~(uint64_t)15;
   return t;
 }
-AM_PHD inline void diff_scratch_bind(uint8_t* p, uint64_t R, uint64_t E, DiffScratch& w) {
+AM_PHD inline void diff_scratch_bind(uint8_t* p, uint64_t R, uint64_t E, DiffScratch& w, uint64_t ps = 1) {
   uint64_t c[DIFF_NCAPS];
-  diff_caps(R, E, c);
+  diff_caps(R, E, c, ps);
   uint64_t o = 0;
   auto take = [&](uint64_t bytes) { uint8_t* at = p + o; o += (bytes + 15) & ~(uint64_t)15; return at; };
   w.obj = reinterpret_cast<DObj*>(take(c[0] * sizeof(DObj))); w.cap_obj = (uint32_t)c[0];
@@ -557,7 +558,9 @@ struct Diff {
   AM_PHD bool update_property(int32_t ob, int32_t row, int32_t f, int64_t lim, int64_t list_index, bool has_old,
                               uint32_t old_succ, bool whole_doc) {
     const int64_t action = s.action(row);
-    if (action < 0 || action >= 8) return fail(PATCH_U_VALUE);
+    // an unknown odd action carries no value and no object (like link); make* actions beyond the
+    // known types would need objectMeta entries of type null (not supported)
+    if (action < 0 || (action >= 8 && action % 2 == 0)) return fail(PATCH_U_VALUE);
     const int64_t idc = s.id_ctr(row);
     const int32_t ida = s.id_actor(row);
     const uint32_t cur_succ = has_old ? nsucc_at(f, lim) : 0u;

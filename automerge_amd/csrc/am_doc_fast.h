@@ -117,8 +117,8 @@ __host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t n
 }
 
 __host__ __device__ inline bool fast_eligible(const DocBounds& b, const am_doc_desc& dd) {
-  if (dd.flags & AM_DOC_WANT_PATCH) return false;  // getPatch: k_doc (P7); applyChanges patches: fast_diff
-  if (b.B == 0 || doc_scattered(b)) return false;
+  if (dd.flags & (AM_DOC_WANT_PATCH | AM_DOC_FIX_UTF8 | AM_DOC_PATCH_ROOM)) return false;  // getPatch: k_doc (P7); applyChanges patches: fast_diff
+  if (b.B == 0 || doc_scattered(b) || b.UC) return false;
   if (dd.base_chunk < 0 && dd.chg_count == 0) return false;
   if (b.span_hi - b.span_lo > FD_SPAN_MAX) return false;
   if (b.R > FD_MAX || b.E > FD_MAX || b.C > FD_MAX || b.N > FD_MAX || b.D > FD_MAX || b.ND > FD_MAX || b.H > FD_MAX)
@@ -1640,6 +1640,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
       m_null = false;
       m_off = (uint32_t)(h.base + h.msg_off - a0);
       m_len = h.msg_len;
+      bad |= !utf8_valid_dev(IN + m_off, m_len);  // k_doc replaces invalid sequences (U+FFFD)
       v_nd = n_nd;
       v_xlen = (int64_t)(((uint64_t)(h.has_extra ? h.extra_len : 0u) << 4) | 7);
       x_off = (uint32_t)(h.base + h.extra_off - a0);

@@ -24,6 +24,24 @@ __device__ __forceinline__ APtr AV(DocShared& s) {
   else return APtr{s.A, 0};
 }
 
+// A key or message with invalid UTF-8 is replaced by its decoded-and-re-encoded form (U+FFFD for
+// every ill-formed subpart; the reference holds strings, encoding.js:15-17) written after the staged
+// input bytes, so (off, len) keep addressing the arena view. Documents staged without
+// AM_DOC_FIX_UTF8 (no room reserved) report AM_U_UTF8 and the host runs them again with it.
+__device__ static bool fix_utf8(DocShared& s, uint64_t& off, uint32_t& len) {
+  const APtr A = AV(s);
+  if (utf8_valid_dev(A + off, len)) return true;
+  if (!(s.b.U & 1) || doc_scattered(s.b)) { set_err(s, AM_U_UTF8); return false; }
+  const uint32_t n = utf8_sanitize_dev(A + off, len, nullptr);
+  const uint32_t at = atomicAdd(&s.xs_used, n);
+  const uint64_t span = s.b.span_hi - s.b.span_lo;
+  if ((uint64_t)at + n > 3 * s.b.S + 64) { set_err(s, AM_U_CAPACITY); return false; }
+  utf8_sanitize_dev(A + off, len, hp<uint8_t>(s, s.L.input) + span + at);
+  off = s.b.span_hi + at;
+  len = n;
+  return true;
+}
+
 __device__ static int64_t base_head_index(DocShared& s, uint32_t h) {
   if (s.dh.has_hidx) {
     Rd r{AV(s) + s.dh.base + s.dh.hidx_off, (uint64_t)1 << 40, 0};
@@ -256,6 +274,7 @@ __device__ static void plan_doc(DocShared& s, const am_doc_desc& dd, const Chunk
       cr.time = h.time;
       cr.msg_off = h.base + h.msg_off;
       cr.msg_len = h.msg_len;
+      if (!fix_utf8(s, cr.msg_off, cr.msg_len)) return;
       cr.ndeps = h.ndeps;
       cr.deps_off = ndep;
       ndep += h.ndeps;
@@ -431,7 +450,7 @@ __device__ static void gather_row(DocShared& s, uint32_t i, const int64_t* cells
   else {
     r.key_len = (uint32_t)(ks & 0xffffffff);
     r.key_off = s.b.span_lo + (uint64_t)(ks >> 32);
-    if (!utf8_valid_dev(AV(s) + r.key_off, r.key_len)) { set_err(s, AM_U_UTF8); bad = true; }
+    if (!fix_utf8(s, r.key_off, r.key_len)) bad = true;
   }
   if (si.is_change) { r.id_actor = (int32_t)si.self; r.id_ctr = si.start_op + q; }
   else { r.id_actor = mapact(c[(uint64_t)5 * nr]); r.id_ctr = c[(uint64_t)6 * nr]; }
@@ -443,7 +462,7 @@ __device__ static void gather_row(DocShared& s, uint32_t i, const int64_t* cells
   const int64_t pc = c[(uint64_t)12 * nr];
   r.ps_cnt = pc == AM_NULL64 ? 0 : (uint32_t)pc;
   r.src_change = (uint8_t)si.is_change;
-  r.is_del = si.is_change && r.action == 3;
+  r.is_del = si.is_change && r.action == 3 && !r.insert;  // an inserting del stays a row (new.js:1143-1150)
   r.flags = 0;
   r.val_off = 0;
   r.ps_off = 0;
@@ -529,7 +548,7 @@ __device__ static void decode_base_chg_col(DocShared& s, uint32_t col) {
         if ((e = cd_next_str(d, so, sl))) break;
         chg[i].msg_len = sl;
         chg[i].msg_off = sl == AM_NOSTR ? 0 : off + so;
-        if (sl != AM_NOSTR && !utf8_valid_dev(A + off + so, sl)) { set_err(s, AM_U_UTF8); return; }
+        if (sl != AM_NOSTR && !fix_utf8(s, chg[i].msg_off, chg[i].msg_len)) return;
       }
       break;
     }
@@ -714,6 +733,9 @@ __device__ static uint32_t encode_column(uint8_t kind, uint32_t n, uint8_t* out,
   return total;
 }
 
+#include "am_unknown.h"
+
+#define ROW_KEEP_DEL 2  // Row.flags: a change's del without pred that stays a document row
 __device__ __forceinline__ bool same_obj(const Row& a, const Row& b) {
   return a.obj_ctr == b.obj_ctr && a.obj_actor == b.obj_actor;
 }
@@ -730,6 +752,52 @@ __device__ static int32_t id_lookup(const IdKey* idk, uint32_t n, int64_t ctr, i
   return -1;
 }
 
+
+// first index of (ctr, actor) in the id index (equal ids are adjacent, ordered by row); a document
+// may hold the same id under different keys, which the reference accepts
+__device__ static uint32_t id_lower(const IdKey* idk, uint32_t n, int64_t ctr, int32_t actor) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const IdKey& k = idk[mid];
+    if (k.ctr < ctr || (k.ctr == ctr && k.actor < actor)) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+#define FOR_ID(k, idk, n, c, a) for (uint32_t k = id_lower(idk, n, c, a); k < (n) && idk[k].ctr == (c) && idk[k].actor == (a); k++)
+
+// does row i (stream order) have a row of the same object before it (an op of the object in the
+// document when i is applied)?
+__device__ static bool obj_has_row_before(const Row* rows, uint32_t i) {
+  for (uint32_t j = 0; j < i; j++)
+    if (!rows[j].is_del && same_obj(rows[j], rows[i])) return true;
+  return false;
+}
+// the list element (key_ctr, key_actor) of row i: an earlier insert of the same object, or -1
+__device__ static int32_t list_elem(const Row* rows, const IdKey* idk, uint32_t R, uint32_t i) {
+  const Row& r = rows[i];
+  if (r.key_actor < 0 || r.key_ctr == AM_NULL64) return -1;
+  FOR_ID(k, idk, R, r.key_ctr, r.key_actor) {
+    const int32_t e = idk[k].row;
+    if (rows[e].insert && !rows[e].is_del && same_obj(rows[e], r) && rows[e].key_len == AM_NOSTR &&
+        (!r.src_change || (uint32_t)e < i))
+      return e;
+  }
+  return -1;
+}
+__device__ static bool list_elem_ok(const Row* rows, const IdKey* idk, uint32_t R, uint32_t i) {
+  return list_elem(rows, idk, R, i) >= 0;
+}
+// the element is missing: seekWithinBlock scans the object's ops and reports the reference element
+// (new.js:177-183, 300); an object without ops is passed over and mergeDocChangeOps reports the
+// element (new.js:1163-1167)
+__device__ static void elem_missing_err(DocShared& s, const Row* rows, const ActorRef* actors, uint32_t R, uint32_t i) {
+  const Row& r = rows[i];
+  const uint64_t ao = r.key_actor >= 0 ? actors[r.key_actor].off : 0;
+  const uint32_t al = r.key_actor >= 0 ? actors[r.key_actor].len : 0;
+  (void)R;
+  set_err(s, obj_has_row_before(rows, i) ? AM_E_REF_NOT_FOUND : AM_E_ELEM_NOT_FOUND, r.key_ctr, 0, ao, al);
+}
 
 // ---- P7: getPatch log (am_patch.h) over the merged rows in document order ----
 struct RowSrc {
@@ -911,6 +979,7 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
     s.max_op = 0;
     s.out_len = 0;
     s.ph_last = clock64();
+    s.xs_used = 0;
     if (ws_off[doc] + s.L.total > ws_cap) set_err(s, AM_U_CAPACITY);
     // chunk-level errors: the base document first (load), then changes in order (new.js:1798)
     if (s.has_base) {
@@ -934,9 +1003,10 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
   if (s.status) goto done;
   // P0: stage the document's input bytes (base + changes, adjacent in the arena) into the hot
   // region with 16-byte coalesced loads; every later parse/decode reads them from there.
-  if constexpr (kHotLds) {
+  // (the global mode stages too when invalid UTF-8 is being replaced: the replacements follow the copy)
+  if (kHotLds || ((s.b.U & 1) && !doc_scattered(s.b))) {
     const uint64_t lo = s.b.span_lo, n = s.b.span_hi - s.b.span_lo;
-    uint8_t* dst = am_lds + L.input;
+    uint8_t* dst = hp<uint8_t>(s, L.input);
     if (n) {
       const uint64_t head = (16 - (lo & 15)) & 15;  // bytes before the first 16-aligned source address
       for (uint64_t q = t; q < head && q < n; q += T) dst[q] = arena[lo + q];
@@ -952,6 +1022,8 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
         for (uint64_t q = head + 16 * nv + t; q < n; q += T) dst[q] = arena[lo + q];
       }
     }
+    // the global mode now reads its input from the staged copy too (same arena offsets)
+    if (!kHotLds && t == 0) s.A = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(dst) - lo);
   }
   __syncthreads();
   PH(0);
@@ -1042,6 +1114,8 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
       }
       if (t == 0 && m > s.max_op) s.max_op = m;
     }
+    // op columns of a future format version, carried through the merge (am_unknown.h)
+    if (s.b.UC && t == 0) unk_collect(s, dd, chunks, info, wsg);
     __syncthreads();
     if (s.status) goto done;
 #if defined(AM_STOP_PHASE) && AM_STOP_PHASE == 3
@@ -1061,7 +1135,19 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
         continue;
       }
       if (r.action == AM_NULL64) { set_err(s, AM_U_VALUE); continue; }
-      if (r.is_del && (r.insert || r.ps_cnt == 0)) { set_err(s, AM_U_DEL_SHAPE); continue; }
+      if (r.is_del && r.ps_cnt == 0 && r.key_len != AM_NOSTR) {
+        // a del without pred disappears once an op of its key with a lower id has been merged
+        // (mergeDocChangeOps drops dels whose preds were all seen, new.js:1199-1212); otherwise the
+        // change ops are taken first and it stays as a row (new.js:1143-1150)
+        bool drop = false;
+        for (uint32_t j = 0; j < i && !drop; j++) {
+          const Row& x = rows[j];
+          drop = !x.is_del && same_obj(x, r) && x.key_len == r.key_len && bytes_eq(A + x.key_off, A + r.key_off, r.key_len) &&
+                 (x.id_ctr < r.id_ctr || (x.id_ctr == r.id_ctr && actor_cmp_dev(A + actors[x.id_actor].off, actors[x.id_actor].len,
+                                                                                A + actors[r.id_actor].off, actors[r.id_actor].len) < 0));
+        }
+        if (!drop) rows[i].flags |= ROW_KEEP_DEL;
+      }
       if (r.insert && r.ps_cnt > 0) {
         const Ent& p = ents[r.ps_off];
         set_err(s, AM_E_PRED_NOT_FOUND, p.ctr, 0, actors[p.actor].off, actors[p.actor].len);
@@ -1069,6 +1155,9 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
       }
       if (r.key_len == AM_NOSTR && !r.insert && r.key_ctr == AM_NULL64) { set_err(s, AM_U_VALUE); continue; }
     }
+    __syncthreads();
+    for (uint32_t i = t; i < R; i += T)
+      if (rows[i].flags & ROW_KEEP_DEL) rows[i].is_del = 0;
     // P5c: id index sorted by (ctr, actor index)
     const uint32_t PR = pow2_ceil(R > 0 ? R : 1);
     IdKey* idk = hp<IdKey>(s, L.idk);
@@ -1085,9 +1174,23 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
       if (a.actor != b.actor) return a.actor < b.actor;
       return a.row < b.row;
     });
-    for (uint32_t i = t + 1; i < R; i += T)
-      if (idk[i].ctr == idk[i - 1].ctr && idk[i].actor == idk[i - 1].actor)
-        set_err(s, AM_E_DUP_OPID, idk[i].ctr, 0, actors[idk[i].actor].off, actors[idk[i].actor].len);
+    // equal ids: mergeDocChangeOps compares ids only among the ops of one key / list element, so a
+    // change op repeating the id of an op in the same key or element fails (new.js:1218-1221) and
+    // repeats elsewhere are kept; insertions are placed before that comparison (new.js:1143)
+    for (uint32_t i = t + 1; i < R; i += T) {
+      if (!(idk[i].ctr == idk[i - 1].ctr && idk[i].actor == idk[i - 1].actor)) continue;
+      const Row& y = rows[idk[i].row];
+      if (!y.src_change || y.insert) continue;
+      for (uint32_t k = i; k-- > 0 && idk[k].ctr == idk[i].ctr && idk[k].actor == idk[i].actor;) {
+        const Row& x = rows[idk[k].row];
+        if (x.is_del || !same_obj(x, y)) continue;
+        bool same;
+        if (y.key_len != AM_NOSTR) same = x.key_len == y.key_len && bytes_eq(A + x.key_off, A + y.key_off, y.key_len);
+        else same = x.key_len == AM_NOSTR && (x.insert ? x.id_ctr : x.key_ctr) == y.key_ctr &&
+                    (x.insert ? x.id_actor : x.key_actor) == y.key_actor;
+        if (same) { set_err(s, AM_E_DUP_OPID, idk[i].ctr, 0, actors[idk[i].actor].off, actors[idk[i].actor].len); break; }
+      }
+    }
     __syncthreads();
     if (s.status) goto done;
 
@@ -1106,22 +1209,33 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
       if (!r.src_change || r.insert) continue;
       for (uint32_t q = 0; q < r.ps_cnt; q++) {
         Ent& p = ents[r.ps_off + q];
-        int32_t tr = id_lookup(idk, R, p.ctr, p.actor);
-        bool ok = tr >= 0 && (uint32_t)tr < i && !rows[tr].is_del;
-        if (ok) {
-          const Row& x = rows[tr];
-          ok = same_obj(x, r) && id_less(x.id_ctr, x.id_actor, r.id_ctr, r.id_actor);
+        int32_t tr = -1;
+        bool ok = false;
+        FOR_ID(k, idk, R, p.ctr, p.actor) {
+          tr = idk[k].row;
+          ok = (uint32_t)tr < i && !rows[tr].is_del;
           if (ok) {
-            if (r.key_len != AM_NOSTR) {
-              ok = x.key_len == r.key_len && bytes_eq(A + x.key_off, A + r.key_off, r.key_len);
-            } else {
-              int64_t ec = x.insert ? x.id_ctr : x.key_ctr;
-              int32_t ea = x.insert ? x.id_actor : x.key_actor;
-              ok = x.key_len == AM_NOSTR && ec == r.key_ctr && ea == r.key_actor;
+            const Row& x = rows[tr];
+            ok = same_obj(x, r) && id_less(x.id_ctr, x.id_actor, r.id_ctr, r.id_actor);
+            if (ok) {
+              if (r.key_len != AM_NOSTR) {
+                ok = x.key_len == r.key_len && bytes_eq(A + x.key_off, A + r.key_off, r.key_len);
+              } else {
+                int64_t ec = x.insert ? x.id_ctr : x.key_ctr;
+                int32_t ea = x.insert ? x.id_actor : x.key_actor;
+                ok = x.key_len == AM_NOSTR && ec == r.key_ctr && ea == r.key_actor;
+              }
             }
           }
+          if (ok) break;
         }
-        if (!ok) { set_err(s, AM_E_PRED_NOT_FOUND, p.ctr, 0, actors[p.actor].off, actors[p.actor].len); break; }
+        if (!ok) {
+          // a list update / delete whose element does not exist fails in seekToOp before its preds
+          // are checked (new.js:275-300, 1163-1167)
+          if (r.key_len == AM_NOSTR && !list_elem_ok(rows, idk, R, i)) elem_missing_err(s, rows, actors, R, i);
+          else set_err(s, AM_E_PRED_NOT_FOUND, p.ctr, 0, actors[p.actor].off, actors[p.actor].len);
+          break;
+        }
         p.row = tr;
       }
     }
@@ -1130,27 +1244,28 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
     // P5e: list elements: reference elements of inserts, target elements of updates
     for (uint32_t i = t; i < R; i += T) {
       const Row& r = rows[i];
-      if (r.key_len != AM_NOSTR || r.is_del) continue;
+      if (r.key_len != AM_NOSTR) continue;
+      if (r.is_del) {  // a del without pred still names an existing element
+        if (r.ps_cnt == 0 && !list_elem_ok(rows, idk, R, i)) elem_missing_err(s, rows, actors, R, i);
+        continue;
+      }
       if (r.insert) {
         elem_of[i] = (int32_t)i;
         if (r.key_ctr == AM_NULL64 || r.key_ctr == 0 || r.key_actor < 0) { parent[i] = -1; continue; }
-        int32_t p = id_lookup(idk, R, r.key_ctr, r.key_actor);
-        bool ok = p >= 0 && rows[p].insert && !rows[p].is_del && same_obj(rows[p], r) && rows[p].key_len == AM_NOSTR &&
-                  (!r.src_change || (uint32_t)p < i);
-        if (!ok) {
-          if (r.src_change) set_err(s, AM_E_REF_NOT_FOUND, r.key_ctr, 0, actors[r.key_actor].off, actors[r.key_actor].len);
-          else set_err(s, AM_U_VALUE);
+        const int32_t p = list_elem(rows, idk, R, i);
+        if (p < 0) {
+          // seekWithinBlock finds nothing to compare against in an object without ops and inserts
+          // at the object's start (new.js:62-64); a loaded document keeps such rows as they are
+          if (!r.src_change || !obj_has_row_before(rows, i)) { parent[i] = -1; continue; }
+          set_err(s, AM_E_REF_NOT_FOUND, r.key_ctr, 0, actors[r.key_actor].off, actors[r.key_actor].len);
           continue;
         }
         if (!(rows[p].id_ctr < r.id_ctr)) { set_err(s, AM_U_NONCAUSAL); continue; }
         parent[i] = p;
       } else {
-        int32_t e = (r.key_actor >= 0) ? id_lookup(idk, R, r.key_ctr, r.key_actor) : -1;
-        bool ok = e >= 0 && rows[e].insert && !rows[e].is_del && same_obj(rows[e], r) && rows[e].key_len == AM_NOSTR &&
-                  (!r.src_change || (uint32_t)e < i);
-        if (!ok) {
-          if (r.src_change) set_err(s, AM_E_ELEM_NOT_FOUND, r.key_ctr, 0, r.key_actor >= 0 ? actors[r.key_actor].off : 0,
-                                    r.key_actor >= 0 ? actors[r.key_actor].len : 0);
+        const int32_t e = list_elem(rows, idk, R, i);
+        if (e < 0) {
+          if (r.src_change) elem_missing_err(s, rows, actors, R, i);
           else set_err(s, AM_U_VALUE);
           continue;
         }
@@ -1366,9 +1481,24 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
     // (-1: an op of the base document -- rows or deletions it recorded only as succ entries)
     if (s.b.P == 2) {
       int32_t* etime = reinterpret_cast<int32_t*>(wsg + L.etime);
-      for (uint32_t j = t; j < NSUCC; j += T) {
-        const int32_t r = id_lookup(idk, R, outent[j].ctr, outent[j].actor);
-        etime[j] = (r >= 0 && (uint32_t)r >= s.nb) ? r - (int32_t)s.nb : -1;
+      for (uint32_t i = t; i < NOUT; i += T) {
+        const int32_t owner = sr[i].row;
+        const uint32_t j1 = i + 1 < NOUT ? succ_cnt[i + 1] : NSUCC;
+        for (uint32_t j = succ_cnt[i]; j < j1; j++) {
+          // the op of a succ entry: the row with that id (when a document repeats an id under
+          // another key, the one whose pred names this row)
+          int32_t r = -1;
+          FOR_ID(k, idk, R, outent[j].ctr, outent[j].actor) {
+            const int32_t c = idk[k].row;
+            if (r < 0) r = c;
+            const Row& y = rows[c];
+            bool hit = false;
+            if (y.src_change && !y.insert)
+              for (uint32_t q = 0; q < y.ps_cnt; q++) hit |= ents[y.ps_off + q].row == owner;
+            if (hit) { r = c; break; }
+          }
+          etime[j] = (r >= 0 && (uint32_t)r >= s.nb) ? r - (int32_t)s.nb : -1;
+        }
       }
     }
     __syncthreads();
@@ -1440,6 +1570,11 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
       if (t == 0) s.col_len[c] = len;
     }
     __syncthreads();
+    if (s.b.UC) unk_encode(s, sr, NOUT, ex, wsg);
+    __syncthreads();
+    if (s.status) goto done;
+    const uint32_t NU = s.b.UC ? s.nunk_ids : 0;
+    const uint32_t* uids = reinterpret_cast<const uint32_t*>(wsg + L.unk_ids);
     PH(11);
     // header + body assembly (encodeDocumentHeader, columnar.js:983-1004)
     uint8_t* out = wsg + L.out;
@@ -1452,6 +1587,8 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
       uint32_t nce = 0, noe = 0;
       for (int c = 0; c < DC_NCOLS; c++) if (s.col_len[16 + c]) { nce++; body += uleb_len(kDocChgColIds[c]) + uleb_len(s.col_len[16 + c]) + s.col_len[16 + c]; }
       for (int c = 0; c < OC_NCOLS; c++) if (s.col_len[c]) { noe++; body += uleb_len(kDocOpColIds[c]) + uleb_len(s.col_len[c]) + s.col_len[c]; }
+      for (uint32_t u = 0; u < NU; u++)
+        if (uids[2 * NU + u]) { noe++; body += uleb_len(uids[u]) + uleb_len(uids[2 * NU + u]) + uids[2 * NU + u]; }
       body += uleb_len(nce) + uleb_len(noe);
       // headsIndexes only when every head index is known (loaded documents may lack them)
       bool write_hidx = true;
@@ -1478,11 +1615,31 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
         o = put_uleb(o, nce);
         for (int c = 0; c < DC_NCOLS; c++) if (s.col_len[16 + c]) { o = put_uleb(o, kDocChgColIds[c]); o = put_uleb(o, s.col_len[16 + c]); }
         o = put_uleb(o, noe);
-        for (int c = 0; c < OC_NCOLS; c++) if (s.col_len[c]) { o = put_uleb(o, kDocOpColIds[c]); o = put_uleb(o, s.col_len[c]); }
+        // op columns in ascending id: the known ones with the unknown ones interleaved
+        {
+          uint32_t u = 0;
+          for (int c = 0; c <= OC_NCOLS; c++) {
+            for (; u < NU && (c == OC_NCOLS || uids[u] < kDocOpColIds[c]); u++)
+              if (uids[2 * NU + u]) { o = put_uleb(o, uids[u]); o = put_uleb(o, uids[2 * NU + u]); }
+            if (c < OC_NCOLS && s.col_len[c]) { o = put_uleb(o, kDocOpColIds[c]); o = put_uleb(o, s.col_len[c]); }
+          }
+        }
         uint64_t pos = (uint64_t)(o - out);
-        // column data positions, in DOCUMENT_COLUMNS then DOC_OPS_COLUMNS order
+        // column data positions, in DOCUMENT_COLUMNS then DOC_OPS_COLUMNS order (unknown op columns
+        // keep their output position in uids[NU + u] rewritten as the document offset)
         for (int c = 0; c < DC_NCOLS; c++) { s.col_pos[16 + c] = (uint32_t)pos; pos += s.col_len[16 + c]; }
-        for (int c = 0; c < OC_NCOLS; c++) { s.col_pos[c] = (uint32_t)pos; pos += s.col_len[c]; }
+        {
+          uint32_t u = 0;
+          uint32_t* uw = reinterpret_cast<uint32_t*>(wsg + L.unk_ids);
+          for (int c = 0; c <= OC_NCOLS; c++) {
+            for (; u < NU && (c == OC_NCOLS || uids[u] < kDocOpColIds[c]); u++) {
+              const uint32_t l = uids[2 * NU + u];
+              uw[3 * NU + u] = (uint32_t)pos;  // (unk_ids has room for 4 NU words)
+              pos += l;
+            }
+            if (c < OC_NCOLS) { s.col_pos[c] = (uint32_t)pos; pos += s.col_len[c]; }
+          }
+        }
         o = out + pos;
         if (write_hidx)
           for (uint32_t i = 0; i < s.nheads; i++) o = put_uleb(o, (uint64_t)hidx[i]);
@@ -1496,6 +1653,11 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
       const uint8_t* src = wsg + L.colbuf[c];
       uint8_t* dst = out + s.col_pos[c];
       for (uint32_t q = t; q < s.col_len[c]; q += T) dst[q] = src[q];
+    }
+    for (uint32_t u = 0; u < NU; u++) {
+      const uint8_t* src = wsg + L.unk_out + uids[NU + u];
+      uint8_t* dst = out + uids[3 * NU + u];
+      for (uint32_t q = t; q < uids[2 * NU + u]; q += T) dst[q] = src[q];
     }
     // P7: getPatch log (lane 0; the merge arrays of the union region are dead, reuse them)
     if (s.b.P && t == 0) {
@@ -1534,7 +1696,7 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
       po.heap = pbase + 64 + 64 * L.patch_nrec + 32 * L.patch_nmval;
       po.cap_rec = L.patch_nrec; po.cap_mval = L.patch_nmval; po.cap_heap = L.patch_heap;
       DiffScratch dw;
-      diff_scratch_bind(wsg + L.dscr, s.b.R, s.b.E, dw);
+      diff_scratch_bind(wsg + L.dscr, s.b.R, s.b.E, dw, (s.b.U & 2) ? 8 : 1);
       DiffSrc src{rows, ents, sr, succ_cnt, outent, reinterpret_cast<const int32_t*>(wsg + L.etime),
                   reinterpret_cast<const uint32_t*>(wsg + L.passend), s.npass, s.nb, s.nrows, NOUT, NSUCC, actors,
                   s.nactors, chg, NC, A};

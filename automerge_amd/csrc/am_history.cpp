@@ -17,6 +17,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <stdexcept>
 #include <map>
 #include <string>
 #include <unordered_map>
@@ -187,7 +188,14 @@ bool history(const uint8_t* doc, size_t len, std::vector<Bytes>& out, std::vecto
   std::vector<Col> cc, oc;
   for (auto* cols : {&cc, &oc}) {
     const uint64_t n = r.u();
-    for (uint64_t i = 0; i < n && !r.bad; i++) { Col c; c.id = (uint32_t)r.u(); c.b.resize(r.u()); cols->push_back(std::move(c)); }
+    for (uint64_t i = 0; i < n && !r.bad; i++) {
+      Col c;
+      c.id = (uint32_t)r.u();
+      const uint64_t l = r.u();
+      if (l > len) { r.bad = true; break; }  // a column cannot be longer than the chunk
+      c.b.resize(l);
+      cols->push_back(std::move(c));
+    }
   }
   for (auto* cols : {&cc, &oc})
     for (auto& c : *cols) {
@@ -412,7 +420,15 @@ extern "C" int am_document_changes(const uint8_t* doc, size_t len, uint8_t** out
   std::vector<Bytes> ch;
   std::vector<std::vector<uint8_t>> hs;
   HErr e;
-  if (!history(doc, len, ch, hs, e)) {
+  bool ok;
+  try {
+    ok = history(doc, len, ch, hs, e);
+  } catch (const std::exception&) {  // allocation failure on hostile input: never across the C ABI
+    ok = false;
+    e.code = AM_U_CAPACITY;
+    e.msg = "automerge_amd: document history exceeds the host memory limits";
+  }
+  if (!ok) {
     if (err) {
       err->code = e.code;
       err->is_type_error = 0;

@@ -278,6 +278,7 @@ __global__ __launch_bounds__(256) void k_copy_chunks(const uint8_t* __restrict__
 
 }  // namespace
 
+static_assert(kLanes * kSlice * sizeof(uint16_t) <= 160 * 1024, "k_inflate LDS exceeds the gfx950 workgroup limit");
 void am_launch_inflate_size(const uint8_t* arena, const am_chunk_desc* chunks, const uint32_t* zidx, uint32_t nz,
                             uint32_t* zlen, hipStream_t s) {
   if (!nz) return;

@@ -36,6 +36,7 @@ struct ChgHdr {              // decodeChangeHeader + column info (columnar.js:63
   int64_t seq, start_op, time;
   uint32_t actor_off, actors_off, deps_off, msg_off, extra_off;
   uint32_t actor_len, nactors, ndeps, msg_len, extra_len, has_extra;
+  uint32_t nunk;             // op columns outside CHANGE_COLUMNS
   uint32_t col_off[OC_NCOLS];
   uint32_t col_len[OC_NCOLS];
 };
@@ -62,6 +63,7 @@ struct DocHdr {              // decodeDocumentHeader (columnar.js:1006-1038)
   uint64_t base;
   uint32_t actors_off, heads_off, hidx_off, extra_off;
   uint32_t nactors, nheads, has_hidx, extra_len;
+  uint32_t nunk;             // op columns outside DOC_OPS_COLUMNS
   uint32_t ccol_off[DC_NCOLS];
   uint32_t ccol_len[DC_NCOLS];
   uint32_t ocol_off[OC_NCOLS];
@@ -72,13 +74,24 @@ struct DocHdr {              // decodeDocumentHeader (columnar.js:1006-1038)
 // order, i.e. ascending id order, so a second pass assigns offsets in spec order.
 // NSPEC is a compile-time constant so the slot writes are predicated register moves rather than
 // a dynamically indexed (scratch) array
+// Columns outside the spec (a future version's columns, new.js:1387-1425) are allowed among the
+// op columns (`unk` non-null): their bytes are counted in `unk_bytes` and skipped, and `pre[j]`
+// records the unknown bytes that precede spec column j in the data. Unknown ids in the pred / succ
+// groups (7, 8) would change the group structure of the known columns and stay unsupported.
 template <int NSPEC>
-__device__ __forceinline__ uint32_t parse_cols(Rd& r, const uint8_t* spec, uint32_t* len, bool is_change) {
+__device__ __forceinline__ uint32_t parse_cols(Rd& r, const uint8_t* spec, uint32_t* len, bool is_change,
+                                               uint32_t* pre = nullptr, uint32_t* nunk = nullptr, uint64_t* unk_bytes = nullptr) {
   int64_t num;
   TRY(rd_u53(r, num));
   int64_t last = -1;
+  uint64_t ub = 0;
+  uint32_t nu = 0;
 #pragma unroll
   for (int i = 0; i < NSPEC; i++) len[i] = 0;
+  if (pre) {
+#pragma unroll
+    for (int i = 0; i < NSPEC; i++) pre[i] = 0xffffffffu;
+  }
   for (int64_t i = 0; i < num; i++) {
     int64_t id, l;
     TRY(rd_u53(r, id));
@@ -91,18 +104,74 @@ __device__ __forceinline__ uint32_t parse_cols(Rd& r, const uint8_t* spec, uint3
     bool found = false;
 #pragma unroll
     for (int j = 0; j < NSPEC; j++)
-      if (spec[j] == id) { len[j] = (uint32_t)l; found = true; }
-    if (!found) return AM_U_UNKNOWN_COLUMN;
+      if (spec[j] == id) { len[j] = (uint32_t)l; found = true; if (pre) pre[j] = (uint32_t)ub; }
+    if (!found) {
+      if (!pre || (id >> 4) == 7 || (id >> 4) == 8 || id > 0xffff) return AM_U_UNKNOWN_COLUMN;
+      ub += (uint64_t)l;
+      nu++;
+    }
+  }
+  if (pre) {
+#pragma unroll
+    for (int i = 0; i < NSPEC; i++) if (pre[i] == 0xffffffffu) pre[i] = (uint32_t)ub;
+    *nunk = nu;
+    *unk_bytes = ub;
   }
   return AM_OK;
 }
+// data of the spec columns (table order = ascending id = spec order), unknown columns interleaved
 template <int NSPEC>
-__device__ __forceinline__ uint32_t place_cols(Rd& r, uint32_t* off, const uint32_t* len) {
+__device__ __forceinline__ uint32_t place_cols(Rd& r, uint32_t* off, const uint32_t* len, const uint32_t* pre = nullptr,
+                                               uint64_t unk_bytes = 0) {
+  const uint64_t at0 = r.off;
+  uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < NSPEC; k++) {
-    uint64_t at;
-    TRY(rd_raw(r, len[k], at));
-    off[k] = (uint32_t)at;
+    off[k] = (uint32_t)(at0 + acc + (pre ? pre[k] : 0u));
+    acc += len[k];
+  }
+  uint64_t at;
+  TRY(rd_raw(r, acc + unk_bytes, at));
+  return AM_OK;
+}
+// Visits the unknown op columns of a change or document chunk body: f(id, offset in data, length).
+template <typename F>
+__device__ uint32_t visit_unknown_cols(const uint8_t* data, uint64_t n, bool is_doc, F f) {
+  Rd r{data, n, 0};
+  int64_t v, l;
+  uint64_t at;
+  if (!is_doc) {
+    TRY(rd_u53(r, v)); TRY(rd_raw(r, (uint64_t)v * 32, at));
+    TRY(rd_u53(r, v)); TRY(rd_raw(r, (uint64_t)v, at));
+    TRY(rd_u53(r, v)); TRY(rd_u53(r, v)); TRY(rd_i53(r, v));
+    TRY(rd_u53(r, v)); TRY(rd_raw(r, (uint64_t)v, at));
+    TRY(rd_u53(r, v));
+    for (int64_t i = 0; i < v; i++) { TRY(rd_u53(r, l)); TRY(rd_raw(r, (uint64_t)l, at)); }
+  } else {
+    TRY(rd_u53(r, v));
+    for (int64_t i = 0; i < v; i++) { TRY(rd_u53(r, l)); TRY(rd_raw(r, (uint64_t)l, at)); }
+    TRY(rd_u53(r, v)); TRY(rd_raw(r, (uint64_t)v * 32, at));
+  }
+  // (document: the change-column table comes first; its data precedes the op columns' data)
+  uint64_t skip = 0;
+  if (is_doc) {
+    TRY(rd_u53(r, v));
+    for (int64_t i = 0; i < v; i++) { int64_t id; TRY(rd_u53(r, id)); TRY(rd_u53(r, l)); skip += (uint64_t)l; }
+  }
+  int64_t num;
+  TRY(rd_u53(r, num));
+  const uint64_t tab = r.off;
+  for (int64_t i = 0; i < num; i++) { int64_t id; TRY(rd_u53(r, id)); TRY(rd_u53(r, l)); }
+  uint64_t pos = r.off + skip;
+  r.off = tab;
+  const uint8_t* spec = is_doc ? kDocOpColIds : kChangeColIds;
+  for (int64_t i = 0; i < num; i++) {
+    int64_t id;
+    TRY(rd_u53(r, id)); TRY(rd_u53(r, l));
+    bool known = false;
+    for (int j = 0; j < OC_NCOLS; j++) known |= spec[j] == id;
+    if (!known) f((uint32_t)id, pos, (uint32_t)l);
+    pos += (uint64_t)l;
   }
   return AM_OK;
 }
@@ -135,8 +204,11 @@ __device__ __forceinline__ uint32_t parse_change_hdr(const uint8_t* data, uint64
     TRY(rd_u53(r, l));
     TRY(rd_raw(r, (uint64_t)l, at));
   }
-  TRY(parse_cols<OC_NCOLS>(r, kChangeColIds, h.col_len, true));
-  TRY(place_cols<OC_NCOLS>(r, h.col_off, h.col_len));
+  uint32_t pre[OC_NCOLS], nunk;
+  uint64_t ub;
+  TRY(parse_cols<OC_NCOLS>(r, kChangeColIds, h.col_len, true, pre, &nunk, &ub));
+  TRY(place_cols<OC_NCOLS>(r, h.col_off, h.col_len, pre, ub));
+  h.nunk = nunk;
   h.has_extra = r.off < r.n;
   h.extra_off = (uint32_t)r.off;
   h.extra_len = (uint32_t)(r.n - r.off);
@@ -160,10 +232,13 @@ __device__ __forceinline__ uint32_t parse_doc_hdr(const uint8_t* data, uint64_t 
   h.nheads = (uint32_t)v;
   TRY(rd_raw(r, (uint64_t)v * 32, at));
   h.heads_off = (uint32_t)at;
+  uint32_t pre[OC_NCOLS], nunk;
+  uint64_t ub;
   TRY(parse_cols<DC_NCOLS>(r, kDocChgColIds, h.ccol_len, false));
-  TRY(parse_cols<OC_NCOLS>(r, kDocOpColIds, h.ocol_len, false));
+  TRY(parse_cols<OC_NCOLS>(r, kDocOpColIds, h.ocol_len, false, pre, &nunk, &ub));
   TRY(place_cols<DC_NCOLS>(r, h.ccol_off, h.ccol_len));
-  TRY(place_cols<OC_NCOLS>(r, h.ocol_off, h.ocol_len));
+  TRY(place_cols<OC_NCOLS>(r, h.ocol_off, h.ocol_len, pre, ub));
+  h.nunk = nunk;
   h.has_hidx = r.off < r.n;
   h.hidx_off = (uint32_t)r.off;
   if (h.has_hidx) {
@@ -171,6 +246,27 @@ __device__ __forceinline__ uint32_t parse_doc_hdr(const uint8_t* data, uint64_t 
   }
   h.extra_off = (uint32_t)r.off;
   h.extra_len = (uint32_t)(r.n - r.off);
+  return AM_OK;
+}
+
+// unknown op columns: count and a bound on their values (every column holds a value per row, or,
+// in an unknown column group, one per entry of that group: at most the sum of its cardinalities)
+__device__ static uint32_t unknown_bound(const uint8_t* data, uint64_t n, bool is_doc, uint32_t nunk, uint32_t nrows,
+                                         ChunkInfo& ci) {
+  uint64_t cards = 0;
+  uint32_t st = AM_OK;
+  uint32_t e = visit_unknown_cols(data, n, is_doc, [&](uint32_t id, uint64_t off, uint32_t l) {
+    if ((id & 7) != 0 || st) return;
+    uint64_t cnt, sum;
+    st = rle_count_sum_i(data + off, l, false, cnt, sum, 0);
+    cards += sum;
+  });
+  if (e) return e;
+  if (st) return st;
+  const uint64_t b = (uint64_t)(nunk + 1) * ((uint64_t)nrows + cards) + 2ull * nrows;
+  if (b > 0x3fffffffull) return AM_U_CAPACITY;
+  ci.nunk = nunk;
+  ci.unkvals = (uint32_t)b;
   return AM_OK;
 }
 
@@ -186,7 +282,7 @@ __device__ __forceinline__ void chunk_body(const uint8_t* p, const am_chunk_desc
 #pragma unroll
   for (int k = 0; k < 8; k++) hw[k] = 0;
   ci.status = AM_OK; ci.type = 0xff; ci.data_off = 0; ci.data_len = 0; ci.nops = 0; ci.nents = 0; ci.nchg = 0;
-  ci.ndeps = 0; ci.nactors = 0; ci.strbytes = 0; ci.nheads = 0; ci.arg0 = 0;
+  ci.ndeps = 0; ci.nactors = 0; ci.strbytes = 0; ci.nheads = 0; ci.arg0 = 0; ci.nunk = 0; ci.unkvals = 0;
   uint32_t st = AM_OK;
   do {
     // decodeContainerHeader (columnar.js:688)
@@ -237,6 +333,7 @@ __device__ __forceinline__ void chunk_body(const uint8_t* p, const am_chunk_desc
       uint64_t scnt, ssum;
       if ((st = rle_count_sum_i(data + hh.col_off[OC_KEY_STR], hh.col_len[OC_KEY_STR], true, scnt, ssum, 0))) break;
       ci.strbytes = (uint32_t)ssum + hh.msg_len;
+      if (hh.nunk && (st = unknown_bound(data, len, false, hh.nunk, ci.nops, ci))) break;
     } else if (ci.type == 0) {
       if (r.off != cd.len) { st = AM_E_DOC_TRAILING; break; }
       DocHdr dh;
@@ -268,6 +365,7 @@ __device__ __forceinline__ void chunk_body(const uint8_t* p, const am_chunk_desc
       if ((st = rle_count_sum_i(data + dh.ocol_off[OC_KEY_STR], dh.ocol_len[OC_KEY_STR], true, cnt, s1, 0))) break;
       if ((st = rle_count_sum_i(data + dh.ccol_off[DC_MESSAGE], dh.ccol_len[DC_MESSAGE], true, cnt, s2, 0))) break;
       ci.strbytes = (uint32_t)(s1 + s2);
+      if (dh.nunk && (st = unknown_bound(data, len, true, dh.nunk, ci.nops, ci))) break;
     } else {
       st = AM_E_CHUNK_TYPE;
       ci.arg0 = ci.type;
@@ -324,12 +422,13 @@ __global__ void __launch_bounds__(256) k_bounds(const am_doc_desc* __restrict__ 
   if (d >= ndocs) return;
   am_doc_desc dd = docs[d];
   DocBounds b;
-  uint64_t R = 0, E = 0, C = 0, D = 0, A = 0, H = 0, S = 0, B = 0, AM = 0, ND = 0;
+  uint64_t R = 0, E = 0, C = 0, D = 0, A = 0, H = 0, S = 0, B = 0, AM = 0, ND = 0, UC = 0, UV = 0;
   uint64_t lo = ~0ull, hi = 0;
   if (dd.base_chunk >= 0) {
     const ChunkInfo& ci = info[dd.base_chunk];
     R += ci.nops; E += ci.nents; C += ci.nchg; D += ci.ndeps; A += ci.nactors; H += ci.nheads;
     S += ci.strbytes; B += chunks[dd.base_chunk].len;
+    UC += ci.nunk; UV += ci.unkvals;
     lo = chunks[dd.base_chunk].off;
     hi = lo + chunks[dd.base_chunk].len;
   }
@@ -338,6 +437,7 @@ __global__ void __launch_bounds__(256) k_bounds(const am_doc_desc* __restrict__ 
     const am_chunk_desc cd = chunks[dd.chg_begin + k];
     R += ci.nops; E += ci.nents; C += 1; D += ci.ndeps; A += 1; H += 1; S += ci.strbytes;
     B += cd.len;
+    UC += ci.nunk; UV += ci.unkvals;
     AM += ci.nactors;
     ND += ci.ndeps;
     if (cd.off < lo) lo = cd.off;
@@ -347,12 +447,13 @@ __global__ void __launch_bounds__(256) k_bounds(const am_doc_desc* __restrict__ 
   // chunks of one document are normally adjacent; a scattered document is not staged in LDS
   if (hi - lo > 2 * B + 64) hi = lo;
   const uint64_t cap = 0x3fffffffull;
-  if (R > cap || E > cap || C > cap || D > cap || AM > cap || ND > cap) { R = E = C = D = AM = ND = 0; A = H = 0; S = B = 0; lo = hi = 0; }
+  if (R > cap || E > cap || C > cap || D > cap || AM > cap || ND > cap || UV > cap) { R = E = C = D = AM = ND = UC = UV = 0; A = H = 0; S = B = 0; lo = hi = 0; }
   b.R = (uint32_t)R; b.E = (uint32_t)E; b.C = (uint32_t)C; b.D = (uint32_t)D; b.A = (uint32_t)A;
   b.H = (uint32_t)H; b.N = dd.chg_count; b.K = (uint32_t)(H + dd.known_count); b.AM = (uint32_t)AM;
   b.ND = (uint32_t)ND; b.S = S; b.B = B; b.span_lo = lo; b.span_hi = hi;
   b.P = (dd.flags & AM_DOC_WANT_PATCH) ? 1u : (dd.flags & AM_DOC_WANT_DIFF) ? 2u : 0u;
-  b.pad = 0;
+  b.U = ((dd.flags & AM_DOC_FIX_UTF8) ? 1u : 0u) | ((dd.flags & AM_DOC_PATCH_ROOM) ? 2u : 0u);
+  b.UC = (uint32_t)UC; b.UV = (uint32_t)UV;
   WsLayout L = ws_layout(b);
   bounds[d] = b;
   ws_bytes[d] = L.total;
@@ -458,6 +559,8 @@ struct DocShared {
   uint64_t out_len;
   uint32_t tmp[DOC_T + 1];
   uint64_t ph_last;
+  uint32_t xs_used;                       // bytes of replaced strings after the staged input (b.U)
+  uint32_t nunk_inst, nunk_ids;           // unknown op columns: instances, distinct output columns
 };
 
 __device__ static void set_err(DocShared& s, uint32_t code, int64_t a0 = 0, int64_t a1 = 0, uint64_t actor_off = 0,

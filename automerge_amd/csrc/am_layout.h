@@ -33,7 +33,10 @@ struct DocBounds {
   uint32_t AM;  // actor-map entries (sum of change actor lists)
   uint32_t ND;  // sum of change deps (plan)
   uint32_t P;   // 1: write the getPatch() log (AM_DOC_WANT_PATCH); 2: the applyChanges patch (AM_DOC_WANT_DIFF)
-  uint32_t pad;
+  uint32_t U;   // bit0: invalid UTF-8 keys / messages are replaced (AM_DOC_FIX_UTF8): room for 3 bytes per input
+                // byte; bit1: 8x applyChanges-patch pools (AM_DOC_PATCH_ROOM)
+  uint32_t UC;  // instances of unknown op columns over the document's chunks (new.js:1387-1425)
+  uint32_t UV;  // bound on their values
   uint64_t S;   // key + message string bytes over all rows
   uint64_t B;   // input bytes (base + changes)
   uint64_t span_lo, span_hi;  // arena byte span covering the document's chunks
@@ -57,7 +60,12 @@ struct WsLayout {
   uint64_t pwire, pwire_cap;  // the same log in wire form (PatchHdr2 + stream, am_patch.h)
   uint64_t etime, passend, dscr;  // applyChanges patch (P == 2): succ-entry times, pass ends, replay pools
   uint64_t colbuf[OC_NCOLS + DC_NCOLS];
+  // unknown op columns (UC > 0): instance table, decoded values, per-(source, column) instance
+  // map, the output columns' ids / lengths / positions, per-row group offsets, encoded output
+  uint64_t unk_inst, unk_cells, unk_map, unk_ids, unk_rowoff, unk_out, unk_out_cap;
 };
+
+#define AM_SZ_UNKINST 48
 
 AM_HD inline uint32_t am_pow2(uint32_t n) {
   uint32_t p = 1;
@@ -114,7 +122,7 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   L.dref_idx = take((uint64_t)b.ND * 8);
   L.docpos = take((uint64_t)(b.A + N) * 4);
   L.head_ref = take((uint64_t)b.H * 4);
-  L.input = take(b.span_hi - b.span_lo);
+  L.input = take((b.span_hi - b.span_lo) + ((b.U & 1) ? 3 * b.S + 64 : 0));
   // union region
   L.u0 = o;
   L.idk = take(PR * AM_SZ_IDKEY);
@@ -131,6 +139,7 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   const uint64_t cells_end = L.u0 + (((13 * R + 2 * E) * 8 + 15) & ~(uint64_t)15);
   if (cells_end > uend) uend = cells_end;
   uint64_t nm = R;
+  if (b.UV > nm) nm = b.UV;
   if (E > nm) nm = E;
   if (C > nm) nm = C;
   if (D > nm) nm = D;
@@ -163,6 +172,12 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
     L.colbuf[c] = take(bound);
     cap += bound;
   }
+  // unknown op columns: a value costs at most 8 LEB bytes plus 2 bytes of RLE headers; raw bytes
+  // come from the input
+  const uint64_t UC = b.UC;
+  L.unk_out_cap = UC ? UC * (10 * (R + b.UV) + 16 + 20) + b.B : 0;
+  L.unk_out = UC ? take(L.unk_out_cap) : 0;
+  cap += L.unk_out_cap;
   // document: header + actor ids + heads + column table + data + headsIndexes + extra bytes
   cap += 64 + 10 * (uint64_t)b.A + b.B + 42 * (uint64_t)b.H + 25 * 20 + b.B;
   L.out_cap = cap;
@@ -174,8 +189,9 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
     L.patch = take(64 + 64 * L.patch_nrec + 32 * L.patch_nmval + L.patch_heap);
   } else if (b.P == 2) {
     // actors + clock + one section per object + keys + prop entries / edits (am_diff.h pools)
-    L.patch_nrec = b.A + C + 2 + 2 * (R + 2) + 8 * R + 128;
-    L.patch_nmval = 4 * R + 64;
+    const uint64_t ps = (b.U & 2) ? 8 : 1;
+    L.patch_nrec = b.A + C + 2 + 2 * (R + 2) + ps * (8 * R + 128);
+    L.patch_nmval = ps * (4 * R + 64);
     L.patch_heap = b.S + 2 * b.B + 16;
     L.patch = take(64 + 64 * L.patch_nrec + 32 * L.patch_nmval + L.patch_heap);
   } else {
@@ -187,9 +203,18 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   if (b.P == 2) {
     L.etime = take(4 * (E + 1));
     L.passend = take(4 * (N + 1));
-    L.dscr = take(diff_scratch_bytes(R, E));
+    L.dscr = take(diff_scratch_bytes(R, E, (b.U & 2) ? 8 : 1));
   } else {
     L.etime = L.passend = L.dscr = 0;
+  }
+  if (UC) {
+    L.unk_inst = take(UC * AM_SZ_UNKINST);
+    L.unk_cells = take(((uint64_t)b.UV + 2 * R + 2) * 8);
+    L.unk_map = take((N + 1) * UC * 4);
+    L.unk_ids = take(UC * 16);
+    L.unk_rowoff = take((R + 1) * 4);
+  } else {
+    L.unk_inst = L.unk_cells = L.unk_map = L.unk_ids = L.unk_rowoff = 0;
   }
   L.total = o;
   return L;

@@ -72,7 +72,8 @@ enum am_status {
   AM_U_HASH_GRAPH = 100,    // needs the deferred hash graph of a loaded document (new.js:1826-1832)
   AM_U_UNKNOWN_COLUMN,      // column id outside DOC_OPS_COLUMNS / CHANGE_COLUMNS (new.js:1387-1425)
   AM_U_NONCAUSAL,           // opId counters violate Lamport order (insert after a later element, ...)
-  AM_U_UTF8,                // invalid UTF-8 in a key or message (reference would canonicalise to U+FFFD)
+  AM_U_UTF8,                // invalid UTF-8 in a key or message and the document was staged without
+                            // AM_DOC_FIX_UTF8: stage it again with the flag (the per-document calls do)
   AM_U_DEL_SHAPE,           // del op without preds, or inserting del (reference keeps it as a row)
   AM_U_VALUE,               // null action / null pred / mixed map+list object / 2^31+ sizes
   AM_U_CAPACITY,            // workspace bound exceeded (internal)
@@ -95,6 +96,8 @@ typedef struct am_doc_desc {
 } am_doc_desc;
 #define AM_DOC_WANT_PATCH 2u
 #define AM_DOC_WANT_DIFF 4u
+#define AM_DOC_PATCH_ROOM 16u /* 8x the applyChanges-patch pools (a rerun after a patch capacity report) */
+#define AM_DOC_FIX_UTF8 8u   /* k_doc reserves room for U+FFFD replacements of invalid UTF-8 (encoding.js:15-17) */
 typedef struct am_known_hash {      // changeIndexByHash entry supplied by the host
   uint8_t hash[32];
   int64_t index;
