@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-phase k_doc cycle profile (probe build with -DAM_PHASE_CLOCK, see tools/build_probe.sh).
 
-  AM_LIB_PATH=tools/probe/libam_clock.so python tools/phase_clock.py [--docs D]
+  AM_LIB_PATH=tools/clock/libam_clock.so python tools/phase_clock.py [--docs D]
 Prints, for each k_doc phase, the average s_memtime cycles per sampled document (every 64th).
 """
 import argparse
@@ -17,16 +17,18 @@ NAMES = ["P0 stage input", "P1 headers", "P2a lookups", "P2b plan (serial)", "P4
 FAST = ["F0 status+stage input", "F1 headers+hashes+refs", "F2 canon+actor table", "F3 base change rows",
         "F4 queue+deps+heads", "F5 op column decode", "F6 rows+entries+checks", "F7 id sort+key rank",
         "F8 preds+elements", "F9 RGA", "F10 doc order+succ", "F11 encode change cols", "F12 encode op cols",
-        "F13 trailer+header+copy"]
+        "F13 trailer+header+copy", "F14 patch (fast_diff)"]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--docs", type=int, default=65536)
     ap.add_argument("--text", type=int, default=0, help="C3 text histories of this many changes instead of C4")
+    ap.add_argument("--patch", action="store_true", help="stage with AM_DOC_WANT_DIFF (the applyChanges patch)")
     args = ap.parse_args()
-    from automerge_amd import _native, workload
-    from automerge_amd.batch import Batch
+    import workload
+    from automerge_amd import _native
+    from automerge_amd.batch import WANT_DIFF, Batch
     lib = _native.lib
     f = lib.amx_phase_cycles
     f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
@@ -34,6 +36,8 @@ def main():
         arena, chunks, docs, ops = workload.text(0, args.docs, args.text, 100, 10)
     else:
         arena, chunks, docs, ops = workload.c4(0, args.docs)
+    if args.patch:
+        docs["flags"] |= WANT_DIFF
     b = Batch(device=0)
     b.stage(arena, chunks, docs)
     b.run(); b.sync()
