@@ -50,7 +50,6 @@ struct ChunkInfo {
   uint32_t strbytes;        // bytes of key strings over all rows (+ messages)
   uint32_t nheads;          // doc: heads
   uint32_t nunk;            // op columns outside the known column set (new.js:1387-1425)
-  uint32_t unkvals;         // bound on the values of those columns (rows, or group entries, per column)
   int64_t arg0;             // error argument
 };
 

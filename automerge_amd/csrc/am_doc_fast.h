@@ -33,6 +33,13 @@
       ph_last = now_;                                                                 \
     }                                                                                 \
   } while (0)
+#elif defined(FD_STOP)
+// probe builds (tools/build_stop.sh): the kernel returns after phase FD_STOP, so PMC counters of
+// the variants give the instructions of each phase
+#define FPH(k)                   \
+  do {                           \
+    if ((k) == FD_STOP) return;  \
+  } while (0)
 #else
 #define FPH(k) \
   do {         \
@@ -429,6 +436,29 @@ __device__ __forceinline__ uint32_t enc32(uint32_t n, int32_t v, bool isnull, ui
   if constexpr (K == EK_U || K == EK_D) {
     if (act && !nul && v < 0) bad = true;
   }
+  if constexpr (K != EK_W && K != EK_B) {
+    if (!__any(act && !nul)) return 0;  // nulls only: nothing is written (RLEEncoder.finish)
+  }
+  if constexpr (K == EK_U || K == EK_S) {
+    // one value n times: a single repetition (n >= 2) or literal (n == 1) record, written by lane 0
+    const int32_t v0 = wave::bcast(v, 0);
+    const bool differs = act && (nul || (K == EK_U ? v != v0 : (l > 0 && !eqs)));
+    if (!__any(differs)) {
+      const uint32_t sl0 = K == EK_S ? wave::bcast(slen, 0) : 0u;
+      const uint32_t vs0 = K == EK_U ? uleb_len32((uint32_t)v0) : uleb_len32(sl0) + sl0;
+      const uint32_t total = (n >= 2 ? sleb_len32((int32_t)n) : 1u) + vs0;
+      if (total > cap) return ~0u;
+      if (l == 0) {
+        uint8_t* o = put_sleb32(out, n >= 2 ? (int32_t)n : -1);
+        if constexpr (K == EK_U) put_uleb32(o, (uint32_t)v0);
+        else {
+          o = put_uleb32(o, sl0);
+          for (uint32_t q = 0; q < sl0; q++) o[q] = in[soff + q];
+        }
+      }
+      return total;
+    }
+  }
   if constexpr (K == EK_D) {
     const int32_t pi = incl_max(act && !nul ? (int32_t)l : -1);
     const int32_t prev = wave::up1(pi, -1);
@@ -455,7 +485,6 @@ __device__ __forceinline__ uint32_t enc32(uint32_t n, int32_t v, bool isnull, ui
   } else if constexpr (K == EK_B) {
     bytes = st ? uleb_len32(rl) + ((l == 0 && v) ? 1u : 0u) : 0u;
   } else {
-    if (!__any(act && !nul)) return 0;  // nulls only: nothing is written (RLEEncoder.finish)
     const bool single = st && !nul && rl == 1;
     const uint64_t SM = __ballot(single);
     gs = single && !(l > 0 && ((SM >> (l - 1)) & 1));
@@ -494,6 +523,73 @@ __device__ __forceinline__ uint32_t enc32(uint32_t n, int32_t v, bool isnull, ui
           for (uint32_t q = 0; q < slen; q++) o[q] = in[soff + q];
         }
       }
+    }
+  }
+  return total;
+}
+// enc32 for four narrow columns at once: each 16-lane DPP row encodes its own column (U or D kind,
+// n <= 16 values, lane p of the row holds value p). Scans, neighbour moves and run searches stay
+// inside the row (row_shr DPP, the row's 16 bits of a ballot). Returns the row's column length, or
+// ~0u when it would exceed `cap`.
+template <uint8_t K>
+__device__ __forceinline__ uint32_t enc32r(uint32_t n, int32_t v, bool isnull, uint8_t* out, uint32_t cap, bool& bad) {
+  static_assert(K == EK_U || K == EK_D, "row encoder: integer kinds");
+  const uint32_t l = lane(), p = l & 15, rb = l & ~15u;
+  const bool act = p < n;
+  const bool nul = act && isnull;
+  if (act && !nul && v < 0) bad = true;
+  if constexpr (K == EK_D) {
+    const int32_t I = INT32_MIN;
+    int32_t pi = act && !nul ? (int32_t)p : -1;
+    pi = max(pi, wave::dpp<wave::ROW_SHR1>(I, pi));
+    pi = max(pi, wave::dpp<wave::ROW_SHR2>(I, pi));
+    pi = max(pi, wave::dpp<wave::ROW_SHR4>(I, pi));
+    pi = max(pi, wave::dpp<wave::ROW_SHR8>(I, pi));
+    const int32_t prev = wave::dpp<wave::ROW_SHR1>(-1, pi);  // last non-null position before p
+    const int32_t pv = __shfl(v, (int)(rb + (prev < 0 ? 0u : (uint32_t)prev)), 64);
+    if (act && !nul) v -= prev < 0 ? 0 : pv;
+  }
+  const int32_t pv = wave::dpp<wave::ROW_SHR1>(0, v);
+  const uint32_t pn = wave::dpp<wave::ROW_SHR1>(0u, (uint32_t)nul);
+  bool same = false;
+  if (act && p > 0) {
+    if (nul) same = pn != 0;
+    else if (pn) same = false;
+    else same = pv == v;
+  }
+  const bool st = act && !same;
+  const uint32_t rowm = (uint32_t)(__ballot(st) >> rb) & 0xffffu;
+  const uint32_t above = rowm >> (p + 1);
+  const uint32_t rl = (above ? p + 1 + (uint32_t)__builtin_ctz(above) : n) - p;
+  const bool row_any = ((uint32_t)(__ballot(act && !nul) >> rb) & 0xffffu) != 0;
+  const bool single = st && !nul && rl == 1;
+  const uint32_t srow = (uint32_t)(__ballot(single) >> rb) & 0xffffu;
+  const bool gs = single && !(p > 0 && ((srow >> (p - 1)) & 1));
+  const uint32_t gcnt = gs ? (uint32_t)__builtin_ctz(~(srow >> p)) : 0u;
+  const uint32_t vs = K == EK_U ? uleb_len32((uint32_t)v) : sleb_len32(v);
+  uint32_t bytes = 0;
+  if (st && row_any) {
+    if (nul) bytes = 1 + uleb_len32(rl);
+    else if (rl >= 2) bytes = sleb_len32((int32_t)rl) + vs;
+    else bytes = vs + (gs ? sleb_len32(-(int32_t)gcnt) : 0u);
+  }
+  uint32_t x = bytes;
+  x += wave::dpp<wave::ROW_SHR1>(0u, x);
+  x += wave::dpp<wave::ROW_SHR2>(0u, x);
+  x += wave::dpp<wave::ROW_SHR4>(0u, x);
+  x += wave::dpp<wave::ROW_SHR8>(0u, x);
+  const uint32_t total = (uint32_t)__shfl((int)x, (int)(rb + 15), 64);
+  if (total > cap) return ~0u;
+  if (bytes) {
+    uint8_t* o = out + (x - bytes);
+    if (nul) {
+      *o++ = 0;
+      put_uleb32(o, rl);
+    } else {
+      if (rl >= 2) o = put_sleb32(o, (int32_t)rl);
+      else if (gs) o = put_sleb32(o, -(int32_t)gcnt);
+      if constexpr (K == EK_U) put_uleb32(o, (uint32_t)v);
+      else put_sleb32(o, v);
     }
   }
   return total;
@@ -1104,14 +1200,28 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   // ready in list order and carry the next seq of its author ----
   uint32_t prior = 0;  // earlier changes of this call by the same author
   for (uint32_t j = 0; j < N; j++) prior += (wave::bcast(a_dp, (int)j) == a_dp && j < l) ? 1u : 0u;
-  if (l < N) {
-    uint32_t mine[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) mine[k] = HT[8 * l + k];
-    for (uint32_t t = 0; t < N + HB + K; t++) {
-      if (t == l || (t < N && t > l)) continue;
-      if (words_eq(HT + 8 * t, mine)) { bad = true; break; }  // duplicate / already applied
+  // hash t's first 8 bytes in lane t (t < N + HB + K): candidates are found by broadcasting the
+  // prefixes (readlane, no LDS traffic); only a prefix hit compares the full 32 bytes
+  const uint32_t NHT = N + HB + K;
+  const uint64_t hpre = l < NHT ? (((uint64_t)HT[8 * l + 1] << 32) | HT[8 * l]) : ~0ull;
+  {
+    uint64_t hitmask = 0;  // (lane-local) earlier changes / heads / known hashes with an equal prefix
+    for (uint32_t t = 0; t < NHT; t++) {
+      const uint64_t pt = wave::bcast(hpre, (int)t);
+      if (pt == hpre && t != l && !(t < N && t > l)) hitmask |= 1ull << t;
     }
+    if (l < N) {
+      uint32_t mine[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) mine[k] = HT[8 * l + k];
+      while (hitmask) {
+        const uint32_t t = (uint32_t)__builtin_ctzll(hitmask);
+        hitmask &= hitmask - 1;
+        if (words_eq(HT + 8 * t, mine)) { bad = true; break; }  // duplicate / already applied
+      }
+    }
+  }
+  if (l < N) {
     const uint32_t* CLK = reinterpret_cast<const uint32_t*>(M + FM_CLOCK);
     const int64_t expect = (int64_t)(a_dp < NB ? CLK[a_dp] : 0u) + prior + 1;
     bad |= chh[l].seq != expect;
@@ -1130,21 +1240,33 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   int64_t dep_idx = 0;
   const uint32_t dep_c = l < nd_total ? M[FM_DOWN + l] : 0u;
   const uint32_t dep_b = __shfl(dbase, dep_c, 64);
+  uint32_t w[8];
+  uint64_t dpre = ~0ull;
+  if (l < nd_total) {
+    const ChgHdrC& h = chh[dep_c];
+    load32(IN + (h.base + h.deps_off + 32 * (l - dep_b) - a0), w);
+    dpre = ((uint64_t)w[1] << 32) | w[0];
+  }
+  uint64_t dmask = 0;  // hashes with the dependency's prefix
+  for (uint32_t t = 0; t < NHT; t++)
+    if (wave::bcast(hpre, (int)t) == dpre) dmask |= 1ull << t;
   if (l < nd_total) {
     const uint32_t c = dep_c;
-    const ChgHdrC& h = chh[c];
-    uint32_t w[8];
-    load32(IN + (h.base + h.deps_off + 32 * (l - dep_b) - a0), w);
     int32_t hit = -1;
-    for (uint32_t t = N; t < N + HB + K && hit < 0; t++)
+    // base heads and host-known hashes first, then the changes of this call
+    for (uint64_t m = dmask >> N; m && hit < 0; m &= m - 1) {
+      const uint32_t t = N + (uint32_t)__builtin_ctzll(m);
       if (words_eq(HT + 8 * t, w)) hit = (int32_t)t;
+    }
     if (hit >= 0) {
       dep_idx = hit < (int32_t)(N + HB) ? reinterpret_cast<const int64_t*>(M + FM_BHIDX)[hit - N]
                                         : reinterpret_cast<const int64_t*>(M + FM_KIDX)[hit - N - HB];
       if (dep_idx < 0) bad = true;
     } else {
-      for (uint32_t t = 0; t < N && hit < 0; t++)
+      for (uint64_t m = dmask & (N < 64 ? (1ull << N) - 1 : ~0ull); m && hit < 0; m &= m - 1) {
+        const uint32_t t = (uint32_t)__builtin_ctzll(m);
         if (words_eq(HT + 8 * t, w)) hit = (int32_t)t;
+      }
       if (hit < 0 || (uint32_t)hit >= c) bad = true;  // missing or later: the change would wait
       dep_idx = (int64_t)nbc + hit;
     }
@@ -1657,11 +1779,41 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     bad |= act && (v_act < 0 || v_act > 0x7fffffff || v_seq < 0 || v_seq > 0x7fffffff || v_max < 0 || v_max > 0x7fffffff ||
                    (v_xlen != AM_NULL64 && (v_xlen < 0 || v_xlen > 0x7fffffff)));
     bad |= l < ND && (v_deps < 0 || v_deps > 0x7fffffff);
+    // narrow integer columns (NC <= 16 change rows): one 16-lane row each, four columns per encoder
+    // pass (enc32r), staged at the end of the image region and copied into place below
+    constexpr uint32_t kRowCap = 176;  // 16 values x (1 + 5 + 5) bytes
+    const bool t31 = __all(!act || v_time == AM_NULL64 || (v_time >= 0 && v_time <= 0x7fffffff));
+    const bool seg = NC <= 16 && F.cells_cap >= cur + 8 * kRowCap + 64;
+    const uint32_t tbase = F.cells_cap - 8 * kRowCap;
+    uint32_t seglen[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // rows: U {actor, depsNum, extraLen}, D {seq, maxOp, time}
+    if (seg) {
+      const uint32_t g = l >> 4, p = l & 15;
+      const int32_t a = __shfl((int32_t)v_act, (int)p, 64), nd = __shfl((int32_t)v_nd, (int)p, 64);
+      const int32_t xl = __shfl((int32_t)v_xlen, (int)p, 64);
+      const bool xn = __shfl((int32_t)(v_xlen == AM_NULL64), (int)p, 64) != 0;
+      const uint32_t lu = enc32r<EK_U>(g < 3 ? NC : 0u, g == 0 ? a : g == 1 ? nd : xl, g == 2 && xn, OB + tbase + g * kRowCap,
+                                       kRowCap, bad);
+      const int32_t sq = __shfl((int32_t)v_seq, (int)p, 64), mx = __shfl((int32_t)v_max, (int)p, 64);
+      const int32_t tm = __shfl((int32_t)v_time, (int)p, 64);
+      const bool tn = __shfl((int32_t)(v_time == AM_NULL64), (int)p, 64) != 0;
+      const uint32_t ld = enc32r<EK_D>(g < (t31 ? 3u : 2u) ? NC : 0u, g == 0 ? sq : g == 1 ? mx : tm, g == 2 && tn,
+                                       OB + tbase + (4 + g) * kRowCap, kRowCap, bad);
+#pragma unroll
+      for (int r = 0; r < 4; r++) { seglen[r] = wave::bcast(lu, 16 * r); seglen[4 + r] = wave::bcast(ld, 16 * r); }
+    }
+    const uint32_t cap_end = seg ? tbase : F.cells_cap;
 #pragma unroll 1
     for (int col = 0; col < DC_NCOLS; col++) {
       uint32_t len;
-      if (col == DC_TIME) {
-        len = enc_col(EK_D, NC, v_time, v_time == AM_NULL64, 0, 0, false, IN, OB + cur, F.cells_cap - cur);
+      const int srow = !seg ? -1 : col == DC_ACTOR ? 0 : col == DC_DEPS_NUM ? 1 : col == DC_EXTRA_LEN ? 2 : col == DC_SEQ ? 4
+                                 : col == DC_MAXOP ? 5 : (col == DC_TIME && t31) ? 6 : -1;
+      if (srow >= 0) {
+        len = seglen[srow];
+        if (len == ~0u || cur + len > cap_end) { bad = true; break; }
+        const uint8_t* src = OB + tbase + srow * kRowCap;
+        for (uint32_t q = l; q < len; q += 64) OB[cur + q] = src[q];
+      } else if (col == DC_TIME) {
+        len = enc_col(EK_D, NC, v_time, v_time == AM_NULL64, 0, 0, false, IN, OB + cur, cap_end - cur);
       } else {
         int32_t v = 0;
         bool nul = false;
@@ -1676,12 +1828,13 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
           case DC_EXTRA_LEN: nul = v_xlen == AM_NULL64; v = (int32_t)v_xlen; break;
           default: so = x_off; sl = x_len; break;
         }
-        len = enc32k(kEncKind[OC_NCOLS + col], n, v, nul, so, sl, meq, IN, OB + cur, F.cells_cap - cur, bad);
+        len = enc32k(kEncKind[OC_NCOLS + col], n, v, nul, so, sl, meq, IN, OB + cur, cap_end - cur, bad);
       }
       if (len == ~0u) { bad = true; break; }
       if (l == 0) COLLEN[OC_NCOLS + col] = len;
       cur += len;
     }
+    wsync();  // the staged rows are read before the op columns overwrite the region
   }
   FPH(11);
   FD_CHECK();
@@ -1743,16 +1896,16 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     }
   }
   FD_CHECK();
-  // header, written to end exactly at T0 (encodeDocumentHeader, columnar.js:983-1004)
-  uint32_t nce = 0, noe = 0, ctab = 0, coltot = 0;
-  for (int c = 0; c < DC_NCOLS; c++) {
-    const uint32_t len = COLLEN[OC_NCOLS + c];
-    if (len) { nce++; ctab += uleb_len(kDocChgColIds[c]) + uleb_len(len); coltot += len; }
-  }
-  for (int c = 0; c < OC_NCOLS; c++) {
-    const uint32_t len = COLLEN[c];
-    if (len) { noe++; ctab += uleb_len(kDocOpColIds[c]) + uleb_len(len); coltot += len; }
-  }
+  // header, written to end exactly at T0 (encodeDocumentHeader, columnar.js:983-1004). Column
+  // table entries: lane e < 25 holds entry e (the 9 change columns, then the 16 op columns)
+  const bool t_chg = l < DC_NCOLS, t_any = l < DC_NCOLS + OC_NCOLS;
+  const uint32_t e_len = t_any ? COLLEN[t_chg ? OC_NCOLS + l : l - DC_NCOLS] : 0u;
+  const uint32_t e_id = t_any ? (t_chg ? kDocChgColIds[l] : kDocOpColIds[l - DC_NCOLS]) : 0u;
+  const uint32_t e_bytes = e_len ? uleb_len32(e_id) + uleb_len32(e_len) : 0u;
+  uint32_t ctab, coltot;
+  const uint32_t e_pos = excl_add(e_bytes, ctab);
+  excl_add(e_len, coltot);
+  const uint32_t nce = (uint32_t)__popcll(__ballot(t_chg && e_len)), noe = (uint32_t)__popcll(__ballot(!t_chg && e_len));
   const uint32_t pre_cols = uleb_len(NA) + alen_sum + uleb_len(NH) + 32 * NH + uleb_len(nce) + uleb_len(noe) + ctab;
   const uint64_t body = (uint64_t)pre_cols + coltot + hib + xlen;
   const uint32_t hs = 9 + uleb_len(body) + pre_cols;
@@ -1778,13 +1931,16 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
       put_uleb(o, NA);
       o = put_uleb(OB + heads0, NH);
       o += 32 * NH;
-      o = put_uleb(o, nce);
-      for (int c = 0; c < DC_NCOLS; c++)
-        if (COLLEN[OC_NCOLS + c]) { o = put_uleb(o, kDocChgColIds[c]); o = put_uleb(o, COLLEN[OC_NCOLS + c]); }
-      o = put_uleb(o, noe);
-      for (int c = 0; c < OC_NCOLS; c++)
-        if (COLLEN[c]) { o = put_uleb(o, kDocOpColIds[c]); o = put_uleb(o, COLLEN[c]); }
+      put_uleb(o, nce);
     }
+    // [nce] change-column entries [noe] op-column entries
+    const uint32_t tab0 = hbytes0 + 32 * NH + uleb_len(nce);
+    if (e_len) {
+      uint8_t* o = OB + tab0 + e_pos + (t_chg ? 0u : uleb_len(noe));
+      o = put_uleb32(o, e_id);
+      put_uleb32(o, e_len);
+    }
+    if (l == DC_NCOLS) put_uleb32(OB + tab0 + e_pos, noe);  // e_pos of the first op entry = end of the change entries
   }
   wsync();
   // copy the image [start, cols_end + hib + xlen) to the document's output slot, one dword per lane

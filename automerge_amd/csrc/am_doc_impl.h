@@ -621,6 +621,12 @@ __device__ __forceinline__ uint8_t* enc_put(uint8_t kind, uint8_t* o, int64_t v,
   return o + l;
 }
 
+// wave-level barrier: encode_column runs on wave 0 alone (the other waves of a global-mode
+// workgroup wait at the next __syncthreads)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
 // Encodes the n values of column c (V already filled) into out; returns the byte length.
 __device__ static uint32_t encode_column(uint8_t kind, uint32_t n, uint8_t* out, EncCtx& x, uint32_t* s_flag) {
   const uint32_t t = threadIdx.x;
@@ -640,7 +646,7 @@ __device__ static uint32_t encode_column(uint8_t kind, uint32_t n, uint8_t* out,
       if (top > carry) carry = top;
     }
     X = x.W;
-    __syncthreads();
+    wave_sync();
   }
   // maximal runs: start positions compacted into RS
   uint32_t nr = 0;
@@ -653,7 +659,7 @@ __device__ static uint32_t encode_column(uint8_t kind, uint32_t n, uint8_t* out,
   }
   const bool rle = kind <= EK_S;
   for (uint32_t r = t; r < nr; r += 64) x.S[r] = 0;
-  __syncthreads();
+  wave_sync();
   // classify runs; literal groups (consecutive single-value runs) get ids and sizes
   bool any = false;
   if (rle) {
@@ -681,7 +687,7 @@ __device__ static uint32_t encode_column(uint8_t kind, uint32_t n, uint8_t* out,
     }
     any = __any(any);
     if (!any) return 0;  // all-null column (wave-uniform)
-    __syncthreads();
+    wave_sync();
   }
   // record bytes -> offsets
   uint32_t total = 0;
@@ -729,7 +735,7 @@ __device__ static uint32_t encode_column(uint8_t kind, uint32_t n, uint8_t* out,
     }
   }
   (void)s_flag;
-  __syncthreads();
+  wave_sync();
   return total;
 }
 
@@ -952,7 +958,7 @@ __device__ static void wire_out(PatchOut& po, int64_t max_op, uint8_t* dst, uint
   patch_pack(po, max_op, dst, cap);
 }
 
-__global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
+__global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
                                                const am_doc_desc* __restrict__ docs, const am_known_hash* __restrict__ known,
                                                const ChunkInfo* __restrict__ info, const DocBounds* __restrict__ bounds,
                                                const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base,
@@ -1098,8 +1104,13 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
     for (uint32_t j = t; j < s.nents; j += T) gather_ent(s, j, cells);
     __syncthreads();
     if (s.status) goto done;
-    wave_excl_scan_arr(vsum, R);
-    wave_excl_scan_arr(psum, R);
+    if (kDocT == 64) {
+      wave_excl_scan_arr(vsum, R);
+      wave_excl_scan_arr(psum, R);
+    } else {
+      block_excl_scan(vsum, R, s.tmp);
+      block_excl_scan(psum, R, s.tmp);
+    }
     __syncthreads();
     for (uint32_t i = t; i < R; i += T) place_row(s, i, vsum, psum);
     // maxOp of the loaded document: the largest counter among its op ids and succs
@@ -1112,7 +1123,7 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
         const int64_t x = __shfl_xor(m, o, 64);
         m = x > m ? x : m;
       }
-      if (t == 0 && m > s.max_op) s.max_op = m;
+      if ((t & 63) == 0) atomicMax(reinterpret_cast<long long*>(&s.max_op), (long long)m);
     }
     // op columns of a future format version, carried through the merge (am_unknown.h)
     if (s.b.UC && t == 0) unk_collect(s, dd, chunks, info, wsg);
@@ -1566,8 +1577,11 @@ __global__ void __launch_bounds__(DOC_T) k_doc(const uint8_t* __restrict__ arena
         ex.V[i] = v;
       }
       __syncthreads();
-      const uint32_t len = encode_column(kEncKind[c], n, wsg + L.colbuf[c], ex, nullptr);
-      if (t == 0) s.col_len[c] = len;
+      if (t < 64) {
+        const uint32_t len = encode_column(kEncKind[c], n, wsg + L.colbuf[c], ex, nullptr);
+        if (t == 0) s.col_len[c] = len;
+      }
+      __syncthreads();
     }
     __syncthreads();
     if (s.b.UC) unk_encode(s, sr, NOUT, ex, wsg);

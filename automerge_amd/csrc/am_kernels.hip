@@ -74,24 +74,22 @@ struct DocHdr {              // decodeDocumentHeader (columnar.js:1006-1038)
 // order, i.e. ascending id order, so a second pass assigns offsets in spec order.
 // NSPEC is a compile-time constant so the slot writes are predicated register moves rather than
 // a dynamically indexed (scratch) array
-// Columns outside the spec (a future version's columns, new.js:1387-1425) are allowed among the
-// op columns (`unk` non-null): their bytes are counted in `unk_bytes` and skipped, and `pre[j]`
-// records the unknown bytes that precede spec column j in the data. Unknown ids in the pred / succ
-// groups (7, 8) would change the group structure of the known columns and stay unsupported.
+// Column table (decodeColumnInfo, columnar.js:609) -> spec slots. The data follows in table
+// order (ascending id), so each spec column's offset relative to the data start is the running
+// sum of the lengths before it (`off`, made absolute by place_cols). Columns outside the spec (a
+// future version's columns, new.js:1387-1425) are allowed among the op columns (`allow_unknown`):
+// counted in `nunk`, their bytes skipped. Unknown ids in the pred / succ groups (7, 8) would change
+// the group structure of the known columns and stay unsupported.
 template <int NSPEC>
-__device__ __forceinline__ uint32_t parse_cols(Rd& r, const uint8_t* spec, uint32_t* len, bool is_change,
-                                               uint32_t* pre = nullptr, uint32_t* nunk = nullptr, uint64_t* unk_bytes = nullptr) {
+__device__ __forceinline__ uint32_t parse_cols(Rd& r, const uint8_t* spec, uint32_t* len, uint32_t* off, bool is_change,
+                                               bool allow_unknown, uint64_t& total, uint32_t& nunk) {
   int64_t num;
   TRY(rd_u53(r, num));
   int64_t last = -1;
-  uint64_t ub = 0;
-  uint32_t nu = 0;
+  uint64_t acc = 0;
+  nunk = 0;
 #pragma unroll
-  for (int i = 0; i < NSPEC; i++) len[i] = 0;
-  if (pre) {
-#pragma unroll
-    for (int i = 0; i < NSPEC; i++) pre[i] = 0xffffffffu;
-  }
+  for (int i = 0; i < NSPEC; i++) { len[i] = 0; off[i] = 0; }
   for (int64_t i = 0; i < num; i++) {
     int64_t id, l;
     TRY(rd_u53(r, id));
@@ -104,34 +102,23 @@ __device__ __forceinline__ uint32_t parse_cols(Rd& r, const uint8_t* spec, uint3
     bool found = false;
 #pragma unroll
     for (int j = 0; j < NSPEC; j++)
-      if (spec[j] == id) { len[j] = (uint32_t)l; found = true; if (pre) pre[j] = (uint32_t)ub; }
+      if (spec[j] == id) { len[j] = (uint32_t)l; off[j] = (uint32_t)acc; found = true; }
     if (!found) {
-      if (!pre || (id >> 4) == 7 || (id >> 4) == 8 || id > 0xffff) return AM_U_UNKNOWN_COLUMN;
-      ub += (uint64_t)l;
-      nu++;
+      if (!allow_unknown || (id >> 4) == 7 || (id >> 4) == 8 || id > 0xffff) return AM_U_UNKNOWN_COLUMN;
+      nunk++;
     }
+    acc += (uint64_t)l;
   }
-  if (pre) {
-#pragma unroll
-    for (int i = 0; i < NSPEC; i++) if (pre[i] == 0xffffffffu) pre[i] = (uint32_t)ub;
-    *nunk = nu;
-    *unk_bytes = ub;
-  }
+  total = acc;
   return AM_OK;
 }
-// data of the spec columns (table order = ascending id = spec order), unknown columns interleaved
 template <int NSPEC>
-__device__ __forceinline__ uint32_t place_cols(Rd& r, uint32_t* off, const uint32_t* len, const uint32_t* pre = nullptr,
-                                               uint64_t unk_bytes = 0) {
+__device__ __forceinline__ uint32_t place_cols(Rd& r, uint32_t* off, uint64_t total) {
   const uint64_t at0 = r.off;
-  uint64_t acc = 0;
 #pragma unroll
-  for (int k = 0; k < NSPEC; k++) {
-    off[k] = (uint32_t)(at0 + acc + (pre ? pre[k] : 0u));
-    acc += len[k];
-  }
+  for (int k = 0; k < NSPEC; k++) off[k] += (uint32_t)at0;
   uint64_t at;
-  TRY(rd_raw(r, acc + unk_bytes, at));
+  TRY(rd_raw(r, total, at));
   return AM_OK;
 }
 // Visits the unknown op columns of a change or document chunk body: f(id, offset in data, length).
@@ -204,10 +191,10 @@ __device__ __forceinline__ uint32_t parse_change_hdr(const uint8_t* data, uint64
     TRY(rd_u53(r, l));
     TRY(rd_raw(r, (uint64_t)l, at));
   }
-  uint32_t pre[OC_NCOLS], nunk;
-  uint64_t ub;
-  TRY(parse_cols<OC_NCOLS>(r, kChangeColIds, h.col_len, true, pre, &nunk, &ub));
-  TRY(place_cols<OC_NCOLS>(r, h.col_off, h.col_len, pre, ub));
+  uint64_t total;
+  uint32_t nunk;
+  TRY(parse_cols<OC_NCOLS>(r, kChangeColIds, h.col_len, h.col_off, true, true, total, nunk));
+  TRY(place_cols<OC_NCOLS>(r, h.col_off, total));
   h.nunk = nunk;
   h.has_extra = r.off < r.n;
   h.extra_off = (uint32_t)r.off;
@@ -232,12 +219,12 @@ __device__ __forceinline__ uint32_t parse_doc_hdr(const uint8_t* data, uint64_t 
   h.nheads = (uint32_t)v;
   TRY(rd_raw(r, (uint64_t)v * 32, at));
   h.heads_off = (uint32_t)at;
-  uint32_t pre[OC_NCOLS], nunk;
-  uint64_t ub;
-  TRY(parse_cols<DC_NCOLS>(r, kDocChgColIds, h.ccol_len, false));
-  TRY(parse_cols<OC_NCOLS>(r, kDocOpColIds, h.ocol_len, false, pre, &nunk, &ub));
-  TRY(place_cols<DC_NCOLS>(r, h.ccol_off, h.ccol_len));
-  TRY(place_cols<OC_NCOLS>(r, h.ocol_off, h.ocol_len, pre, ub));
+  uint64_t ctot, otot;
+  uint32_t cunk, nunk;
+  TRY(parse_cols<DC_NCOLS>(r, kDocChgColIds, h.ccol_len, h.ccol_off, false, false, ctot, cunk));
+  TRY(parse_cols<OC_NCOLS>(r, kDocOpColIds, h.ocol_len, h.ocol_off, false, true, otot, nunk));
+  TRY(place_cols<DC_NCOLS>(r, h.ccol_off, ctot));
+  TRY(place_cols<OC_NCOLS>(r, h.ocol_off, otot));
   h.nunk = nunk;
   h.has_hidx = r.off < r.n;
   h.hidx_off = (uint32_t)r.off;
@@ -251,8 +238,8 @@ __device__ __forceinline__ uint32_t parse_doc_hdr(const uint8_t* data, uint64_t 
 
 // unknown op columns: count and a bound on their values (every column holds a value per row, or,
 // in an unknown column group, one per entry of that group: at most the sum of its cardinalities)
-__device__ static uint32_t unknown_bound(const uint8_t* data, uint64_t n, bool is_doc, uint32_t nunk, uint32_t nrows,
-                                         ChunkInfo& ci) {
+// (noinline, results by value: the caller's ChunkInfo stays in registers -- no scratch)
+__device__ __noinline__ static uint64_t unknown_bound(const uint8_t* data, uint64_t n, bool is_doc, uint32_t nunk, uint32_t nrows) {
   uint64_t cards = 0;
   uint32_t st = AM_OK;
   uint32_t e = visit_unknown_cols(data, n, is_doc, [&](uint32_t id, uint64_t off, uint32_t l) {
@@ -261,13 +248,11 @@ __device__ static uint32_t unknown_bound(const uint8_t* data, uint64_t n, bool i
     st = rle_count_sum_i(data + off, l, false, cnt, sum, 0);
     cards += sum;
   });
-  if (e) return e;
-  if (st) return st;
+  if (e) return (uint64_t)e << 32;
+  if (st) return (uint64_t)st << 32;
   const uint64_t b = (uint64_t)(nunk + 1) * ((uint64_t)nrows + cards) + 2ull * nrows;
-  if (b > 0x3fffffffull) return AM_U_CAPACITY;
-  ci.nunk = nunk;
-  ci.unkvals = (uint32_t)b;
-  return AM_OK;
+  if (b > 0x3fffffffull) return (uint64_t)AM_U_CAPACITY << 32;
+  return b;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -282,7 +267,7 @@ __device__ __forceinline__ void chunk_body(const uint8_t* p, const am_chunk_desc
 #pragma unroll
   for (int k = 0; k < 8; k++) hw[k] = 0;
   ci.status = AM_OK; ci.type = 0xff; ci.data_off = 0; ci.data_len = 0; ci.nops = 0; ci.nents = 0; ci.nchg = 0;
-  ci.ndeps = 0; ci.nactors = 0; ci.strbytes = 0; ci.nheads = 0; ci.arg0 = 0; ci.nunk = 0; ci.unkvals = 0;
+  ci.ndeps = 0; ci.nactors = 0; ci.strbytes = 0; ci.nheads = 0; ci.arg0 = 0; ci.nunk = 0;
   uint32_t st = AM_OK;
   do {
     // decodeContainerHeader (columnar.js:688)
@@ -333,7 +318,7 @@ __device__ __forceinline__ void chunk_body(const uint8_t* p, const am_chunk_desc
       uint64_t scnt, ssum;
       if ((st = rle_count_sum_i(data + hh.col_off[OC_KEY_STR], hh.col_len[OC_KEY_STR], true, scnt, ssum, 0))) break;
       ci.strbytes = (uint32_t)ssum + hh.msg_len;
-      if (hh.nunk && (st = unknown_bound(data, len, false, hh.nunk, ci.nops, ci))) break;
+      ci.nunk = hh.nunk;  // their value bound: k_bounds (unknown_bound)
     } else if (ci.type == 0) {
       if (r.off != cd.len) { st = AM_E_DOC_TRAILING; break; }
       DocHdr dh;
@@ -365,7 +350,7 @@ __device__ __forceinline__ void chunk_body(const uint8_t* p, const am_chunk_desc
       if ((st = rle_count_sum_i(data + dh.ocol_off[OC_KEY_STR], dh.ocol_len[OC_KEY_STR], true, cnt, s1, 0))) break;
       if ((st = rle_count_sum_i(data + dh.ccol_off[DC_MESSAGE], dh.ccol_len[DC_MESSAGE], true, cnt, s2, 0))) break;
       ci.strbytes = (uint32_t)(s1 + s2);
-      if (dh.nunk && (st = unknown_bound(data, len, true, dh.nunk, ci.nops, ci))) break;
+      ci.nunk = dh.nunk;
     } else {
       st = AM_E_CHUNK_TYPE;
       ci.arg0 = ci.type;
@@ -415,7 +400,7 @@ __global__ void __launch_bounds__(256) k_chunks(const uint8_t* __restrict__ aren
 // ------------------------------------------------------------------------------------------
 // k_bounds: one thread per document -> workspace bounds
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_bounds(const am_doc_desc* __restrict__ docs, uint32_t ndocs,
+__global__ void __launch_bounds__(256) k_bounds(const uint8_t* __restrict__ arena, const am_doc_desc* __restrict__ docs, uint32_t ndocs,
                                                 const am_chunk_desc* __restrict__ chunks, const ChunkInfo* __restrict__ info,
                                                 DocBounds* __restrict__ bounds, uint64_t* __restrict__ ws_bytes) {
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
@@ -428,7 +413,12 @@ __global__ void __launch_bounds__(256) k_bounds(const am_doc_desc* __restrict__ 
     const ChunkInfo& ci = info[dd.base_chunk];
     R += ci.nops; E += ci.nents; C += ci.nchg; D += ci.ndeps; A += ci.nactors; H += ci.nheads;
     S += ci.strbytes; B += chunks[dd.base_chunk].len;
-    UC += ci.nunk; UV += ci.unkvals;
+    if (ci.nunk && !ci.status) {
+      const uint64_t ub = unknown_bound(arena + chunks[dd.base_chunk].off + ci.data_off, ci.data_len, true, ci.nunk, ci.nops);
+      UC += ci.nunk;
+      // a malformed unknown column: a row-sized bound, k_doc's decode reports the error itself
+      UV += (ub >> 32) ? (uint64_t)(ci.nunk + 3) * ci.nops : (uint32_t)ub;
+    }
     lo = chunks[dd.base_chunk].off;
     hi = lo + chunks[dd.base_chunk].len;
   }
@@ -437,7 +427,11 @@ __global__ void __launch_bounds__(256) k_bounds(const am_doc_desc* __restrict__ 
     const am_chunk_desc cd = chunks[dd.chg_begin + k];
     R += ci.nops; E += ci.nents; C += 1; D += ci.ndeps; A += 1; H += 1; S += ci.strbytes;
     B += cd.len;
-    UC += ci.nunk; UV += ci.unkvals;
+    if (ci.nunk && !ci.status) {
+      const uint64_t ub = unknown_bound(arena + cd.off + ci.data_off, ci.data_len, false, ci.nunk, ci.nops);
+      UC += ci.nunk;
+      UV += (ub >> 32) ? (uint64_t)(ci.nunk + 3) * ci.nops : (uint32_t)ub;
+    }
     AM += ci.nactors;
     ND += ci.ndeps;
     if (cd.off < lo) lo = cd.off;
@@ -509,6 +503,7 @@ __global__ void __launch_bounds__(SCAN_T) k_scan_add(uint64_t* __restrict__ out,
 // k_doc: one workgroup (one wave) per document
 // ------------------------------------------------------------------------------------------
 #define DOC_T 64
+#define DOC_T_GLB 256  // global-mode k_doc workgroup (4 waves per document)
 
 struct IdKey { int64_t ctr; int32_t actor; int32_t row; };
 struct ElemKey { int64_t obj_ctr; int64_t id_ctr; int32_t obj_rank; int32_t parent; int32_t id_rank; int32_t row; };
@@ -557,7 +552,7 @@ struct DocShared {
   uint32_t col_len[OC_NCOLS + DC_NCOLS];
   uint32_t col_pos[OC_NCOLS + DC_NCOLS];
   uint64_t out_len;
-  uint32_t tmp[DOC_T + 1];
+  uint32_t tmp[DOC_T_GLB + 1];
   uint64_t ph_last;
   uint32_t xs_used;                       // bytes of replaced strings after the staged input (b.U)
   uint32_t nunk_inst, nunk_ids;           // unknown op columns: instances, distinct output columns
@@ -595,13 +590,27 @@ __host__ __device__ inline bool doc_scattered(const DocBounds& b) { return b.spa
 
 extern __shared__ __attribute__((aligned(16))) uint8_t am_lds[];
 
+#define K_DOC_WAVES_ATTR
 namespace lds_mode {
 constexpr bool kHotLds = true;
+constexpr uint32_t kDocT = DOC_T;  // one wave: the hot set is this document's LDS slice
 #include "am_doc_impl.h"
 }  // namespace lds_mode
+#undef K_DOC_WAVES_ATTR
+#ifndef AM_GLB_WAVES
+#define AM_GLB_WAVES 4
+#endif
 namespace glb_mode {
 constexpr bool kHotLds = false;
+// four waves: large documents' sorts, scans and list ranking are latency-bound chains over global
+// arrays; more lanes in flight per document (and more waves per SIMD) hide that latency
+constexpr uint32_t kDocT = DOC_T_GLB;
+#undef K_DOC_WAVES_ATTR
+// four waves per SIMD (<= 128 VGPRs, the rest spills): four documents share a CU; measured on C3
+// (1000 x 100k-op texts): 1 wave 1076 ms, 4 waves at 2 per SIMD 931 ms, at 4 per SIMD 783 ms
+#define K_DOC_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(AM_GLB_WAVES, 8)))
 #include "am_doc_impl.h"
+#undef K_DOC_WAVES_ATTR
 }  // namespace glb_mode
 #include "am_doc_fast.h"
 
@@ -687,7 +696,7 @@ void am_launch_chunks(const BatchDev& b, hipStream_t s) {
 void am_launch_bounds(const BatchDev& b, hipStream_t s) {
   if (!b.ndocs) return;
   (void)hipMemsetAsync(b.max_hot, 0, 2 * sizeof(uint64_t), s);
-  hipLaunchKernelGGL(k_bounds, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, b.docs, b.ndocs, b.chunks, b.info, b.bounds,
+  hipLaunchKernelGGL(k_bounds, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, b.arena, b.docs, b.ndocs, b.chunks, b.info, b.bounds,
                      b.ws_bytes);
   hipLaunchKernelGGL(k_max_hot, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, b.bounds, b.docs, b.ndocs, b.max_hot);
   uint32_t nblk = (b.ndocs + SCAN_T - 1) / SCAN_T;
@@ -713,7 +722,7 @@ void am_launch_doc(const BatchDev& b, hipStream_t s) {
     hipLaunchKernelGGL(lds_mode::k_doc, dim3(b.ndocs), dim3(DOC_T), b.lds_bytes, s, b.arena, b.chunks, b.docs, b.known,
                        b.info, b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd);
     if (b.max_hot_host > b.lds_bytes)
-      hipLaunchKernelGGL(glb_mode::k_doc, dim3(b.ndocs), dim3(DOC_T), 0, s, b.arena, b.chunks, b.docs, b.known, b.info,
+      hipLaunchKernelGGL(glb_mode::k_doc, dim3(b.ndocs), dim3(DOC_T_GLB), 0, s, b.arena, b.chunks, b.docs, b.known, b.info,
                          b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd);
   }
 }

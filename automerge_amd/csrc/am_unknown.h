@@ -164,7 +164,7 @@ __device__ static void unk_encode(DocShared& s, const SortRec* sr, uint32_t NOUT
     const bool member = unk_member_type(id, cu >= 0);
     uint32_t n = NOUT;
     if (member) {
-      for (uint32_t k = t; k < NOUT; k += 64) {
+      for (uint32_t k = t; k < NOUT; k += blockDim.x) {
         const int32_t row = sr[k].row;
         const uint32_t src = src_of(s, (uint32_t)row, false);
         const int32_t ci = map[src * nu + cu];
@@ -176,11 +176,11 @@ __device__ static void unk_encode(DocShared& s, const SortRec* sr, uint32_t NOUT
         rowoff[k] = (uint32_t)c;
       }
       __syncthreads();
-      n = wave_excl_scan_arr(rowoff, NOUT);
+      n = block_excl_scan(rowoff, NOUT, s.tmp);
       __syncthreads();
     }
     if (n > L.enc_n) { if (t == 0) set_err(s, AM_U_CAPACITY); return; }
-    for (uint32_t k = t; k < NOUT; k += 64) {
+    for (uint32_t k = t; k < NOUT; k += blockDim.x) {
       const int32_t row = sr[k].row;
       const uint32_t src = src_of(s, (uint32_t)row, false);
       const SrcInfo si = src_info(s, src);
@@ -198,9 +198,11 @@ __device__ static void unk_encode(DocShared& s, const SortRec* sr, uint32_t NOUT
     }
     __syncthreads();
     const uint8_t kind = type == 3 ? EK_D : type == 4 ? EK_B : type == 5 ? EK_S : type == 7 ? EK_W : EK_U;
-    const uint32_t len = encode_column(kind, n, out + pos, ex, nullptr);
-    if (t == 0) { ids[nu + u] = (uint32_t)pos; ids[2 * nu + u] = len; }
-    pos += len;
+    if (t < 64) {
+      const uint32_t len = encode_column(kind, n, out + pos, ex, nullptr);
+      if (t == 0) { ids[nu + u] = (uint32_t)pos; ids[2 * nu + u] = len; }
+    }
     __syncthreads();
+    pos += ids[2 * nu + u];
   }
 }
