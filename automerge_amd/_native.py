@@ -56,7 +56,7 @@ class Span(C.Structure):
 
 
 class Error(C.Structure):
-    _fields_ = [("code", C.c_uint32), ("is_type_error", C.c_int32), ("message", C.c_char * 480)]
+    _fields_ = [("code", C.c_uint32), ("is_type_error", C.c_int32), ("message", C.c_char * 8184)]
 
 
 P = C.c_void_p
@@ -72,8 +72,9 @@ _sigs = {
     "am_batch_results": (C.c_int, [P, P]),
     "am_batch_chunk_results": (C.c_int, [P, P, P, P]),
     "am_batch_doc_output": (C.c_int, [P, C.c_uint32, P, C.c_uint64, C.POINTER(C.c_uint64)]),
-    "am_document_changes": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.POINTER(C.c_uint64)),
+    "am_document_changes": (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.POINTER(C.c_uint64)),
                                       C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
+    "am_document_changes_batch": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t, P]),
     "am_doc_compute_hash_graph": (C.c_int, [P, C.POINTER(Error)]),
     "am_inflate_raw": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t), C.c_size_t, C.POINTER(u8p),
                                  C.POINTER(C.c_size_t), P, C.POINTER(Error)]),
@@ -166,9 +167,13 @@ class AutomergeError(Exception):
         return self.code >= 100
 
 
-def raise_for(err):
+def error_for(err):
     msg = err.message.decode("utf-8", "replace")
-    raise AutomergeError(msg, err.code, "TypeError" if err.is_type_error else "RangeError")
+    return AutomergeError(msg, err.code, "TypeError" if err.is_type_error else "RangeError")
+
+
+def raise_for(err):
+    raise error_for(err)
 
 
 _engines = {}
@@ -243,21 +248,43 @@ def inflate_raw(buffers, device=0):
     return res
 
 
-def document_changes(doc):
-    """decodeChanges([doc]) re-encoded (computeHashGraph, new.js:1879-1904): [(change bytes, hash hex)]
-    of a saved document in its change order (am_document_changes, host stage)."""
-    out, hs = u8p(), u8p()
-    offs = C.POINTER(C.c_uint64)()
-    n = C.c_size_t()
-    err = Error()
-    if lib.am_document_changes(bytes(doc), len(doc), C.byref(out), C.byref(offs), C.byref(hs), C.byref(n),
-                               C.byref(err)):
-        raise_for(err)
+class History(C.Structure):
+    """am_history (include/automerge_amd.h): one document's reconstructed changes or its error."""
+    _fields_ = [("changes", u8p), ("offs", C.POINTER(C.c_uint64)), ("hashes32", u8p), ("nchanges", C.c_size_t),
+                ("err", Error)]
+
+
+def document_changes_batch(docs, device=0):
+    """decodeChanges([doc]) re-encoded (computeHashGraph, new.js:1879-1904) for many saved documents
+    in one GPU batch (k_history): per document [(change bytes, hash hex)], or the AutomergeError it
+    raises."""
+    n = len(docs)
+    if n == 0:
+        return []
+    arr = (C.c_char_p * n)(*[bytes(d) for d in docs])
+    lens = (C.c_size_t * n)(*[len(d) for d in docs])
+    hs = (History * n)()
+    lib.am_document_changes_batch(engine(device), arr, lens, n, hs)
     res = []
-    for i in range(n.value):
-        a, b = offs[i], offs[i + 1]
-        res.append((C.string_at(C.addressof(out.contents) + a, b - a) if b > a else b"",
-                    C.string_at(C.addressof(hs.contents) + 32 * i, 32).hex()))
-    for p in (out, offs, hs):
-        lib.am_free(p)
+    for h in hs:
+        if h.err.code:
+            res.append(error_for(h.err))
+            continue
+        out = []
+        for i in range(h.nchanges):
+            a, b = h.offs[i], h.offs[i + 1]
+            out.append((C.string_at(C.addressof(h.changes.contents) + a, b - a) if b > a else b"",
+                        C.string_at(C.addressof(h.hashes32.contents) + 32 * i, 32).hex()))
+        res.append(out)
+        for p in (h.changes, h.offs, h.hashes32):
+            lib.am_free(p)
     return res
+
+
+def document_changes(doc, device=0):
+    """decodeChanges([doc]) re-encoded (computeHashGraph, new.js:1879-1904): [(change bytes, hash hex)]
+    of a saved document in its change order (am_document_changes_batch with one document)."""
+    r = document_changes_batch([doc], device)[0]
+    if isinstance(r, Exception):
+        raise r
+    return r

@@ -1226,6 +1226,14 @@ bool stage_doc(am_engine* e, const std::vector<uint8_t>& in, std::vector<uint8_t
 
 }  // namespace
 
+bool am_stage_doc_chunk(am_engine* e, const std::vector<uint8_t>& in, std::vector<uint8_t>& out, bool& verified, am_error* err) {
+  Err er;
+  if (stage_doc(e, in, out, verified, er)) return true;
+  to_c(er, err);
+  return false;
+}
+std::string am_message_for(uint32_t code, int64_t a0, int64_t a1, const std::string& actor) { return message_for(code, a0, a1, actor); }
+
 extern "C" am_doc* am_doc_init(am_engine* eng) {
   am_doc* d = new am_doc();
   d->eng = eng;
@@ -1475,14 +1483,14 @@ extern "C" size_t am_doc_get_heads(const am_doc* d, uint8_t* out32, size_t cap) 
 extern "C" size_t am_doc_pending(const am_doc* d) { return d->queue.size(); }
 extern "C" int64_t am_doc_max_op(const am_doc* d) { return d->max_op; }
 extern "C" size_t am_doc_num_changes(const am_doc* d) { return d->nchanges; }
-// computeHashGraph (new.js:1879-1904): the history decoded from save() (am_history.cpp)
+// computeHashGraph (new.js:1879-1904): the history decoded from the document (k_history, am_hist.hip)
 extern "C" int am_doc_compute_hash_graph(am_doc* d, am_error* err) {
   if (err) err->code = 0;
   if (d->have_hash_graph) return 0;
   uint8_t *out = nullptr, *hs = nullptr;
   uint64_t* offs = nullptr;
   size_t n = 0;
-  if (am_document_changes(d->state.data(), d->state.size(), &out, &offs, &hs, &n, err)) return 1;
+  if (am_document_changes(d->eng, d->state.data(), d->state.size(), &out, &offs, &hs, &n, err)) return 1;
   d->changes.clear();
   d->hashes.clear();
   d->graph.clear();

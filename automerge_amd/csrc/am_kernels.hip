@@ -613,6 +613,7 @@ constexpr uint32_t kDocT = DOC_T_GLB;
 #undef K_DOC_WAVES_ATTR
 }  // namespace glb_mode
 #include "am_doc_fast.h"
+#include "am_hist_dev.h"
 
 // ------------------------------------------------------------------------------------------
 // k_compact: workgroup per document copies its merged chunk into the dense output arena
@@ -692,6 +693,11 @@ __global__ void __launch_bounds__(256) k_max_hot(const DocBounds* __restrict__ b
 void am_launch_chunks(const BatchDev& b, hipStream_t s) {
   if (!b.nchunks) return;
   hipLaunchKernelGGL(k_chunks, dim3((b.nchunks + 255) / 256), dim3(256), 0, s, b.arena, b.chunks, b.nchunks, b.info, b.hdr);
+}
+void am_launch_history(const uint8_t* arena, const am_chunk_desc* chunks, const ChunkInfo* info, const HistDesc* hd, uint32_t ndocs,
+                       uint8_t* ws, uint8_t* out, HistResult* res, HistChange* chg_out, hipStream_t s) {
+  if (!ndocs) return;
+  hipLaunchKernelGGL(k_history, dim3(ndocs), dim3(64), 0, s, arena, chunks, info, hd, ndocs, ws, out, res, chg_out);
 }
 void am_launch_bounds(const BatchDev& b, hipStream_t s) {
   if (!b.ndocs) return;

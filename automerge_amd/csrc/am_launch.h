@@ -4,6 +4,10 @@
 
 #include "am_common.h"
 #include "am_layout.h"
+#include "am_hist.h"
+
+#include <string>
+#include <vector>
 
 struct BatchDev {
   const uint8_t* arena;
@@ -66,3 +70,11 @@ void am_launch_bloom_probe(const uint8_t* d_filters, const uint64_t* d_foff, uin
 void am_launch_sync_select(uint32_t npairs, const uint64_t* d_coff, const uint8_t* d_hashes, const uint64_t* d_doff,
                            const int32_t* d_didx, const uint64_t* d_pfoff, const uint8_t* d_filters, const uint64_t* d_foff,
                            uint8_t* d_send, uint8_t* d_status, hipStream_t s);
+
+// k_history (am_hist_dev.h): one workgroup per document of the change history
+void am_launch_history(const uint8_t* arena, const am_chunk_desc* chunks, const ChunkInfo* info, const HistDesc* hd, uint32_t ndocs,
+                       uint8_t* ws, uint8_t* out, HistResult* res, HistChange* chg_out, hipStream_t s);
+// host stages of am_capi.hip shared with am_hist.hip: Backend.load's staging of a document chunk
+// (DEFLATEd columns inflated, checksum verified), the reference error text of an AM_* code
+bool am_stage_doc_chunk(am_engine* e, const std::vector<uint8_t>& in, std::vector<uint8_t>& out, bool& verified, am_error* err);
+std::string am_message_for(uint32_t code, int64_t a0, int64_t a1, const std::string& actor);

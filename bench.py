@@ -53,6 +53,28 @@ def cpu_baseline(arena, chunks, docs, seconds=12.0, ops_per_doc=60, name="C4"):
             "sample": "%d %s documents (load + applyChanges + save) by oracle/liboracle.so, 1 thread, %.1f s" % (n, name, dt)}
 
 
+def kernel_source_digest():
+    """Digest of the engine's kernel sources: profiles/traffic_k_doc.json (the PMC FETCH_SIZE /
+    WRITE_SIZE passes, tools/gpu_traffic.sh + tools/traffic.py) is reported only for the sources it
+    was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    src = os.path.join(ROOT, "automerge_amd", "csrc")
+    for name in sorted(os.listdir(src)):
+        if name.endswith((".h", ".hip")):
+            with open(os.path.join(src, name), "rb") as f:
+                h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
+def measured_traffic():
+    try:
+        rec = json.load(open(os.path.join(ROOT, "profiles", "traffic_k_doc.json")))
+    except (OSError, ValueError):
+        return None
+    return rec if rec.get("src_digest") == kernel_source_digest() else None
+
+
 def cpu_reference():
     """The reference JS backend under Node (measured in the build container by
     tools/cpu_reference.js, which cannot run on the GPU box): per core and on all cores."""
@@ -273,6 +295,11 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
     value = tot[1] / (elapsed / args.steps)
     achieved = alg_launch / (t_doc * 1e-3) / 1e9 if t_doc else None
+    tr = measured_traffic() if args.mode == "pipe" and args.workload == "c4" and not args.no_patch else None
+    if tr is not None and t_doc:
+        # decode GB/s: HBM bytes the document kernel fetches per launch / its time
+        extra["decode_GBps"] = 2 * tr["fetch_size_kib"] * 1024 / (t_doc * 1e-3) / 1e9
+        extra["decode_frac_of_hbm_peak"] = extra["decode_GBps"] / HBM_PEAK_GBPS
     cpu = None if args.no_cpu_baseline else cpu_baseline(arena, chunks, docs, ops_per_doc=per_doc, name=args.workload.upper())
     wl = {"c4": "C4 1M-document job: load base doc + applyChanges of 12 concurrent changes (4 actors x 3), 60 ops/doc",
           "c2": "C2: applyChanges of 3 changes (10 map/counter/string sets + 2 concurrent inc/overwrite), 14 ops/doc"}
@@ -290,7 +317,7 @@ def main():
                    "parallelism": "doc-sharded dp%d" % world},
         "roofline": {"kernel": "k_doc_fast (+ k_doc for the rest)", "bound": "hbm", "achieved": achieved,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS if achieved else None,
-                     "traffic": None, "alg_bytes_per_launch": alg_launch, "avg_ms": t_doc,
+                     "traffic": tr["traffic_bytes"] if tr else None, "alg_bytes_per_launch": alg_launch, "avg_ms": t_doc,
                      "limiter": "VALU issue of the one-wave-per-document merge (DESIGN.md 4); not HBM"},
         "errors": tot[2], "verified_docs": checked, "input_bytes_rank0": in_b, "output_bytes_rank0": out_bytes,
         "patch_bytes_rank0": patch_bytes, "workspace_bytes_per_batch": workspace, "gen_s": t_gen,

@@ -128,7 +128,7 @@ enum am_change_state { CHG_UNSEEN = -4, CHG_DUP = -3, CHG_QUEUED = -2, CHG_ERROR
 typedef struct am_error {
   uint32_t code;          /* AM_* status; 0 = ok */
   int32_t is_type_error;  /* the reference throws TypeError (else RangeError/Error) */
-  char message[480];      /* the reference's message text */
+  char message[8184];     /* the reference's message text (heads lists of a history error run long) */
 } am_error;
 
 typedef struct am_engine am_engine;
@@ -163,10 +163,23 @@ int am_batch_doc_output(am_batch *b, uint32_t doc, uint8_t *dst, uint64_t cap, u
  * two inflate passes (ms, HIP events). */
 int am_batch_inflate_info(am_batch *b, uint64_t *nchunks, uint64_t *arena_bytes, float *ms);
 /* computeHashGraph (new.js:1879-1904) / decodeDocument (columnar.js:1040-1046, groupChangeOps :876-943,
- * decodeDocumentChanges :945-981): the change history of a document chunk, every change re-encoded
- * by encodeChange (deflated when >= 256 B) in the document's change order. *out = the changes back
- * to back, (*offs)[0..n] their offsets, *hashes32 their hashes (all malloc'd, am_free). Host stage. */
-int am_document_changes(const uint8_t *doc, size_t len, uint8_t **out, uint64_t **offs, uint8_t **hashes32,
+ * decodeDocumentChanges :945-981) of n documents in one GPU batch (k_history, one workgroup per
+ * document): the change history of each document chunk, every change re-encoded by encodeChange
+ * (deflated when >= 256 B) in the document's change order. Per document: changes = the change
+ * chunks back to back, offs[0..nchanges] their offsets, hashes32 their hashes (malloc'd, am_free),
+ * or err.code != 0 with the reference's RangeError text (AM_E_HISTORY) or the codec error.
+ * Returns nonzero when any document failed. */
+typedef struct am_history {
+  uint8_t *changes;
+  uint64_t *offs;
+  uint8_t *hashes32;
+  size_t nchanges;
+  am_error err;
+} am_history;
+int am_document_changes_batch(am_engine *eng, const uint8_t *const *docs, const size_t *lens, size_t n, am_history *out);
+/* One document through am_document_changes_batch: *out = the changes back to back, (*offs)[0..n]
+ * their offsets, *hashes32 their hashes (all malloc'd, am_free). */
+int am_document_changes(am_engine *eng, const uint8_t *doc, size_t len, uint8_t **out, uint64_t **offs, uint8_t **hashes32,
                         size_t *nchanges, am_error *err);
 /* Backend state of a loaded document: fills in its hash graph (new.js:1879-1904) so that
  * getAllChanges / getChanges / getChangeByHash see the whole history; no-op when it is known. */

@@ -1,9 +1,13 @@
-"""Change history of a saved document (computeHashGraph new.js:1879-1904 =
-decodeDocument + groupChangeOps + decodeDocumentChanges + encodeChange, columnar.js:876-981, 710):
-am_document_changes against Backend.getAllChanges(Backend.load(saved)) as the reference returns it
-for every saved document of the golden scenarios and for text histories with deflated columns and
-deflated changes (tests/golden/history.json, tests/golden/gen/make_history.js). Host stage: runs
-without a GPU."""
+"""Change history of saved documents (computeHashGraph new.js:1879-1904 =
+decodeDocument + groupChangeOps + decodeDocumentChanges + encodeChange, columnar.js:876-981, 710),
+batched on the GPU (k_history, am_document_changes_batch):
+- against Backend.getAllChanges(Backend.load(saved)) as the reference returns it for every saved
+  document of the golden scenarios and for text histories with deflated columns and deflated
+  changes (tests/golden/history.json, tests/golden/gen/make_history.js);
+- against concurrent multi-actor histories and the RangeErrors of groupChangeOps /
+  decodeDocumentChanges on mutated documents (tests/golden/history_cases.json,
+  tests/golden/gen/make_history_cases.js: decodeChanges + encodeChange run straight on the bytes,
+  and getAllChanges after load where load accepts them)."""
 import json
 import os
 
@@ -12,25 +16,96 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+def _load(name):
+    return json.load(open(os.path.join(HERE, "golden", name)))
+
+
+def test_history_fixtures_shape():
+    """The fixtures hold what the GPU tests below rely on: enough documents and changes, valid
+    concurrent histories, and every history RangeError kind of columnar.js:876-981."""
+    cases = _load("history.json")
+    assert len(cases) > 300 and sum(len(c["changes"]) for c in cases) > 3000
+    hc = _load("history_cases.json")
+    for c in hc:
+        assert (c["direct"] is None) != (c["direct_error"] is None), c["name"]
+    errs = " | ".join(c["direct_error"] for c in hc if c["direct_error"])
+    for kind in ("Expected seq = ", "maxOp must increase", "outside of allowed range", "No hash for index",
+                 "Mismatched heads hashes", "Bad datatype for extra bytes", "document should not contain del"):
+        assert kind in errs, kind
+    assert sum(1 for c in hc if c["direct"] and c["name"].startswith("concurrent")) >= 7
+
+
+@pytest.mark.gpu
 def test_document_changes_match_reference():
+    """All 359 documents in ONE batch (one workgroup per document)."""
     from automerge_amd import _native as N
-    cases = json.load(open(os.path.join(HERE, "golden", "history.json")))
-    assert len(cases) > 300
+    cases = _load("history.json")
+    got = N.document_changes_batch([bytes.fromhex(c["doc"]) for c in cases])
     nchg = 0
-    for i, c in enumerate(cases):
-        got = N.document_changes(bytes.fromhex(c["doc"]))
-        assert [b.hex() for b, _ in got] == c["changes"], i
-        nchg += len(got)
+    for i, (c, g) in enumerate(zip(cases, got)):
+        assert not isinstance(g, Exception), (i, g)
+        assert [b.hex() for b, _ in g] == c["changes"], i
+        nchg += len(g)
     assert nchg > 3000
 
 
+@pytest.mark.gpu
 def test_document_changes_hashes_are_change_hashes():
     import oracle_ffi as O
     from automerge_amd import _native as N
-    cases = json.load(open(os.path.join(HERE, "golden", "history.json")))
+    cases = _load("history.json")
     for c in cases[::25]:
         for b, h in N.document_changes(bytes.fromhex(c["doc"])):
             assert O.change_meta(b)["hash"] == h
+
+
+@pytest.mark.gpu
+def test_document_changes_cases():
+    """Concurrent histories (parallel branches hash in the same round) and every RangeError of the
+    history decode, batched; each document's result matches decodeChanges + encodeChange."""
+    from automerge_amd import _native as N
+    hc = _load("history_cases.json")
+    got = N.document_changes_batch([bytes.fromhex(c["doc"]) for c in hc])
+    for c, g in zip(hc, got):
+        if c["direct_error"] is not None:
+            assert isinstance(g, Exception), c["name"]
+            assert str(g) == c["direct_error"], c["name"]
+            assert g.kind == "RangeError", c["name"]
+        else:
+            assert not isinstance(g, Exception), (c["name"], g)
+            assert [b.hex() for b, _ in g] == c["direct"], c["name"]
+
+
+@pytest.mark.gpu
+def test_document_changes_singly_equals_batched():
+    """A document's history does not depend on the batch it runs in."""
+    from automerge_amd import _native as N
+    hc = _load("history_cases.json")
+    docs = [bytes.fromhex(c["doc"]) for c in hc[:12]]
+    batched = N.document_changes_batch(docs)
+    for d, b in zip(docs, batched):
+        s = N.document_changes_batch([d])[0]
+        assert type(s) is type(b)
+        if not isinstance(s, Exception):
+            assert s == b
+
+
+@pytest.mark.gpu
+def test_get_all_changes_after_load_cases():
+    """Backend.load + getAllChanges through the drop-in mirror where the reference's load accepts the
+    document: the changes, or the RangeError getAllChanges throws."""
+    from automerge_amd import backend as B
+    from automerge_amd._native import AutomergeError
+    for c in _load("history_cases.json"):
+        if c["load_error"] is not None:
+            continue
+        st = B.load(bytes.fromhex(c["doc"]))
+        if c["error"] is not None:
+            with pytest.raises(AutomergeError) as ei:
+                B.getAllChanges(st)
+            assert str(ei.value) == c["error"], c["name"]
+        else:
+            assert [b.hex() for b in B.getAllChanges(st)] == c["changes"], c["name"]
 
 
 @pytest.mark.gpu

@@ -21,12 +21,20 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 STAGE = ("k_doc_fast", "lds_mode::k_doc", "glb_mode::k_doc")
 
 
+def kernel_key(name):
+    """'void k_doc_fast<true>(...)' -> 'k_doc_fast'; 'lds_mode::k_doc(...)' -> 'lds_mode::k_doc'."""
+    name = name.split("(")[0]
+    if name.startswith("void "):
+        name = name[5:]
+    return name.split("<")[0]
+
+
 def per_launch(root, counter):
     vals = defaultdict(list)
     for f in glob.glob(os.path.join(root, counter, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == counter:
-                vals[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+                vals[kernel_key(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
