@@ -5,6 +5,7 @@ an engine raises if no HIP device is visible.
 """
 import ctypes as C
 import os
+import time
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AM_LIB_PATH") or os.path.join(_HERE, "libautomerge_amd.so")
@@ -254,7 +255,7 @@ class History(C.Structure):
                 ("err", Error)]
 
 
-def document_changes_batch(docs, device=0):
+def document_changes_batch(docs, device=0, stats=None):
     """decodeChanges([doc]) re-encoded (computeHashGraph, new.js:1879-1904) for many saved documents
     in one GPU batch (k_history): per document [(change bytes, hash hex)], or the AutomergeError it
     raises."""
@@ -264,7 +265,11 @@ def document_changes_batch(docs, device=0):
     arr = (C.c_char_p * n)(*[bytes(d) for d in docs])
     lens = (C.c_size_t * n)(*[len(d) for d in docs])
     hs = (History * n)()
-    lib.am_document_changes_batch(engine(device), arr, lens, n, hs)
+    eng = engine(device)
+    t0 = time.perf_counter()
+    lib.am_document_changes_batch(eng, arr, lens, n, hs)
+    if stats is not None:
+        stats["c_seconds"] = time.perf_counter() - t0
     res = []
     for h in hs:
         if h.err.code:

@@ -276,6 +276,7 @@ struct am_engine {
   hipStream_t stream = nullptr;
   hipEvent_t ev[5] = {};
   am_batch* scratch = nullptr;  // batch reused by the per-document API
+  void* hist = nullptr;         // device buffers of the history batches (am_hist.hip)
 };
 
 struct am_batch {
@@ -321,6 +322,7 @@ extern "C" const char* am_version(void) { return "automerge_amd 0.1 (gfx950)"; }
 // accessors for the other translation units (am_launch.h)
 hipStream_t am_engine_stream(am_engine* e) { return e->stream; }
 int am_engine_device(am_engine* e) { return e->device; }
+void*& am_engine_hist(am_engine* e) { return e->hist; }
 
 extern "C" am_engine* am_engine_create(int device, am_error* err) {
   int n = 0;
@@ -352,6 +354,7 @@ extern "C" void am_engine_destroy(am_engine* eng) {
   if (!eng) return;
   set_device(eng);
   am_batch_destroy(eng->scratch);
+  am_hist_cache_free(eng->hist);
   for (auto& ev : eng->ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(eng->stream);
   delete eng;

@@ -881,7 +881,10 @@ __device__ __forceinline__ bool fast_diff(const uint8_t* IN, uint8_t* PS, uint32
 #ifndef AM_FAST_WAVES
 #define AM_FAST_WAVES 3
 #endif
-#define FD_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(AM_FAST_WAVES, 8)))
+#ifndef AM_FAST_WAVES_DIFF
+#define AM_FAST_WAVES_DIFF AM_FAST_WAVES
+#endif
+#define FD_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(kDiff ? AM_FAST_WAVES_DIFF : AM_FAST_WAVES, 8)))
 // kDiff: the variant launched for batches that ask for applyChanges patches (it also merges the
 // documents that do not); the other keeps the register budget of the plain merge.
 template <bool kDiff>

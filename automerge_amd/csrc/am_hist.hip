@@ -25,10 +25,18 @@
 namespace {
 
 template <typename T>
-struct DBuf {
+struct DevArr {
   T* p = nullptr;
-  bool alloc(size_t n) { return hipMalloc(&p, (n ? n : 1) * sizeof(T)) == hipSuccess; }
-  ~DBuf() { if (p) (void)hipFree(p); }
+  size_t cap = 0;
+  bool ensure(size_t n) {
+    if (n <= cap && p) return true;
+    if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+    const size_t want = n + n / 4 + 64;  // headroom: batches of similar sizes reuse the buffer
+    if (hipMalloc(&p, want * sizeof(T)) != hipSuccess) { p = nullptr; return false; }
+    cap = want;
+    return true;
+  }
+  ~DevArr() { if (p) (void)hipFree(p); }
 };
 
 std::string hexstr(const uint8_t* p, size_t n) {
@@ -42,12 +50,12 @@ std::string hexstr(const uint8_t* p, size_t n) {
 // actor ids and heads of a document chunk (decodeDocumentHeader, columnar.js:1006-1021), for the
 // error text only (the kernel has validated the header when it reports a history error)
 struct HdrText { std::vector<std::string> actors, heads; };
-HdrText header_text(const std::vector<uint8_t>& d) {
+HdrText header_text(const uint8_t* d, size_t n) {
   HdrText h;
   size_t o = 9;
   auto u = [&](uint64_t& v) {
     v = 0;
-    for (int sh = 0; o < d.size() && sh < 64; sh += 7) {
+    for (int sh = 0; o < n && sh < 64; sh += 7) {
       const uint8_t c = d[o++];
       v |= (uint64_t)(c & 0x7f) << sh;
       if (!(c & 0x80)) return true;
@@ -58,65 +66,115 @@ HdrText header_text(const std::vector<uint8_t>& d) {
   if (!u(len) || !u(na)) return h;
   for (uint64_t i = 0; i < na; i++) {
     uint64_t l;
-    if (!u(l) || l > d.size() - o) return h;
-    h.actors.push_back(hexstr(d.data() + o, l));
+    if (!u(l) || l > n - o) return h;
+    h.actors.push_back(hexstr(d + o, l));
     o += l;
   }
   if (!u(nh)) return h;
-  for (uint64_t i = 0; i < nh && o + 32 <= d.size(); i++, o += 32) h.heads.push_back(hexstr(d.data() + o, 32));
+  for (uint64_t i = 0; i < nh && o + 32 <= n; i++, o += 32) h.heads.push_back(hexstr(d + o, 32));
   return h;
 }
 
 struct DocRun {
   HistResult r{};
-  std::vector<HistChange> ch;
-  std::vector<uint8_t> bytes;  // the document's change-chunk region
-  uint64_t cap = 0;            // its size
+  std::vector<HistChange> ch;  // off = offset in `bytes`
+  const uint8_t* bytes = nullptr;
+  uint64_t cap = 0;            // the change-chunk region the kernel had
+};
+
+// device buffers kept by the engine between history batches (grown on demand)
+struct HistCache {
+  DevArr<uint8_t> arena, ws, out, dense;
+  DevArr<am_chunk_desc> chunks;
+  DevArr<ChunkInfo> info;
+  DevArr<HdrSlot> hdr;
+  DevArr<HistDesc> hd;
+  DevArr<HistResult> res;
+  DevArr<HistChange> chg;
+  DevArr<uint32_t> nchg;
+  DevArr<uint64_t> sizes, doff, scan_tmp;
+  std::vector<uint8_t> host;   // dense change bytes of the last batch
 };
 
 #define HCHECK(expr)                                                                       \
   do {                                                                                     \
     if ((expr) != hipSuccess) { why = std::string("automerge_amd: ") + #expr + " failed"; return false; } \
   } while (0)
+#define HALLOC(buf, n)                                                                     \
+  do {                                                                                     \
+    if (!(buf).ensure(n)) { why = "automerge_amd: device memory for the history batch"; return false; } \
+  } while (0)
 
-// k_chunks + k_history over `docs` (staged chunks); caps[i] = change-chunk bytes (0: the guess)
-bool run_history(am_engine* e, const std::vector<const std::vector<uint8_t>*>& docs, const std::vector<uint8_t>& verified,
+// A document chunk whose columns are stored as they are (no DEFLATEd column) goes to the GPU
+// unchanged; false also for anything the header walk cannot read (Backend.load's staging reports it)
+bool plain_columns(const uint8_t* p, size_t n) {
+  size_t o = 9;
+  auto u = [&](uint64_t& v) {
+    v = 0;
+    for (int sh = 0; o < n && sh < 64; sh += 7) {
+      const uint8_t c = p[o++];
+      v |= (uint64_t)(c & 0x7f) << sh;
+      if (!(c & 0x80)) return true;
+    }
+    return false;
+  };
+  uint64_t len, na, nh, nc, id, cl;
+  if (n < 10 || p[8] != 0 || !u(len) || !u(na)) return false;
+  for (uint64_t i = 0; i < na; i++) {
+    if (!u(cl) || cl > n - o) return false;
+    o += cl;
+  }
+  if (!u(nh) || nh > (n - o) / 32) return false;
+  o += 32 * nh;
+  for (int part = 0; part < 2; part++) {
+    if (!u(nc)) return false;
+    for (uint64_t i = 0; i < nc; i++) {
+      if (!u(id) || !u(cl)) return false;
+      if (id & 8) return false;
+    }
+  }
+  return true;
+}
+
+// k_chunks + k_history (+ the dense copy of the change chunks) over `docs` (staged chunks);
+// caps[i] = change-chunk bytes (0: the guess)
+bool run_history(am_engine* e, const std::vector<std::pair<const uint8_t*, size_t>>& docs, const std::vector<uint8_t>& verified,
                  const std::vector<uint64_t>& caps, std::vector<DocRun>& runs, std::string& why) {
   const uint32_t n = (uint32_t)docs.size();
   runs.assign(n, DocRun());
   if (!n) return true;
   HCHECK(hipSetDevice(am_engine_device(e)));
   hipStream_t s = am_engine_stream(e);
-  std::vector<uint8_t> arena;
+  void*& slot = am_engine_hist(e);
+  if (!slot) slot = new HistCache();
+  HistCache& K = *static_cast<HistCache*>(slot);
   std::vector<am_chunk_desc> cds(n);
+  uint64_t asz = 0;
   for (uint32_t i = 0; i < n; i++) {
-    cds[i] = {arena.size(), (uint32_t)docs[i]->size(), verified[i] ? 1u : 0u};
-    arena.insert(arena.end(), docs[i]->begin(), docs[i]->end());
-    arena.resize((arena.size() + 15) & ~(size_t)15);
+    cds[i] = {asz, (uint32_t)docs[i].second, verified[i] ? 1u : 0u};
+    asz = (asz + docs[i].second + 15) & ~(uint64_t)15;
   }
-  DBuf<uint8_t> da;
-  DBuf<am_chunk_desc> dc;
-  DBuf<ChunkInfo> di;
-  DBuf<HdrSlot> dhs;
-  HCHECK(da.alloc(arena.size() + 16) ? hipSuccess : hipErrorOutOfMemory);
-  HCHECK(dc.alloc(n) ? hipSuccess : hipErrorOutOfMemory);
-  HCHECK(di.alloc(n) ? hipSuccess : hipErrorOutOfMemory);
-  HCHECK(dhs.alloc(n) ? hipSuccess : hipErrorOutOfMemory);
-  HCHECK(hipMemcpyAsync(da.p, arena.data(), arena.size(), hipMemcpyHostToDevice, s));
-  HCHECK(hipMemcpyAsync(dc.p, cds.data(), sizeof(am_chunk_desc) * n, hipMemcpyHostToDevice, s));
+  std::vector<uint8_t> arena(asz);
+  for (uint32_t i = 0; i < n; i++) std::memcpy(arena.data() + cds[i].off, docs[i].first, docs[i].second);
+  HALLOC(K.arena, asz + 16);
+  HALLOC(K.chunks, n);
+  HALLOC(K.info, n);
+  HALLOC(K.hdr, n);
+  HCHECK(hipMemcpyAsync(K.arena.p, arena.data(), asz, hipMemcpyHostToDevice, s));
+  HCHECK(hipMemcpyAsync(K.chunks.p, cds.data(), sizeof(am_chunk_desc) * n, hipMemcpyHostToDevice, s));
   BatchDev bd{};
-  bd.arena = da.p;
-  bd.chunks = dc.p;
-  bd.info = di.p;
-  bd.hdr = dhs.p;
+  bd.arena = K.arena.p;
+  bd.chunks = K.chunks.p;
+  bd.info = K.info.p;
+  bd.hdr = K.hdr.p;
   bd.nchunks = n;
   am_launch_chunks(bd, s);
   std::vector<ChunkInfo> info(n);
-  HCHECK(hipMemcpyAsync(info.data(), di.p, sizeof(ChunkInfo) * n, hipMemcpyDeviceToHost, s));
+  HCHECK(hipMemcpyAsync(info.data(), K.info.p, sizeof(ChunkInfo) * n, hipMemcpyDeviceToHost, s));
   HCHECK(hipStreamSynchronize(s));
   // layout: workspace, change-chunk regions and change records per document
   std::vector<HistDesc> hd;
-  std::vector<uint32_t> which;  // hd index -> document
+  std::vector<uint32_t> which, nchg;  // hd index -> document, its change count
   uint64_t ws_tot = 0, out_tot = 0, chg_tot = 0;
   const uint64_t kDocLimit = 32ull << 30;  // one document's workspace + output
   for (uint32_t i = 0; i < n; i++) {
@@ -141,44 +199,58 @@ bool run_history(am_engine* e, const std::vector<const std::vector<uint8_t>*>& d
     runs[i].cap = cap;
     hd.push_back(h);
     which.push_back(i);
+    nchg.push_back(ok ? ci.nchg : 0);
   }
   const uint32_t nd = (uint32_t)hd.size();
   if (!nd) return true;
-  DBuf<uint8_t> dws, dout;
-  DBuf<HistDesc> dhd;
-  DBuf<HistResult> dres;
-  DBuf<HistChange> dch;
-  if (!dws.alloc(ws_tot) || !dout.alloc(out_tot + 16) || !dhd.alloc(nd) || !dres.alloc(nd) || !dch.alloc(chg_tot)) {
-    why = "automerge_amd: device memory for the history batch";
-    return false;
-  }
-  HCHECK(hipMemcpyAsync(dhd.p, hd.data(), sizeof(HistDesc) * nd, hipMemcpyHostToDevice, s));
-  am_launch_history(da.p, dc.p, di.p, dhd.p, nd, dws.p, dout.p, dres.p, dch.p, s);
+  HALLOC(K.ws, ws_tot);
+  HALLOC(K.out, out_tot + 16);
+  HALLOC(K.hd, nd);
+  HALLOC(K.res, nd);
+  HALLOC(K.chg, chg_tot);
+  HALLOC(K.nchg, nd);
+  HALLOC(K.sizes, nd);
+  HALLOC(K.doff, nd + 1);
+  HALLOC(K.scan_tmp, am_scan_tmp_elems(nd));
+  HCHECK(hipMemcpyAsync(K.hd.p, hd.data(), sizeof(HistDesc) * nd, hipMemcpyHostToDevice, s));
+  HCHECK(hipMemcpyAsync(K.nchg.p, nchg.data(), sizeof(uint32_t) * nd, hipMemcpyHostToDevice, s));
+  am_launch_history(K.arena.p, K.chunks.p, K.info.p, K.hd.p, nd, K.ws.p, K.out.p, K.res.p, K.chg.p, s);
   HCHECK(hipGetLastError());
+  // the change chunks of the documents that succeeded, back to back (k_history_sizes rewrites the
+  // records' offsets: dense offset in the low word)
+  am_launch_history_sizes(K.res.p, K.hd.p, nd, K.nchg.p, K.chg.p, K.sizes.p, s);
+  am_launch_scan(K.sizes.p, K.doff.p, K.scan_tmp.p, nd, K.doff.p + nd, s);
   std::vector<HistResult> res(nd);
   std::vector<HistChange> chs(chg_tot);
-  std::vector<uint8_t> outb(out_tot);
-  HCHECK(hipMemcpyAsync(res.data(), dres.p, sizeof(HistResult) * nd, hipMemcpyDeviceToHost, s));
-  if (chg_tot) HCHECK(hipMemcpyAsync(chs.data(), dch.p, sizeof(HistChange) * chg_tot, hipMemcpyDeviceToHost, s));
-  if (out_tot) HCHECK(hipMemcpyAsync(outb.data(), dout.p, out_tot, hipMemcpyDeviceToHost, s));
+  std::vector<uint64_t> doff(nd + 1);
+  HCHECK(hipMemcpyAsync(res.data(), K.res.p, sizeof(HistResult) * nd, hipMemcpyDeviceToHost, s));
+  if (chg_tot) HCHECK(hipMemcpyAsync(chs.data(), K.chg.p, sizeof(HistChange) * chg_tot, hipMemcpyDeviceToHost, s));
+  HCHECK(hipMemcpyAsync(doff.data(), K.doff.p, sizeof(uint64_t) * (nd + 1), hipMemcpyDeviceToHost, s));
+  HCHECK(hipStreamSynchronize(s));
+  const uint64_t dense = doff[nd];
+  HALLOC(K.dense, dense);
+  am_launch_history_compact(K.res.p, K.hd.p, nd, K.nchg.p, K.chg.p, K.doff.p, K.out.p, K.dense.p, s);
+  K.host.resize(dense);
+  if (dense) HCHECK(hipMemcpyAsync(K.host.data(), K.dense.p, dense, hipMemcpyDeviceToHost, s));
   HCHECK(hipStreamSynchronize(s));
   for (uint32_t k = 0; k < nd; k++) {
     DocRun& r = runs[which[k]];
     r.r = res[k];
-    const uint64_t nc = info[which[k]].nchg;
     if (r.r.status == HE_OK || r.r.status == HE_HEADS) {
-      r.ch.assign(chs.begin() + hd[k].chg_off, chs.begin() + hd[k].chg_off + nc);
-      r.bytes.assign(outb.begin() + hd[k].out_off, outb.begin() + hd[k].out_off + hd[k].out_cap);
+      r.ch.assign(chs.begin() + hd[k].chg_off, chs.begin() + hd[k].chg_off + nchg[k]);
+      if (r.r.status == HE_OK)
+        for (HistChange& c : r.ch) c.off = (uint32_t)c.off;
+      r.bytes = K.host.data() + doff[k];
     }
   }
   return true;
 }
 
-std::string history_message(const DocRun& r, const std::vector<uint8_t>& doc, uint32_t& code) {
+std::string history_message(const DocRun& r, const uint8_t* doc, size_t len, uint32_t& code) {
   code = AM_E_HISTORY;
   const HistResult& x = r.r;
   auto actor = [&](int64_t a) {
-    const HdrText h = header_text(doc);
+    const HdrText h = header_text(doc, len);
     return a >= 0 && (size_t)a < h.actors.size() ? h.actors[a] : std::string("undefined");
   };
   char buf[256];
@@ -196,7 +268,7 @@ std::string history_message(const DocRun& r, const std::vector<uint8_t>& doc, ui
     case HE_EXTRA: return "Bad datatype for extra bytes: 7";
     case HE_DEL: return "document should not contain del operations";
     case HE_HEADS: {
-      const HdrText h = header_text(doc);
+      const HdrText h = header_text(doc, len);
       std::vector<std::string> got;
       for (auto& c : r.ch) if (c.head) got.push_back(hexstr(c.hash, 32));
       std::sort(got.begin(), got.end());
@@ -219,27 +291,37 @@ void set_err(am_error* e, uint32_t code, const std::string& m) {
 
 }  // namespace
 
+void am_hist_cache_free(void* cache) { delete static_cast<HistCache*>(cache); }
+
 extern "C" int am_document_changes_batch(am_engine* eng, const uint8_t* const* docs, const size_t* lens, size_t n, am_history* out) {
   for (size_t i = 0; i < n; i++) { std::memset(&out[i], 0, sizeof(am_history)); }
-  // Backend.load's staging of every document
+  // Backend.load's staging of every document: chunks with DEFLATEd columns are inflated (and their
+  // checksum verified) first, the others go to the GPU as they are
   std::vector<std::vector<uint8_t>> staged(n);
+  std::vector<std::pair<const uint8_t*, size_t>> src(n);
   std::vector<uint8_t> verified(n, 0);
   std::vector<uint32_t> live;
   for (size_t i = 0; i < n; i++) {
-    std::vector<uint8_t> in(docs[i], docs[i] + lens[i]);
-    bool v = false;
-    if (!am_stage_doc_chunk(eng, in, staged[i], v, &out[i].err)) continue;
-    verified[i] = v;
+    if (plain_columns(docs[i], lens[i])) {
+      src[i] = {docs[i], lens[i]};
+    } else {
+      std::vector<uint8_t> in(docs[i], docs[i] + lens[i]);
+      bool v = false;
+      if (!am_stage_doc_chunk(eng, in, staged[i], v, &out[i].err)) continue;
+      verified[i] = v;
+      src[i] = {staged[i].data(), staged[i].size()};
+    }
     live.push_back((uint32_t)i);
   }
   std::vector<DocRun> runs(n);
+  std::vector<std::vector<uint8_t>> keep;  // the first pass's change bytes when a second pass runs
   std::string why;
   for (int pass = 0; pass < 2 && !live.empty(); pass++) {
-    std::vector<const std::vector<uint8_t>*> ds;
+    std::vector<std::pair<const uint8_t*, size_t>> ds;
     std::vector<uint8_t> vs;
     std::vector<uint64_t> caps;
     for (uint32_t i : live) {
-      ds.push_back(&staged[i]);
+      ds.push_back(src[i]);
       vs.push_back(verified[i]);
       caps.push_back(pass ? (uint64_t)runs[i].r.a1 : 0);
     }
@@ -256,6 +338,12 @@ extern "C" int am_document_changes_batch(am_engine* eng, const uint8_t* const* d
       if (!pass && runs[i].r.status == HE_CODE && runs[i].r.a0 == AM_U_CAPACITY && (uint64_t)runs[i].r.a1 > runs[i].cap)
         again.push_back(i);
     }
+    if (!pass && !again.empty()) {  // the cache's host buffer is reused by the second pass
+      HistCache& K = *static_cast<HistCache*>(am_engine_hist(eng));
+      keep.emplace_back(K.host);
+      for (size_t i = 0; i < n; i++)
+        if (runs[i].bytes) runs[i].bytes = keep.back().data() + (runs[i].bytes - K.host.data());
+    }
     live.swap(again);
   }
   int rc = 0;
@@ -264,7 +352,7 @@ extern "C" int am_document_changes_batch(am_engine* eng, const uint8_t* const* d
     const DocRun& r = runs[i];
     if (r.r.status != HE_OK) {
       uint32_t code;
-      const std::string m = history_message(r, staged[i], code);
+      const std::string m = history_message(r, src[i].first, src[i].second, code);
       set_err(&out[i].err, code ? code : AM_U_VALUE, m);
       rc = 1;
       continue;
@@ -272,8 +360,7 @@ extern "C" int am_document_changes_batch(am_engine* eng, const uint8_t* const* d
     std::vector<Bytes> chs;
     size_t total = 0;
     for (const HistChange& c : r.ch) {
-      if (c.off + c.len > r.bytes.size()) { set_err(&out[i].err, AM_U_CAPACITY, "automerge_amd: history output out of range"); break; }
-      chs.push_back(deflate_change(Bytes(r.bytes.begin() + c.off, r.bytes.begin() + c.off + c.len)));
+      chs.push_back(deflate_change(Bytes(r.bytes + c.off, r.bytes + c.off + c.len)));
       total += chs.back().size();
     }
     if (out[i].err.code) { rc = 1; continue; }

@@ -699,6 +699,47 @@ void am_launch_history(const uint8_t* arena, const am_chunk_desc* chunks, const 
   if (!ndocs) return;
   hipLaunchKernelGGL(k_history, dim3(ndocs), dim3(64), 0, s, arena, chunks, info, hd, ndocs, ws, out, res, chg_out);
 }
+__global__ void __launch_bounds__(256) k_history_sizes(const HistResult* __restrict__ res, const HistDesc* __restrict__ hd, uint32_t ndocs,
+                                                      const uint32_t* __restrict__ nchg, HistChange* __restrict__ chg,
+                                                      uint64_t* __restrict__ sizes) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= ndocs) return;
+  uint64_t acc = 0;
+  if (res[d].status == HE_OK) {
+    HistChange* c = chg + hd[d].chg_off;
+    for (uint32_t k = 0; k < nchg[d]; k++) {
+      const uint64_t src = c[k].off;
+      c[k].off = acc | (src << 32);  // dense offset (low) | region offset (high): both < 4 GiB per document
+      acc += c[k].len;
+    }
+  }
+  sizes[d] = acc;
+}
+__global__ void __launch_bounds__(64) k_history_compact(const HistResult* __restrict__ res, const HistDesc* __restrict__ hd, uint32_t ndocs,
+                                                        const uint32_t* __restrict__ nchg,
+                                                        const HistChange* __restrict__ chg, const uint64_t* __restrict__ doc_off,
+                                                        const uint8_t* __restrict__ out, uint8_t* __restrict__ dst) {
+  const uint32_t d = blockIdx.x;
+  if (d >= ndocs || res[d].status != HE_OK) return;  // only documents whose records k_history_sizes rewrote
+  const HistDesc h = hd[d];
+  uint8_t* o = dst + doc_off[d];
+  for (uint32_t k = 0; k < nchg[d]; k++) {
+    const HistChange c = chg[h.chg_off + k];
+    const uint8_t* src = out + h.out_off + (c.off >> 32);
+    uint8_t* q = o + (uint32_t)c.off;
+    for (uint32_t i = threadIdx.x; i < c.len; i += 64) q[i] = src[i];
+  }
+}
+void am_launch_history_sizes(const HistResult* res, const HistDesc* hd, uint32_t ndocs, const uint32_t* nchg, HistChange* chg,
+                             uint64_t* sizes, hipStream_t s) {
+  if (!ndocs) return;
+  hipLaunchKernelGGL(k_history_sizes, dim3((ndocs + 255) / 256), dim3(256), 0, s, res, hd, ndocs, nchg, chg, sizes);
+}
+void am_launch_history_compact(const HistResult* res, const HistDesc* hd, uint32_t ndocs, const uint32_t* nchg, const HistChange* chg,
+                               const uint64_t* doc_off, const uint8_t* out, uint8_t* dst, hipStream_t s) {
+  if (!ndocs) return;
+  hipLaunchKernelGGL(k_history_compact, dim3(ndocs), dim3(64), 0, s, res, hd, ndocs, nchg, chg, doc_off, out, dst);
+}
 void am_launch_bounds(const BatchDev& b, hipStream_t s) {
   if (!b.ndocs) return;
   (void)hipMemsetAsync(b.max_hot, 0, 2 * sizeof(uint64_t), s);

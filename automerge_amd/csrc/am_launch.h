@@ -74,6 +74,16 @@ void am_launch_sync_select(uint32_t npairs, const uint64_t* d_coff, const uint8_
 // k_history (am_hist_dev.h): one workgroup per document of the change history
 void am_launch_history(const uint8_t* arena, const am_chunk_desc* chunks, const ChunkInfo* info, const HistDesc* hd, uint32_t ndocs,
                        uint8_t* ws, uint8_t* out, HistResult* res, HistChange* chg_out, hipStream_t s);
+// per-document change bytes of the history batch (thread per document over its change records:
+// offsets within the document, its total), then the dense copy (workgroup per document) to
+// dst + doc_off[d] (an exclusive scan of the totals)
+void am_launch_history_sizes(const HistResult* res, const HistDesc* hd, uint32_t ndocs, const uint32_t* nchg, HistChange* chg,
+                             uint64_t* sizes, hipStream_t s);
+void am_launch_history_compact(const HistResult* res, const HistDesc* hd, uint32_t ndocs, const uint32_t* nchg, const HistChange* chg,
+                               const uint64_t* doc_off, const uint8_t* out, uint8_t* dst, hipStream_t s);
+// the engine's history buffers (am_hist.hip), freed with the engine
+void*& am_engine_hist(am_engine* e);
+void am_hist_cache_free(void* cache);
 // host stages of am_capi.hip shared with am_hist.hip: Backend.load's staging of a document chunk
 // (DEFLATEd columns inflated, checksum verified), the reference error text of an AM_* code
 bool am_stage_doc_chunk(am_engine* e, const std::vector<uint8_t>& in, std::vector<uint8_t>& out, bool& verified, am_error* err);

@@ -5,10 +5,10 @@ set -e
 cd "$(dirname "$0")/../automerge_amd/csrc"
 F="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -munsafe-fp-atomics"
 mkdir -p ../../tools/probe
-make -s am_capi.o am_workload.o am_sync.o
+make -s am_capi.o am_sync.o am_inflate.o am_hist.o am_graph.o am_local.o am_sync_proto.o
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   /opt/rocm/bin/hipcc $F $flags -c am_kernels.hip -o /tmp/am_kernels_$name.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared -o ../../tools/probe/libam_$name.so /tmp/am_kernels_$name.o am_capi.o am_sync.o am_workload.o -lz -lpthread
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared -o ../../tools/probe/libam_$name.so /tmp/am_kernels_$name.o am_capi.o am_sync.o am_inflate.o am_hist.o am_graph.o am_local.o am_sync_proto.o -lz -lpthread -lhsa-runtime64
   echo built tools/probe/libam_$name.so
 done

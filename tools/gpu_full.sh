@@ -11,3 +11,7 @@ timeout -k 10 400 python bench.py > gpurun_out/$TAG/bench.json 2> gpurun_out/$TA
 cut -c1-1500 gpurun_out/$TAG/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$TAG/prof -o run -- python3 bench.py --no-cpu-baseline --check 4 > gpurun_out/$TAG/bench_prof.json 2> gpurun_out/$TAG/bench_prof.err || { tail -20 gpurun_out/$TAG/bench_prof.err; exit 1; }
 find gpurun_out/$TAG/prof -name "*stats*.csv"
+timeout -k 10 300 python tools/bench_history.py > gpurun_out/$TAG/history_bench.json 2>&1 || { tail -20 gpurun_out/$TAG/history_bench.json; exit 1; }
+cat gpurun_out/$TAG/history_bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$TAG/hprof -o run -- python3 tools/bench_history.py --reps 2 > gpurun_out/$TAG/history_prof.json 2>&1 || { tail -20 gpurun_out/$TAG/history_prof.json; exit 1; }
+find gpurun_out/$TAG/hprof -name "*stats*.csv"
