@@ -67,12 +67,14 @@ def kernel_source_digest():
     return h.hexdigest()[:16]
 
 
-def measured_traffic():
+def measured_traffic(batch_docs):
+    """profiles/traffic_k_doc.json when it was measured on these kernel sources and batch size."""
     try:
         rec = json.load(open(os.path.join(ROOT, "profiles", "traffic_k_doc.json")))
     except (OSError, ValueError):
         return None
-    return rec if rec.get("src_digest") == kernel_source_digest() else None
+    ok = rec.get("src_digest") == kernel_source_digest() and rec.get("batch_docs") == batch_docs
+    return rec if ok else None
 
 
 def cpu_reference():
@@ -185,7 +187,10 @@ def main():
             return b.doc_output(i, res[i]), (b.doc_patch(i) if not args.no_patch else None)
     else:
         from automerge_amd import pipe
-        batch = args.batch or max(16384, min(131072, -(-D // 4)))
+        # 65536 documents per batch: the pipeline is bound by H2D and by the kernel chain alike, and
+        # smaller batches shorten its fill and drain (131072: 52-57 ms per step, 65536: 48 ms, 32768:
+        # 49 ms, 16384: 57 ms; tools/gpu_batch_ab.sh)
+        batch = args.batch or max(16384, min(65536, -(-D // 4)))
         parts = split_batches(arena, chunks, docs, batch)
         # capacities from a representative batch (the largest one), staged the ordinary way
         probe = Batch(device=local)
@@ -295,7 +300,8 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
     value = tot[1] / (elapsed / args.steps)
     achieved = alg_launch / (t_doc * 1e-3) / 1e9 if t_doc else None
-    tr = measured_traffic() if args.mode == "pipe" and args.workload == "c4" and not args.no_patch else None
+    tr = (measured_traffic(extra.get("batch_docs")) if args.mode == "pipe" and args.workload == "c4" and not args.no_patch
+          else None)
     if tr is not None and t_doc:
         # decode GB/s: HBM bytes the document kernel fetches per launch / its time
         extra["decode_GBps"] = 2 * tr["fetch_size_kib"] * 1024 / (t_doc * 1e-3) / 1e9

@@ -43,11 +43,18 @@ def main():
     from bench import kernel_source_digest
     fetch = per_launch(root, "FETCH_SIZE")
     write = per_launch(root, "WRITE_SIZE")
+    batch = None
+    try:  # the bench line of the FETCH_SIZE pass names its batch size
+        line = [x for x in open(os.path.join(root, "FETCH_SIZE.log")) if x.startswith("{")][-1]
+        batch = json.loads(line).get("batch_docs")
+    except (OSError, IndexError, ValueError):
+        pass
     kf = sum(v for k, v in fetch.items() if k in STAGE)
     kw = sum(v for k, v in write.items() if k in STAGE)
     rec = {
         "kernel": "k_doc",
         "src_digest": kernel_source_digest(),
+        "batch_docs": batch,
         "fetch_size_kib": kf, "write_size_kib": kw,
         "traffic_bytes": int(2 * kf * 1024 + kw * 1024),
         "correction": "2 x FETCH_SIZE (gfx950, 16 B/lane streaming reads) + WRITE_SIZE",
