@@ -6,7 +6,7 @@ import json
 import os
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-FILES = ["sync", "backend", "test", "text", "table", "errors"]
+FILES = ["sync", "sync_random", "backend", "test", "text", "table", "errors"]
 # Scenarios where this engine knowingly differs from the reference, with the reason. Each must still
 # fail loudly with an "automerge_amd: unsupported" error (never a silently different result).
 KNOWN_DIVERGENT = {
@@ -64,6 +64,8 @@ def canon(x):
         return [canon(v) for v in x]
     if isinstance(x, dict):
         return {k: canon(x[k]) for k in sorted(x)}
+    if _is_handle(x):
+        return {"$h": "?"}  # a backend state (only in mismatch reports)
     raise TypeError("cannot canonicalize %r" % (x,))
 
 

@@ -5,6 +5,8 @@
 // Backend exports of backend/index.js: tests/js/backend_log_replay.js replays each call against
 // automerge_amd/js/backend.js and compares every result.
 //   NODE_PATH=tests/golden/gen/node_modules node tests/golden/gen/make_backend_log.js
+// AM_LOG_FILES=sync_random AM_LOG_MAX=4000 records the randomized sync sessions instead
+// (backend_log_sync_random.json).
 // Clock and randomness are pinned (Date without arguments = epoch, seeded randomBytes and
 // Math.random), so a re-run reproduces the committed tests/golden/backend_log_*.json byte for byte.
 'use strict'
@@ -105,11 +107,67 @@ function harness(file) {
   return tests
 }
 
+// ---- randomized sync sessions (getChangesToSend, sync.js:246-306, and the protocol around it) ----
+// Two peers with a shared prefix and divergent histories (map sets, list inserts/deletes, text),
+// synced with the reference's own generateSyncMessage / receiveSyncMessage until both stop sending;
+// some sessions edit while syncing, some reconnect midway with a persisted sync state
+// (encodeSyncState / decodeSyncState keep lastSync only), large histories make the Bloom filters
+// report false positives that the `need` round trip repairs (sync.js:246-306, 327-473).
+function randomSyncTests() {
+  const tests = []
+  let s = 0x5eed
+  const rnd = n => { s = (Math.imul(s, 1103515245) + 12345) >>> 0; return (s >>> 8) % n }
+  const edit = (doc, k) => Automerge.change(doc, {time: 0}, d => {
+    if (!d.list) { d.list = []; d.text = new Automerge.Text(); d.map = {} }
+    for (let q = 0; q < 1 + rnd(4); q++) {
+      const x = rnd(5)
+      if (x === 0) d.map['k' + rnd(6)] = rnd(1000)
+      else if (x === 1) d.list.push(k * 100 + q)
+      else if (x === 2 && d.list.length) d.list.splice(rnd(d.list.length), 1)
+      else if (x === 3) d.text.insertAt(rnd(d.text.length + 1), String.fromCharCode(97 + rnd(26)))
+      else if (d.text.length) d.text.deleteAt(rnd(d.text.length))
+    }
+  })
+  for (let k = 0; k < 36; k++) {
+    tests.push({name: 'random sync session ' + k, before: [], after: [], fn: () => {
+      const big = k % 6 === 5
+      // the list / text / map objects come from one shared first change: two peers creating the same
+      // root key concurrently make the patches depend on new.js's per-pass objectMeta.children
+      // snapshot (DESIGN.md §1, residual divergences), which this log is not about
+      const shared = 1 + (rnd(3) ? rnd(big ? 60 : 15) : 0)
+      const na = rnd(big ? 150 : 12), nb = rnd(big ? 150 : 12)
+      let a = Automerge.init((0xa000 + k).toString(16) + 'aa'), b = Automerge.init((0xb000 + k).toString(16) + 'bb')
+      for (let i = 0; i < shared; i++) a = edit(a, i)
+      b = Automerge.merge(b, a)
+      for (let i = 0; i < na; i++) a = edit(a, 1000 + i)
+      for (let i = 0; i < nb; i++) b = edit(b, 2000 + i)
+      let sa = Automerge.initSyncState(), sb = Automerge.initSyncState()
+      const concurrent = k % 4 === 1, reconnect = k % 4 === 2
+      for (let round = 0; round < 40; round++) {
+        let msg, sent = false;
+        [sa, msg] = Automerge.generateSyncMessage(a, sa)
+        if (msg) { sent = true; [b, sb] = Automerge.receiveSyncMessage(b, sb, msg) }
+        [sb, msg] = Automerge.generateSyncMessage(b, sb)
+        if (msg) { sent = true; [a, sa] = Automerge.receiveSyncMessage(a, sa, msg) }
+        if (concurrent && round < 3) { a = edit(a, 3000 + round); b = edit(b, 4000 + round) }
+        if (reconnect && round === 1) {
+          sa = Automerge.Backend.decodeSyncState(Automerge.Backend.encodeSyncState(sa))
+          sb = Automerge.Backend.decodeSyncState(Automerge.Backend.encodeSyncState(sb))
+        }
+        if (!sent && !(concurrent && round < 3)) break
+      }
+      const heads = d => Automerge.Backend.getHeads(Automerge.Frontend.getBackendState(d))
+      assert.deepStrictEqual(heads(a), heads(b))
+    }})
+  }
+  return tests
+}
+
 const MAX_ENTRIES = +(process.env.AM_LOG_MAX || 400)
 function run(file) {
   const scenarios = []
   let passed = 0, failed = 0, skipped = 0
-  for (const t of harness(file)) {
+  for (const t of (file === 'sync_random' ? randomSyncTests() : harness(file))) {
     if (t.fn.length > 0) { skipped++; continue }  // callback-style tests
     handles = new Map()
     nextHandle = 0
@@ -122,6 +180,7 @@ function run(file) {
       for (const a of t.after) a()
     } catch (e) {
       ok = false
+      if (process.env.AM_LOG_DEBUG) console.log(t.name, e.stack)
     }
     if (ok) passed++; else failed++
     if (ok && log.length > 0 && log.length <= MAX_ENTRIES) scenarios.push({name: t.name, log})
