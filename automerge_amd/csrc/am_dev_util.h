@@ -540,6 +540,81 @@ __device__ static uint32_t block_excl_scan(uint32_t* a, uint32_t n, uint32_t* s_
   return carry;
 }
 
+// Stable LSD radix sort of n (key, val) pairs by the low `bits` bits of the keys, 8-bit digits, by
+// the whole block (blockDim.x a multiple of 64, at most 256). k0 / v0 hold the input and on return
+// the sorted pairs; k1 / v1 are scratch of n entries. Per digit: an LDS histogram, its exclusive
+// scan, then tiles of blockDim.x pairs scattered in order -- a pair's place is its bucket's base,
+// the same-digit pairs of earlier waves of the tile and its rank among its wave's same-digit lanes
+// (eight ballots). A digit every key shares is skipped. O(n) per digit against bitonic's
+// O(n log^2 n) compare-exchanges, for the large documents' id and document-order sorts.
+__device__ static void block_radix_sort(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, uint32_t n, uint32_t bits) {
+  __shared__ uint32_t s_hist[256];
+  __shared__ uint32_t s_wc[4 * 256];
+  __shared__ uint32_t s_skip;
+  const uint32_t T = blockDim.x, t = threadIdx.x, w = t >> 6, lane = t & 63, W = T >> 6;
+  uint64_t* ka = k0;
+  uint32_t* va = v0;
+  uint64_t* kb = k1;
+  uint32_t* vb = v1;
+  for (uint32_t sh = 0; sh < bits; sh += 8) {
+    for (uint32_t d = t; d < 256; d += T) s_hist[d] = 0;
+    if (t == 0) s_skip = 0;
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += T) atomicAdd(&s_hist[(uint32_t)(ka[i] >> sh) & 255u], 1u);
+    __syncthreads();
+    if (t == 0) {  // exclusive scan of the 256 buckets; one bucket holding every key: nothing to do
+      uint32_t run = 0;
+      for (uint32_t d = 0; d < 256; d++) {
+        const uint32_t c = s_hist[d];
+        if (c == n) s_skip = 1;
+        s_hist[d] = run;
+        run += c;
+      }
+    }
+    __syncthreads();
+    const bool skip = s_skip != 0;
+    __syncthreads();  // every thread has read s_skip before the next pass resets it
+    if (skip) continue;
+    for (uint32_t b0 = 0; b0 < n; b0 += T) {
+      const uint32_t i = b0 + t;
+      const bool act = i < n;
+      const uint64_t key = act ? ka[i] : 0;
+      const uint32_t val = act ? va[i] : 0;
+      const uint32_t dg = (uint32_t)(key >> sh) & 255u;
+      uint64_t peers = __ballot(act);
+#pragma unroll
+      for (int bt = 0; bt < 8; bt++) {
+        const uint64_t m = __ballot(act && ((dg >> bt) & 1u));
+        peers &= ((dg >> bt) & 1u) ? m : ~m;
+      }
+      const uint32_t rank = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+      for (uint32_t x = t; x < W * 256; x += T) s_wc[x] = 0;
+      __syncthreads();
+      if (act && rank == 0) s_wc[w * 256 + dg] = (uint32_t)__popcll(peers);
+      __syncthreads();
+      if (act) {
+        uint32_t off = s_hist[dg] + rank;
+        for (uint32_t q = 0; q < w; q++) off += s_wc[q * 256 + dg];
+        kb[off] = key;
+        vb[off] = val;
+      }
+      __syncthreads();
+      for (uint32_t d = t; d < 256; d += T) {
+        uint32_t c = 0;
+        for (uint32_t q = 0; q < W; q++) c += s_wc[q * 256 + d];
+        s_hist[d] += c;
+      }
+      __syncthreads();
+    }
+    uint64_t* tk = ka; ka = kb; kb = tk;
+    uint32_t* tv = va; va = vb; vb = tv;
+  }
+  if (ka != k0) {  // an odd number of scatters: the result is in the scratch arrays
+    for (uint32_t i = t; i < n; i += T) { k0[i] = ka[i]; v0[i] = va[i]; }
+    __syncthreads();
+  }
+}
+
 // Bitonic sort of a[0..P) (P power of two, padded with elements that compare as +inf).
 template <typename T, typename Less>
 __device__ static void block_bitonic_sort(T* a, uint32_t P, Less less) {

@@ -958,6 +958,128 @@ __device__ static void wire_out(PatchOut& po, int64_t max_op, uint8_t* dst, uint
   patch_pack(po, max_op, dst, cap);
 }
 
+// ---- radix sorts of the large-document path (global mode): the id index (P5c) and the document
+// order (P5g) as stable LSD radix sorts of packed integer keys (block_radix_sort) instead of
+// bitonic sorts; scratch in the tour arrays (dead before P5f, and again once P5g's keys are built:
+// 16 R + 16 R bytes). Keys outside the packing (counters >= 2^46, 2^16+ actors) keep the bitonic
+// sort. ----
+__device__ __forceinline__ uint32_t rs_bits(uint64_t mx) { return mx ? 64u - (uint32_t)__clzll((long long)mx) : 0u; }
+
+// P5c: (ctr, actor index, row) ascending; the rows enter in row order, so a stable sort by
+// ctr << 16 | actor keeps equal ids in row order
+__device__ static bool radix_idk(DocShared& s, IdKey* idk, uint32_t R) {
+  __shared__ unsigned long long s_max;
+  __shared__ uint32_t s_bad;
+  const uint32_t t = threadIdx.x, T = blockDim.x;
+  uint64_t* k0 = hp<uint64_t>(s, s.L.tour_nxt);
+  uint64_t* k1 = k0 + R;
+  uint32_t* v0 = hp<uint32_t>(s, s.L.tour_w);
+  uint32_t* v1 = v0 + R;
+  if (t == 0) { s_max = 0; s_bad = 0; }
+  __syncthreads();
+  for (uint32_t i = t; i < R; i += T) {
+    const int64_t c = idk[i].ctr;
+    const int32_t a = idk[i].actor;
+    if (c < 0 || c >= (1ll << 46) || a < 0 || a >= 65536) { s_bad = 1; continue; }
+    const uint64_t key = ((uint64_t)c << 16) | (uint64_t)a;
+    k0[i] = key;
+    v0[i] = (uint32_t)idk[i].row;
+    atomicMax(&s_max, (unsigned long long)key);
+  }
+  __syncthreads();
+  const bool bad = s_bad != 0;
+  const uint32_t bits = rs_bits(s_max);
+  __syncthreads();
+  if (bad) return false;
+  block_radix_sort(k0, v0, k1, v1, R, bits);
+  for (uint32_t i = t; i < R; i += T) {
+    IdKey k;
+    k.ctr = (int64_t)(k0[i] >> 16);
+    k.actor = (int32_t)(k0[i] & 0xffff);
+    k.row = (int32_t)v0[i];
+    idk[i] = k;
+  }
+  __syncthreads();
+  return true;
+}
+
+// P5g: object, then (map key in UTF-16 order | list position), then opId -- three stable passes,
+// least significant first. Map keys get dense ranks from a bitonic sort of the keyed records only
+// (few in list-heavy documents). Afterwards only sr[i].row is meaningful (all that later phases read).
+__device__ static bool radix_docorder(DocShared& s, SortRec* sr, uint32_t n, uint32_t R, const APtr A) {
+  __shared__ unsigned long long s_max;
+  __shared__ uint32_t s_bad;
+  const uint32_t t = threadIdx.x, T = blockDim.x;
+  uint64_t* k0 = hp<uint64_t>(s, s.L.tour_nxt);
+  uint64_t* k1 = k0 + n;
+  uint32_t* v0 = hp<uint32_t>(s, s.L.tour_w);
+  uint32_t* v1 = v0 + n;
+  uint32_t* sk = v0 + 2 * (uint64_t)R;  // keyed records (pow2 <= 2 R entries)
+  if (t == 0) s_bad = 0;
+  __syncthreads();
+  for (uint32_t i = t; i < n; i += T) {
+    const SortRec& r = sr[i];
+    if (r.obj_ctr + 1 < 0 || r.obj_ctr + 1 >= (1ll << 46) || r.obj_rank + 1 < 0 || r.obj_rank + 1 >= 65536 || r.id_ctr < 0 ||
+        r.id_ctr >= (1ll << 46) || r.id_rank < 0 || r.id_rank >= 65536 || (r.kind && (r.k1 > 0 || r.k1 < -(1ll << 38))))
+      s_bad = 1;
+    v1[i] = r.kind == 0 ? 1u : 0u;
+  }
+  __syncthreads();
+  const bool bad = s_bad != 0;
+  __syncthreads();
+  if (bad) return false;
+  // dense UTF-16 ranks of the map keys (into k1 of the keyed records)
+  const uint32_t K = block_excl_scan(v1, n, s.tmp);
+  __syncthreads();
+  if (K) {
+    const uint32_t PK = pow2_ceil(K);
+    for (uint32_t i = t; i < n; i += T)
+      if (sr[i].kind == 0) sk[v1[i]] = i;
+    for (uint32_t j = K + t; j < PK; j += T) sk[j] = ~0u;
+    __syncthreads();
+    auto kcmp = [&](uint32_t a, uint32_t b) {
+      return utf16_cmp_dev(A + sr[a].key_off, sr[a].key_len, A + sr[b].key_off, sr[b].key_len);
+    };
+    block_bitonic_sort(sk, PK, [&](uint32_t a, uint32_t b) {
+      if (a == ~0u || b == ~0u) return a != ~0u && b == ~0u;
+      const int c = kcmp(a, b);
+      return c ? c < 0 : a < b;
+    });
+    for (uint32_t j = t; j < K; j += T) v1[j] = (j == 0 || kcmp(sk[j - 1], sk[j]) != 0) ? 1u : 0u;
+    __syncthreads();
+    block_excl_scan(v1, K, s.tmp);
+    __syncthreads();
+    for (uint32_t j = t; j < K; j += T) {
+      const bool fresh = j == 0 || kcmp(sk[j - 1], sk[j]) != 0;
+      sr[sk[j]].k1 = (int64_t)(v1[j] + (fresh ? 1u : 0u)) - 1;  // dense rank
+    }
+    __syncthreads();
+  }
+  for (int stage = 0; stage < 3; stage++) {
+    if (t == 0) s_max = 0;
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += T) {
+      const SortRec& r = sr[stage == 0 ? i : v0[i]];
+      uint64_t key;
+      if (stage == 0) key = ((uint64_t)r.id_ctr << 16) | (uint64_t)r.id_rank;
+      else if (stage == 1) key = r.kind ? ((1ull << 40) | (uint64_t)(r.k1 + (1ll << 39))) : (uint64_t)r.k1;
+      else key = ((uint64_t)(r.obj_ctr + 1) << 17) | (uint64_t)(r.obj_rank + 1);
+      if (stage == 0) v0[i] = i;
+      k0[i] = key;
+      atomicMax(&s_max, (unsigned long long)key);
+    }
+    __syncthreads();
+    const uint32_t bits = rs_bits(s_max);
+    __syncthreads();
+    block_radix_sort(k0, v0, k1, v1, n, bits);
+  }
+  for (uint32_t i = t; i < n; i += T) v1[i] = (uint32_t)sr[v0[i]].row;
+  __syncthreads();
+  for (uint32_t i = t; i < n; i += T) sr[i].row = (int32_t)v1[i];
+  __syncthreads();
+  return true;
+}
+
 __global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
                                                const am_doc_desc* __restrict__ docs, const am_known_hash* __restrict__ known,
                                                const ChunkInfo* __restrict__ info, const DocBounds* __restrict__ bounds,
@@ -1180,11 +1302,14 @@ __global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* _
     }
     __syncthreads();
     if (s.status) goto done;
-    block_bitonic_sort(idk, PR, [](const IdKey& a, const IdKey& b) {
-      if (a.ctr != b.ctr) return a.ctr < b.ctr;
-      if (a.actor != b.actor) return a.actor < b.actor;
-      return a.row < b.row;
-    });
+    bool idk_sorted = false;
+    if constexpr (!kHotLds) idk_sorted = radix_idk(s, idk, R);
+    if (!idk_sorted)
+      block_bitonic_sort(idk, PR, [](const IdKey& a, const IdKey& b) {
+        if (a.ctr != b.ctr) return a.ctr < b.ctr;
+        if (a.actor != b.actor) return a.actor < b.actor;
+        return a.row < b.row;
+      });
     // equal ids: mergeDocChangeOps compares ids only among the ops of one key / list element, so a
     // change op repeating the id of an op in the same key or element fails (new.js:1218-1221) and
     // repeats elsewhere are kept; insertions are placed before that comparison (new.js:1143)
@@ -1399,6 +1524,9 @@ __global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* _
     }
     for (uint32_t i = NOUT + t; i < PO; i += T) { SortRec k; k.row = -1; k.obj_ctr = INT64_MAX; k.obj_rank = 0; k.kind = 0; k.k1 = 0; k.key_off = 0; k.key_len = 0; k.id_ctr = 0; k.id_rank = 0; k.pad = 0; sr[i] = k; }
     __syncthreads();
+    bool sr_sorted = false;
+    if constexpr (!kHotLds) sr_sorted = radix_docorder(s, sr, NOUT, R, A);
+    if (!sr_sorted)
     block_bitonic_sort(sr, PO, [A](const SortRec& a, const SortRec& b) {
       if ((a.row < 0) != (b.row < 0)) return b.row < 0;
       if (a.row < 0) return false;

@@ -7,5 +7,5 @@ mkdir -p ../../tools/clock
 make -s
 /opt/rocm/bin/hipcc $F -DAM_PHASE_CLOCK -c am_kernels.hip -o /tmp/am_kernels_clock.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared -o ../../tools/clock/libam_clock.so /tmp/am_kernels_clock.o \
-  am_capi.o am_sync.o am_inflate.o am_history.o am_graph.o am_local.o am_sync_proto.o -lz -lpthread -lhsa-runtime64
+  am_capi.o am_sync.o am_inflate.o am_hist.o am_graph.o am_local.o am_sync_proto.o -lz -lpthread -lhsa-runtime64
 echo built tools/clock/libam_clock.so
