@@ -1003,6 +1003,99 @@ __device__ static bool radix_idk(DocShared& s, IdKey* idk, uint32_t R) {
   return true;
 }
 
+// P5f: list elements by (object, parent element, opId descending) -- the children of an element in
+// descending opId order (new.js:145-163). Three stable passes; the records are gathered through
+// the sortrec region (free until P5g) and copied back.
+__device__ static bool radix_elemk(DocShared& s, ElemKey* ek, uint32_t M, uint32_t R) {
+  __shared__ unsigned long long s_max;
+  __shared__ uint32_t s_bad;
+  const uint32_t t = threadIdx.x, T = blockDim.x;
+  uint64_t* k0 = hp<uint64_t>(s, s.L.tour_nxt);
+  uint64_t* k1 = k0 + M;
+  uint32_t* v0 = hp<uint32_t>(s, s.L.tour_w);
+  uint32_t* v1 = v0 + M;
+  ElemKey* tmp = hp<ElemKey>(s, s.L.sortrec);  // PR * 56 bytes >= M * 32
+  if (t == 0) s_bad = 0;
+  __syncthreads();
+  for (uint32_t i = t; i < M; i += T) {
+    const ElemKey& e = ek[i];
+    if (e.obj_ctr + 1 < 0 || e.obj_ctr + 1 >= (1ll << 46) || e.obj_rank + 1 < 0 || e.obj_rank + 1 >= 65536 || e.id_ctr < 0 ||
+        e.id_ctr >= (1ll << 46) || e.id_rank < 0 || e.id_rank >= 65536 || e.parent < -1 || e.parent >= (int32_t)R)
+      s_bad = 1;
+  }
+  __syncthreads();
+  const bool bad = s_bad != 0;
+  __syncthreads();
+  if (bad || M > R) return false;
+  for (int stage = 0; stage < 3; stage++) {
+    if (t == 0) s_max = 0;
+    __syncthreads();
+    for (uint32_t i = t; i < M; i += T) {
+      const ElemKey& e = ek[stage == 0 ? i : v0[i]];
+      uint64_t key;
+      if (stage == 0) key = (((1ull << 46) - 1 - (uint64_t)e.id_ctr) << 16) | (uint64_t)(65535 - e.id_rank);  // descending
+      else if (stage == 1) key = (uint64_t)(e.parent + 1);
+      else key = ((uint64_t)(e.obj_ctr + 1) << 17) | (uint64_t)(e.obj_rank + 1);
+      if (stage == 0) v0[i] = i;
+      k0[i] = key;
+      atomicMax(&s_max, (unsigned long long)key);
+    }
+    __syncthreads();
+    const uint32_t bits = rs_bits(s_max);
+    __syncthreads();
+    block_radix_sort(k0, v0, k1, v1, M, bits);
+  }
+  for (uint32_t i = t; i < M; i += T) tmp[i] = ek[v0[i]];
+  __syncthreads();
+  for (uint32_t i = t; i < M; i += T) ek[i] = tmp[i];
+  __syncthreads();
+  return true;
+}
+
+// P5h: the new succ entries by (target row, owner opId): two stable passes, records gathered through
+// the elemk region (dead after P5f)
+__device__ static bool radix_newent(DocShared& s, NewEnt* ne, uint32_t N, uint32_t R) {
+  __shared__ unsigned long long s_max;
+  __shared__ uint32_t s_bad;
+  const uint32_t t = threadIdx.x, T = blockDim.x;
+  if (N > R) return false;  // the scratch is sized by rows
+  uint64_t* k0 = hp<uint64_t>(s, s.L.tour_nxt);
+  uint64_t* k1 = k0 + N;
+  uint32_t* v0 = hp<uint32_t>(s, s.L.tour_w);
+  uint32_t* v1 = v0 + N;
+  NewEnt* tmp = hp<NewEnt>(s, s.L.elemk);  // PR * 32 bytes >= N * 24
+  if (t == 0) s_bad = 0;
+  __syncthreads();
+  for (uint32_t i = t; i < N; i += T) {
+    const NewEnt& e = ne[i];
+    if (e.ctr < 0 || e.ctr >= (1ll << 46) || e.rank < 0 || e.rank >= 65536 || e.target < 0 || e.target >= (int32_t)R) s_bad = 1;
+  }
+  __syncthreads();
+  const bool bad = s_bad != 0;
+  __syncthreads();
+  if (bad) return false;
+  for (int stage = 0; stage < 2; stage++) {
+    if (t == 0) s_max = 0;
+    __syncthreads();
+    for (uint32_t i = t; i < N; i += T) {
+      const NewEnt& e = ne[stage == 0 ? i : v0[i]];
+      const uint64_t key = stage == 0 ? (((uint64_t)e.ctr << 16) | (uint64_t)e.rank) : (uint64_t)e.target;
+      if (stage == 0) v0[i] = i;
+      k0[i] = key;
+      atomicMax(&s_max, (unsigned long long)key);
+    }
+    __syncthreads();
+    const uint32_t bits = rs_bits(s_max);
+    __syncthreads();
+    block_radix_sort(k0, v0, k1, v1, N, bits);
+  }
+  for (uint32_t i = t; i < N; i += T) tmp[i] = ne[v0[i]];
+  __syncthreads();
+  for (uint32_t i = t; i < N; i += T) ne[i] = tmp[i];
+  __syncthreads();
+  return true;
+}
+
 // P5g: object, then (map key in UTF-16 order | list position), then opId -- three stable passes,
 // least significant first. Map keys get dense ranks from a bitonic sort of the keyed records only
 // (few in list-heavy documents). Afterwards only sr[i].row is meaningful (all that later phases read).
@@ -1435,6 +1528,9 @@ __global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* _
       }
     for (uint32_t i = M + t; i < PM; i += T) { ElemKey k; k.obj_ctr = INT64_MAX; k.row = -1; k.obj_rank = 0; k.parent = 0; k.id_ctr = 0; k.id_rank = 0; ek[i] = k; }
     __syncthreads();
+    bool ek_sorted = false;
+    if constexpr (!kHotLds) ek_sorted = radix_elemk(s, ek, M, R);
+    if (!ek_sorted)
     block_bitonic_sort(ek, PM, [](const ElemKey& a, const ElemKey& b) {
       if (a.obj_ctr != b.obj_ctr) return a.obj_ctr < b.obj_ctr;
       if (a.obj_rank != b.obj_rank) return a.obj_rank < b.obj_rank;
@@ -1567,6 +1663,9 @@ __global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* _
       }
     }
     __syncthreads();
+    bool ne_sorted = false;
+    if constexpr (!kHotLds) ne_sorted = radix_newent(s, ne, NNEW, R);
+    if (!ne_sorted)
     block_bitonic_sort(ne, PN, [](const NewEnt& a, const NewEnt& b) {
       if (a.target != b.target) return a.target < b.target;
       if (a.ctr != b.ctr) return a.ctr < b.ctr;
