@@ -3,10 +3,11 @@ documents with 100k-op interleaved editing histories; --cross 0 --docs 1 --chang
 
 Each document is Backend.load(base) + Backend.applyChanges(rest): base = save() of the first half
 of the history (made by the engine in an untimed preparation launch), rest = the second half as
-compressed (type 2) change chunks, exactly as encodeChange writes them. Timed per step, inputs
-resident in HBM: the GPU pipeline (SHA-256 + parse, causal queue, decode, merge, re-encode,
-checksums) over all documents. The GPU DEFLATE inflate of the compressed changes runs in the batch
-stage and is reported separately (inflate_ms, inflate_GBps of inflated bytes). Documents 0 and 1
+compressed (type 2) change chunks, exactly as encodeChange writes them. `value` times the whole job
+from host memory per step: H2D of the chunks, the GPU DEFLATE inflate of the compressed changes and
+the GPU pipeline (SHA-256 + parse, causal queue, decode, merge, re-encode, checksums) over all
+documents; `kernel_resident_ops_per_s` repeats the pipeline alone on the staged inputs. Also
+reported: the k_doc time of one document's applyChanges patch (WANT_DIFF, 50k ops onto 50k). Documents 0 and 1
 are checked against the reference backend's own digests (tests/golden/text.json, c3full) when the
 configuration matches; the rest against the engine's own second run (determinism).
 
@@ -75,6 +76,14 @@ def main():
         for i, x in enumerate(b.stage_times()):
             stage_ms[i] += x
     elapsed = (time.perf_counter() - t0) / args.steps
+    # the whole job from host memory: H2D of the encoded chunks, the GPU inflate of the compressed
+    # changes and the pipeline, per step
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        b.stage(arena2, chunks2, docs2)
+        b.run()
+        b.sync()
+    elapsed_h2d = (time.perf_counter() - t0) / args.steps
     r = b.results()
     nerr = int((r["status"] != 0).sum())
     checked = []
@@ -85,6 +94,18 @@ def main():
             assert hashlib.sha256(bases[i]).hexdigest() == e["split"]["base"], "base %d differs from the reference" % i
             assert hashlib.sha256(b.doc_save(i)).hexdigest() == e["split"]["save"], "doc %d differs from the reference" % i
             checked.append(i)
+    # the applyChanges patch of one 100k-op document (Backend.applyChanges' return value, P8)
+    from automerge_amd.batch import WANT_DIFF
+    pb = Batch()
+    pb.stage(*pack([(bases[0], rest[0])], flags=WANT_DIFF))
+    pb.run()
+    pb.sync()
+    patch_ms = []
+    for _ in range(3):
+        pb.run()
+        pb.sync()
+        patch_ms.append(pb.stage_times()[2])
+    assert int(pb.results()["status"][0]) == 0, "patch run failed"
     cpu = None
     if args.cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -100,7 +121,10 @@ def main():
     line = {
         "workload": "C3 text histories: load(save(first half)) + applyChanges(second half, deflated chunks)",
         "docs": args.docs, "ops_per_doc": 1 + args.changes * args.per_change, "ops_applied": ops_applied,
-        "value": ops_applied / elapsed, "unit": "ops/s", "ms_per_step": elapsed * 1e3, "steps": k,
+        "value": ops_applied / elapsed_h2d, "unit": "ops/s", "ms_per_step": elapsed_h2d * 1e3, "steps": k,
+        "what": "H2D + GPU inflate + pipeline per step (inputs in host memory)",
+        "kernel_resident_ops_per_s": ops_applied / elapsed, "kernel_resident_ms_per_step": elapsed * 1e3,
+        "patch_100k_doc_k_doc_ms": min(patch_ms),
         "stage_ms": {"k_chunks": stage_ms[0] / k, "k_bounds+scan": stage_ms[1] / k, "k_doc": stage_ms[2] / k,
                      "k_out_hash": stage_ms[3] / k},
         "inflate": {"chunks": ninf, "ms": inf_ms, "inflated_arena_bytes": inf_bytes,
