@@ -621,15 +621,15 @@ __device__ __forceinline__ uint8_t* enc_put(uint8_t kind, uint8_t* o, int64_t v,
   return o + l;
 }
 
-// wave-level barrier: encode_column runs on wave 0 alone (the other waves of a global-mode
-// workgroup wait at the next __syncthreads)
+// wave-level barrier: encode_column runs on one wave (wave 0, or in a large document each wave on
+// a column of its own; the other waves wait at the next __syncthreads)
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   __builtin_amdgcn_wave_barrier();
 }
 // Encodes the n values of column c (V already filled) into out; returns the byte length.
 __device__ static uint32_t encode_column(uint8_t kind, uint32_t n, uint8_t* out, EncCtx& x, uint32_t* s_flag) {
-  const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x & 63;  // one wave
   if (n == 0) return 0;
   int64_t* X = x.V;
   if (kind == EK_D) {  // differences against the previous non-null value
@@ -1760,55 +1760,87 @@ __global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* _
     const uint64_t lo = s.b.span_lo;
     auto pk = [lo](uint64_t off, uint32_t len) -> int64_t { return (int64_t)((off - lo) << 32) | (int64_t)len; };
     auto act = [](int32_t a) -> int64_t { return a < 0 ? AM_NULL64 : (int64_t)a; };
-    for (int c = 0; c < OC_NCOLS + DC_NCOLS; c++) {
-      const uint32_t n = c < OC_GRP_ACTOR ? NOUT : c < OC_NCOLS ? NSUCC : c == OC_NCOLS + DC_DEPS_INDEX ? s.ndeps : NC;
-      for (uint32_t i = t; i < n; i += T) {
-        int64_t v = 0;
-        if (c < OC_GRP_NUM) {
-          const Row& r = rows[sr[i].row];
-          switch (c) {
-            case OC_OBJ_ACTOR: v = act(r.obj_actor); break;
-            case OC_OBJ_CTR: v = r.obj_ctr; break;
-            case OC_KEY_ACTOR: v = act(r.key_actor); break;
-            case OC_KEY_CTR: v = r.key_ctr; break;
-            case OC_KEY_STR: v = r.key_len == AM_NOSTR ? AM_NULL64 : pk(r.key_off, r.key_len); break;
-            case OC_ID_ACTOR: v = act(r.id_actor); break;
-            case OC_ID_CTR: v = r.id_ctr; break;
-            case OC_INSERT: v = r.insert; break;
-            case OC_ACTION: v = r.action; break;
-            case OC_VAL_LEN: v = r.val_len; break;
-            case OC_VAL_RAW: v = pk(r.val_off, r.val_len == AM_NULL64 ? 0u : (uint32_t)((uint64_t)r.val_len >> 4)); break;
-            case OC_CHLD_ACTOR: v = act(r.chld_actor); break;
-            default: v = r.chld_ctr; break;
-          }
-        } else if (c == OC_GRP_NUM) {
-          v = (int64_t)(i + 1 < NOUT ? succ_cnt[i + 1] : NSUCC) - succ_cnt[i];
-        } else if (c == OC_GRP_ACTOR) {
-          v = act(outent[i].actor);
-        } else if (c == OC_GRP_CTR) {
-          v = outent[i].ctr;
-        } else {
-          const ChgRow& g = chg[i < NC ? i : 0];
-          switch (c - OC_NCOLS) {
-            case DC_ACTOR: v = g.actor; break;
-            case DC_SEQ: v = g.seq; break;
-            case DC_MAXOP: v = g.max_op; break;
-            case DC_TIME: v = g.time; break;
-            case DC_MESSAGE: v = g.msg_len == AM_NOSTR ? AM_NULL64 : pk(g.msg_off, g.msg_len); break;
-            case DC_DEPS_NUM: v = (int64_t)g.ndeps; break;
-            case DC_DEPS_INDEX: v = depsv[i]; break;
-            case DC_EXTRA_LEN: v = g.extra_len; break;
-            default: v = pk(g.extra_off, g.extra_raw_len); break;
-          }
+    // the value of column c at position i
+    auto colval = [&](int c, uint32_t i) -> int64_t {
+      int64_t v = 0;
+      if (c < OC_GRP_NUM) {
+        const Row& r = rows[sr[i].row];
+        switch (c) {
+          case OC_OBJ_ACTOR: v = act(r.obj_actor); break;
+          case OC_OBJ_CTR: v = r.obj_ctr; break;
+          case OC_KEY_ACTOR: v = act(r.key_actor); break;
+          case OC_KEY_CTR: v = r.key_ctr; break;
+          case OC_KEY_STR: v = r.key_len == AM_NOSTR ? AM_NULL64 : pk(r.key_off, r.key_len); break;
+          case OC_ID_ACTOR: v = act(r.id_actor); break;
+          case OC_ID_CTR: v = r.id_ctr; break;
+          case OC_INSERT: v = r.insert; break;
+          case OC_ACTION: v = r.action; break;
+          case OC_VAL_LEN: v = r.val_len; break;
+          case OC_VAL_RAW: v = pk(r.val_off, r.val_len == AM_NULL64 ? 0u : (uint32_t)((uint64_t)r.val_len >> 4)); break;
+          case OC_CHLD_ACTOR: v = act(r.chld_actor); break;
+          default: v = r.chld_ctr; break;
         }
-        ex.V[i] = v;
+      } else if (c == OC_GRP_NUM) {
+        v = (int64_t)(i + 1 < NOUT ? succ_cnt[i + 1] : NSUCC) - succ_cnt[i];
+      } else if (c == OC_GRP_ACTOR) {
+        v = act(outent[i].actor);
+      } else if (c == OC_GRP_CTR) {
+        v = outent[i].ctr;
+      } else {
+        const ChgRow& g = chg[i < NC ? i : 0];
+        switch (c - OC_NCOLS) {
+          case DC_ACTOR: v = g.actor; break;
+          case DC_SEQ: v = g.seq; break;
+          case DC_MAXOP: v = g.max_op; break;
+          case DC_TIME: v = g.time; break;
+          case DC_MESSAGE: v = g.msg_len == AM_NOSTR ? AM_NULL64 : pk(g.msg_off, g.msg_len); break;
+          case DC_DEPS_NUM: v = (int64_t)g.ndeps; break;
+          case DC_DEPS_INDEX: v = depsv[i]; break;
+          case DC_EXTRA_LEN: v = g.extra_len; break;
+          default: v = pk(g.extra_off, g.extra_raw_len); break;
+        }
       }
-      __syncthreads();
-      if (t < 64) {
-        const uint32_t len = encode_column(kEncKind[c], n, wsg + L.colbuf[c], ex, nullptr);
-        if (t == 0) s.col_len[c] = len;
+      return v;
+    };
+    auto coln = [&](int c) -> uint32_t {
+      return c < OC_GRP_ACTOR ? NOUT : c < OC_NCOLS ? NSUCC : c == OC_NCOLS + DC_DEPS_INDEX ? s.ndeps : NC;
+    };
+    // a large document in global mode: each wave encodes a column of its own (waves 1..3 with the
+    // scratch at L.enc_x), four columns at a time
+    const uint32_t NW = (kDocT > 64 && L.enc_x) ? kDocT / 64 : 1u;
+    if (NW > 1) {
+      const uint32_t wv = t >> 6, ln = t & 63;
+      EncCtx exw = ex;
+      if (wv > 0) {
+        exw.V = reinterpret_cast<int64_t*>(wsg + L.enc_x + (uint64_t)(wv - 1) * 32 * L.enc_n);
+        exw.W = exw.V + L.enc_n;
+        exw.S = reinterpret_cast<uint32_t*>(exw.W + L.enc_n);
+        exw.RS = exw.S + L.enc_n;
+        exw.RB = exw.RS + L.enc_n;
+        exw.RG = exw.RB + L.enc_n;
       }
-      __syncthreads();
+      for (int c0 = 0; c0 < OC_NCOLS + DC_NCOLS; c0 += (int)NW) {
+        const int c = c0 + (int)wv;
+        if (c < OC_NCOLS + DC_NCOLS) {
+          const uint32_t n = coln(c);
+          for (uint32_t i = ln; i < n; i += 64) exw.V[i] = colval(c, i);
+          wave_sync();
+          const uint32_t len = encode_column(kEncKind[c], n, wsg + L.colbuf[c], exw, nullptr);
+          if (ln == 0) s.col_len[c] = len;
+        }
+        __syncthreads();
+      }
+    } else {
+      for (int c = 0; c < OC_NCOLS + DC_NCOLS; c++) {
+        const uint32_t n = coln(c);
+        for (uint32_t i = t; i < n; i += T) ex.V[i] = colval(c, i);
+        __syncthreads();
+        if (t < 64) {
+          const uint32_t len = encode_column(kEncKind[c], n, wsg + L.colbuf[c], ex, nullptr);
+          if (t == 0) s.col_len[c] = len;
+        }
+        __syncthreads();
+      }
     }
     __syncthreads();
     if (s.b.UC) unk_encode(s, sr, NOUT, ex, wsg);

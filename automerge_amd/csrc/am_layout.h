@@ -59,6 +59,7 @@ struct WsLayout {
   uint64_t patch, patch_nrec, patch_nmval, patch_heap;  // patch log, working form (when P)
   uint64_t pwire, pwire_cap;  // the same log in wire form (PatchHdr2 + stream, am_patch.h)
   uint64_t etime, passend, dscr;  // applyChanges patch (P == 2): succ-entry times, pass ends, replay pools
+  uint64_t enc_x;             // encode scratch of waves 1..3 of a large document (0: wave 0 encodes alone)
   uint64_t colbuf[OC_NCOLS + DC_NCOLS];
   // unknown op columns (UC > 0): instance table, decoded values, per-(source, column) instance
   // map, the output columns' ids / lengths / positions, per-row group offsets, encoded output
@@ -207,6 +208,8 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   } else {
     L.etime = L.passend = L.dscr = 0;
   }
+  // large documents: waves 1..3 of the global-mode workgroup encode columns of their own (P6)
+  L.enc_x = nm >= 1024 ? take(3 * 32 * nm) : 0;
   if (UC) {
     L.unk_inst = take(UC * AM_SZ_UNKINST);
     L.unk_cells = take(((uint64_t)b.UV + 2 * R + 2) * 8);
