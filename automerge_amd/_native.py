@@ -275,12 +275,11 @@ def document_changes_batch(docs, device=0, stats=None):
         if h.err.code:
             res.append(error_for(h.err))
             continue
-        out = []
-        for i in range(h.nchanges):
-            a, b = h.offs[i], h.offs[i + 1]
-            out.append((C.string_at(C.addressof(h.changes.contents) + a, b - a) if b > a else b"",
-                        C.string_at(C.addressof(h.hashes32.contents) + 32 * i, 32).hex()))
-        res.append(out)
+        nc = h.nchanges
+        offs = h.offs[:nc + 1]  # one copy of each buffer, then slices
+        buf = C.string_at(h.changes, offs[-1]) if nc and offs[-1] else b""
+        hx = C.string_at(h.hashes32, 32 * nc).hex() if nc else ""
+        res.append([(buf[offs[i]:offs[i + 1]], hx[64 * i:64 * i + 64]) for i in range(nc)])
         for p in (h.changes, h.offs, h.hashes32):
             lib.am_free(p)
     return res
