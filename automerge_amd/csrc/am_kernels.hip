@@ -261,7 +261,7 @@ __device__ __noinline__ static uint64_t unknown_bound(const uint8_t* data, uint6
 // Per chunk: container header, SHA-256 (hash + checksum), change/document header parse into the
 // compact slot, row/entry/string counts. `p` is the chunk start: a staged LDS copy or the arena.
 __device__ __forceinline__ void chunk_body(const uint8_t* p, const am_chunk_desc cd, uint32_t i, ChunkInfo* __restrict__ info,
-                                           HdrSlot* __restrict__ hdr) {
+                                           HdrSlot* __restrict__ hdr, bool defer_counts, uint32_t* dcols) {
   ChunkInfo ci;
   uint32_t* hw = reinterpret_cast<uint32_t*>(ci.hash);
 #pragma unroll
@@ -283,13 +283,18 @@ __device__ __forceinline__ void chunk_body(const uint8_t* p, const am_chunk_desc
     if ((st = rd_raw(r, (uint64_t)len, at))) break;
     ci.data_off = (uint32_t)at;
     ci.data_len = (uint32_t)len;
-    uint32_t h[8];
-    sha256_words(p + 8, r.off - 8, h);
+    // SHA-256: a change's hash, or a document's checksum -- unless the host stage has verified the
+    // document already (its columns were inflated, am_stage_document): a document has no hash of
+    // its own, so a verified one skips the single-lane pass over all its bytes
+    if (!(ci.type == 0 && (cd.flags & 1))) {
+      uint32_t h[8];
+      sha256_words(p + 8, r.off - 8, h);
 #pragma unroll
-    for (int k = 0; k < 8; k++) hw[k] = __builtin_bswap32(h[k]);
-    if (!(cd.flags & 1) && ((uint32_t)p[4] << 24 | (uint32_t)p[5] << 16 | (uint32_t)p[6] << 8 | p[7]) != h[0]) {
-      st = AM_E_CHECKSUM;
-      break;
+      for (int k = 0; k < 8; k++) hw[k] = __builtin_bswap32(h[k]);
+      if (!(cd.flags & 1) && ((uint32_t)p[4] << 24 | (uint32_t)p[5] << 16 | (uint32_t)p[6] << 8 | p[7]) != h[0]) {
+        st = AM_E_CHECKSUM;
+        break;
+      }
     }
     const uint8_t* data = p + at;
     if (ci.type == 1) {
@@ -336,6 +341,18 @@ __device__ __forceinline__ void chunk_body(const uint8_t* p, const am_chunk_desc
       }
       ci.nactors = dh.nactors;
       ci.nheads = dh.nheads;
+      ci.nunk = dh.nunk;
+      if (defer_counts) {  // a large document: the wave counts its columns together (k_chunks)
+        const uint8_t kc[6] = {(uint8_t)DC_ACTOR, (uint8_t)DC_DEPS_NUM, (uint8_t)(OC_NCOLS + OC_ID_CTR), (uint8_t)(OC_NCOLS + OC_GRP_NUM),
+                               (uint8_t)(OC_NCOLS + OC_KEY_STR), (uint8_t)DC_MESSAGE};
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+          const uint32_t c = kc[k];
+          dcols[2 * k] = (uint32_t)at + (c < OC_NCOLS ? dh.ccol_off[c] : dh.ocol_off[c - OC_NCOLS]);
+          dcols[2 * k + 1] = c < OC_NCOLS ? dh.ccol_len[c] : dh.ocol_len[c - OC_NCOLS];
+        }
+        break;
+      }
       uint64_t cnt, sum;
       if ((st = rle_count_sum_i(data + dh.ccol_off[DC_ACTOR], dh.ccol_len[DC_ACTOR], false, cnt, sum, 0))) break;
       ci.nchg = (uint32_t)cnt;
@@ -361,6 +378,156 @@ __device__ __forceinline__ void chunk_body(const uint8_t* p, const am_chunk_desc
 }
 
 #define KC_STAGE 12288  // bytes of LDS per wave for its 64 chunks
+#define KC_BIG 16384     // a document chunk this large has its columns counted by the whole wave
+
+// ---- wave-cooperative counting of a large document's columns: every lane runs the same parse
+// over a window of the chunk in the wave's LDS slice, refilled with 16-byte loads of all 64 lanes
+// when the parse leaves it, so the long dependent chain of LEB128 reads hits LDS instead of global
+// memory. Same results and status codes as rle_count_sum (the LEB readers mirror leb_u64 /
+// leb_i64 / rd_u53 / rd_i53). ----
+#define KC_WIN 8192
+struct WinRd {
+  const uint8_t* g;  // chunk start (global)
+  uint8_t* win;      // the wave's LDS window
+  uint64_t lim;      // readable bytes from g (chunk length)
+  uint64_t wb;       // window start (offset from g); ~0: empty
+};
+__device__ __forceinline__ uint8_t win_byte(WinRd& w, uint64_t k) {
+  if (k < w.wb || k >= w.wb + KC_WIN) {  // wave-uniform: every lane parses the same bytes
+    const uint64_t nb = k & ~(uint64_t)15;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t l = threadIdx.x & 63;
+    for (uint32_t q = 16 * l; q < KC_WIN; q += 1024) {
+      if (nb + q < w.lim) {
+        // 16 B per lane; the arena carries >= 16 bytes of slack past its last chunk
+        const uint8_t* src = w.g + nb + q;
+        uint32_t v[4];
+        for (int b = 0; b < 4; b++) v[b] = (uint32_t)src[4 * b] | (uint32_t)src[4 * b + 1] << 8 | (uint32_t)src[4 * b + 2] << 16 | (uint32_t)src[4 * b + 3] << 24;
+        uint32_t* d = reinterpret_cast<uint32_t*>(w.win + q);
+        d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    w.wb = nb;
+  }
+  return w.win[k - w.wb];
+}
+struct WinCur { uint64_t off, n; };  // a column: [off, off + n) of the chunk
+__device__ static uint32_t win_leb_u64(WinRd& w, WinCur& d, uint32_t& hi, uint32_t& lo) {
+  uint32_t low = 0, high = 0;
+  int shift = 0;
+  while (d.off < d.n && shift <= 28) {
+    const uint8_t b = win_byte(w, d.off);
+    low |= (uint32_t)(b & 0x7f) << shift;
+    if (shift == 28) high = (b & 0x70) >> 4;
+    shift += 7;
+    d.off++;
+    if (!(b & 0x80)) { hi = high; lo = low; return AM_OK; }
+  }
+  shift = 3;
+  while (d.off < d.n) {
+    const uint8_t b = win_byte(w, d.off);
+    if (shift == 31 && (b & 0xfe) != 0) return AM_E_LEB_RANGE;
+    high |= (uint32_t)(b & 0x7f) << shift;
+    shift += 7;
+    d.off++;
+    if (!(b & 0x80)) { hi = high; lo = low; return AM_OK; }
+  }
+  return AM_E_LEB_INCOMPLETE;
+}
+__device__ static uint32_t win_leb_i64(WinRd& w, WinCur& d, int32_t& hi, uint32_t& lo) {
+  uint32_t low = 0;
+  int32_t high = 0;
+  int shift = 0;
+  while (d.off < d.n && shift <= 28) {
+    const uint8_t b = win_byte(w, d.off);
+    low |= (uint32_t)(b & 0x7f) << shift;
+    if (shift == 28) high = (b & 0x70) >> 4;
+    shift += 7;
+    d.off++;
+    if (!(b & 0x80)) {
+      if (b & 0x40) {
+        if (shift < 32) low |= 0xffffffffu << shift;
+        const int s2 = shift - 32 > 0 ? shift - 32 : 0;
+        high |= (int32_t)(0xffffffffu << s2);
+      }
+      hi = high; lo = low;
+      return AM_OK;
+    }
+  }
+  shift = 3;
+  while (d.off < d.n) {
+    const uint8_t b = win_byte(w, d.off);
+    if (shift == 31 && b != 0 && b != 0x7f) return AM_E_LEB_RANGE;
+    high |= (int32_t)((uint32_t)(b & 0x7f) << shift);
+    shift += 7;
+    d.off++;
+    if (!(b & 0x80)) {
+      if ((b & 0x40) && shift < 32) high |= (int32_t)(0xffffffffu << shift);
+      hi = high; lo = low;
+      return AM_OK;
+    }
+  }
+  return AM_E_LEB_INCOMPLETE;
+}
+__device__ __forceinline__ uint32_t win_u53(WinRd& w, WinCur& d, int64_t& v) {
+  uint32_t hi, lo;
+  TRY(win_leb_u64(w, d, hi, lo));
+  if (hi > 0x1fffff) return AM_E_LEB_RANGE;
+  v = (int64_t)hi * 4294967296LL + lo;
+  return AM_OK;
+}
+__device__ __forceinline__ uint32_t win_i53(WinRd& w, WinCur& d, int64_t& v) {
+  int32_t hi;
+  uint32_t lo;
+  TRY(win_leb_i64(w, d, hi, lo));
+  if (hi < -0x200000 || (hi == -0x200000 && lo == 0) || hi > 0x1fffff) return AM_E_LEB_RANGE;
+  v = (int64_t)hi * 4294967296LL + lo;
+  return AM_OK;
+}
+// rle_count_sum over the window (same record rules, same errors)
+__device__ __forceinline__ uint32_t win_count_sum(WinRd& w, uint64_t off, uint64_t n, bool is_str, bool is_signed, uint64_t& count, uint64_t& sum) {
+  WinCur d{off, off + n};
+  count = 0;
+  sum = 0;
+  while (d.off < d.n) {
+    int64_t c;
+    TRY(win_i53(w, d, c));
+    if (c > 0) {
+      int64_t v;
+      if (is_str) {
+        TRY(win_u53(w, d, v));
+        if (d.off + (uint64_t)v > d.n) return AM_E_SUBARRAY;
+        d.off += (uint64_t)v;
+      } else if (is_signed) {
+        TRY(win_i53(w, d, v));
+        v = 0;
+      } else {
+        TRY(win_u53(w, d, v));
+      }
+      count += (uint64_t)c;
+      sum += (uint64_t)c * (uint64_t)v;
+    } else if (c < 0) {
+      for (int64_t i = 0; i < -c; i++) {
+        int64_t v;
+        if (is_signed) { TRY(win_i53(w, d, v)); v = 0; } else { TRY(win_u53(w, d, v)); }
+        if (is_str) {
+          if (d.off + (uint64_t)v > d.n) return AM_E_SUBARRAY;
+          d.off += (uint64_t)v;
+        }
+        sum += (uint64_t)v;
+      }
+      count += (uint64_t)(-c);
+    } else {
+      int64_t z;
+      TRY(win_u53(w, d, z));
+      count += (uint64_t)z;
+    }
+  }
+  return AM_OK;
+}
 // k_chunks: thread per chunk. Each wave first stages the byte span of its 64 chunks (adjacent in
 // the arena for staged batches) into LDS with 16-byte loads, so the SHA-256 rounds and the
 // dependent LEB128 reads of the header parse hit LDS; a wave whose span does not fit reads the
@@ -392,9 +559,57 @@ __global__ void __launch_bounds__(256) k_chunks(const uint8_t* __restrict__ aren
     for (uint32_t v = l; v < nv; v += 64) dst[v] = src[v];
   }
   __syncthreads();
-  if (!valid) return;
-  if (staged) chunk_body(stage[w] + (cd.off - lo16), cd, i, info, hdr);
-  else chunk_body(arena + cd.off, cd, i, info, hdr);
+  // a large document: counted by the whole wave over an LDS window when the wave holds at most two
+  // (one at a time, each ~3x faster than one lane's chain over global memory); a wave of many large
+  // documents keeps one lane per document, their chains overlapping
+  const bool large = valid && cd.len > KC_BIG && arena[cd.off + 8] == 0;
+  const bool defer = large && __popcll(__ballot(large)) <= 2;
+  uint32_t dcols[12];
+#pragma unroll
+  for (int k = 0; k < 12; k++) dcols[k] = 0;
+  if (valid) {
+    if (staged) chunk_body(stage[w] + (cd.off - lo16), cd, i, info, hdr, false, dcols);
+    else chunk_body(arena + cd.off, cd, i, info, hdr, defer, dcols);
+  }
+  // the large documents of this wave, one at a time, counted by all 64 lanes over an LDS window
+  // (their chunk_body stopped before the counts when its header parse succeeded)
+  uint64_t big = __ballot(defer && dcols[1] + dcols[3] + dcols[5] + dcols[7] + dcols[9] + dcols[11] + dcols[0] > 0);
+  while (big) {
+    const int j = __builtin_ctzll(big);
+    big &= big - 1;
+    const uint64_t goff = __shfl(cd.off, j, 64);
+    const uint64_t glen = __shfl((uint64_t)cd.len, j, 64);
+    const uint32_t o0 = __shfl(dcols[0], j, 64), n0 = __shfl(dcols[1], j, 64), o1 = __shfl(dcols[2], j, 64), n1 = __shfl(dcols[3], j, 64);
+    const uint32_t o2 = __shfl(dcols[4], j, 64), n2 = __shfl(dcols[5], j, 64), o3 = __shfl(dcols[6], j, 64), n3 = __shfl(dcols[7], j, 64);
+    const uint32_t o4 = __shfl(dcols[8], j, 64), n4 = __shfl(dcols[9], j, 64), o5 = __shfl(dcols[10], j, 64), n5 = __shfl(dcols[11], j, 64);
+    WinRd wr{arena + goff, stage[w], glen, ~0ull};
+    uint64_t nchg = 0, ndeps = 0, nops = 0, nents = 0, sbytes = 0;
+    uint32_t st = AM_OK;
+#pragma unroll 1
+    for (int k = 0; k < 6 && !st; k++) {
+      const uint32_t o = k == 0 ? o0 : k == 1 ? o1 : k == 2 ? o2 : k == 3 ? o3 : k == 4 ? o4 : o5;
+      const uint32_t n = k == 0 ? n0 : k == 1 ? n1 : k == 2 ? n2 : k == 3 ? n3 : k == 4 ? n4 : n5;
+      uint64_t c, sm;
+      st = win_count_sum(wr, o, n, k >= 4, k == 2, c, sm);
+      if (k == 0) nchg = c;
+      else if (k == 1) ndeps = sm;
+      else if (k == 2) nops = c;
+      else if (k == 3) nents = sm;
+      else sbytes += sm;
+    }
+    if ((int)l == j) {
+      ChunkInfo& ci = info[i];
+      if (st) {
+        ci.status = st;
+      } else {
+        ci.nchg = (uint32_t)nchg;
+        ci.ndeps = (uint32_t)ndeps;
+        ci.nops = (uint32_t)nops;
+        ci.nents = (uint32_t)nents;
+        ci.strbytes = (uint32_t)sbytes;
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
