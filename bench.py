@@ -287,7 +287,11 @@ def main():
         for i in range(min(args.check, D)):
             base, changes = workload.doc_chunks(arena, chunks, docs, i)
             ref = O.Doc.load(base) if base else O.Doc.init()
-            want = ref.apply_patch(changes) if not args.no_patch else None
+            if args.no_patch:
+                ref.apply(changes)  # apply_patch applies the changes too; without a patch apply them here
+                want = None
+            else:
+                want = ref.apply_patch(changes)
             got, log = check(i)
             assert got == ref.save(), "document %d differs from the oracle" % i
             if log is not None:
