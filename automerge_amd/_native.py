@@ -27,7 +27,7 @@ class ChunkDesc(C.Structure):
 class DocDesc(C.Structure):
     _fields_ = [("base_chunk", C.c_int64), ("chg_begin", C.c_uint32), ("chg_count", C.c_uint32),
                 ("known_begin", C.c_uint32), ("known_count", C.c_uint32), ("flags", C.c_uint32),
-                ("pad", C.c_uint32)]
+                ("meta_chunk", C.c_uint32)]
 
 
 class KnownHash(C.Structure):

@@ -9,7 +9,7 @@ from . import _native as N
 
 CHUNK_DT = np.dtype([("off", "<u8"), ("len", "<u4"), ("flags", "<u4")])
 DOC_DT = np.dtype([("base_chunk", "<i8"), ("chg_begin", "<u4"), ("chg_count", "<u4"), ("known_begin", "<u4"),
-                   ("known_count", "<u4"), ("flags", "<u4"), ("pad", "<u4")])
+                   ("known_count", "<u4"), ("flags", "<u4"), ("meta_chunk", "<u4")])
 RESULT_DT = np.dtype([("status", "<u4"), ("err_change", "<u4"), ("arg0", "<i8"), ("arg1", "<i8"),
                       ("arg_actor_off", "<u8"), ("arg_actor_len", "<u4"), ("napplied", "<u4"), ("nqueued", "<u4"),
                       ("nheads", "<u4"), ("nops", "<u4"), ("nchanges", "<u4"), ("max_op", "<i8"),

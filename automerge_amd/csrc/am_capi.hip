@@ -380,7 +380,7 @@ static bool inflate_stage(am_batch* b, const uint8_t* arena, uint64_t arena_len,
   std::vector<uint32_t> zidx;
   for (uint32_t c = 0; c < nchunks; c++) {
     const am_chunk_desc& k = chunks[c];
-    if (!is_base[c] && k.len > 9 && k.off + k.len <= arena_len && arena[k.off + 8] == 2 &&
+    if (!is_base[c] && !(k.flags & AM_CHUNK_RAW) && k.len > 9 && k.off + k.len <= arena_len && arena[k.off + 8] == 2 &&
         std::memcmp(arena + k.off, "\x85\x6f\x4a\x83", 4) == 0)
       zidx.push_back(c);
   }
@@ -575,8 +575,9 @@ extern "C" int am_batch_doc_patch(am_batch* b, uint32_t doc, uint8_t* dst, uint6
   const uint8_t* base = b->ws.p + r.ws_off + L.pwire;
   PatchHdr2 h;
   if (hipMemcpy(&h, base, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-  if (h.magic != AM_PATCH_MAGIC || sizeof h + h.nbytes > L.pwire_cap) return 1;
-  const uint64_t total = sizeof h + h.nbytes;
+  // AM_DOC_META: the objectMeta blob follows the stream (PatchHdr2.meta_bytes)
+  if (h.magic != AM_PATCH_MAGIC || sizeof h + h.nbytes + h.meta_bytes > L.pwire_cap) return 1;
+  const uint64_t total = sizeof h + h.nbytes + h.meta_bytes;
   *len = total;
   if (cap == 0) return 0;
   if (cap < total) return 2;
@@ -1010,6 +1011,10 @@ struct am_doc {
   std::vector<std::array<uint8_t, 32>> heads;
   std::vector<std::array<uint8_t, 32>> load_heads;     // changeIndexByHash of a loaded document without its graph
   HashGraph graph;                                     // over changes[0, graph.size()) (am_graph.h)
+  // objectMeta's children snapshots as this handle's last applyChanges left them (am_diff.h
+  // diff_meta_pack; new.js:1812, 1857); empty: documentPatch's of the state (load / init)
+  std::vector<uint8_t> meta;
+  bool meta_lost = false;  // a patchless call could not follow objectMeta (a PATCH_U_* input)
   int64_t max_op = 0;
   size_t nchanges = 0;
 };
@@ -1053,12 +1058,15 @@ struct OneResult {
   std::vector<std::array<uint8_t, 32>> hashes;
   std::vector<std::array<uint8_t, 32>> heads;
   std::vector<uint8_t> patch;  // patch log (patch_mode: 1 getPatch, 2 the applyChanges patch)
+  std::vector<uint8_t> meta;   // AM_DOC_META: the objectMeta blob the call leaves
 };
 
 // Runs one document (optional base chunk + change list) through the GPU pipeline.
+// With `meta` (patch_mode 2): the handle's objectMeta snapshots go in (empty: documentPatch's) and
+// res.meta receives what the call leaves.
 bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified, const std::vector<std::vector<uint8_t>>& chg,
              const std::vector<am_known_hash>& known, bool have_graph, OneResult& res, std::vector<uint8_t>& arena, Err& err,
-             int patch_mode = 0, uint32_t extra_flags = 0) {
+             int patch_mode = 0, uint32_t extra_flags = 0, const std::vector<uint8_t>* meta = nullptr) {
   arena.clear();
   std::vector<am_chunk_desc> cds;
   am_doc_desc dd{};
@@ -1078,6 +1086,15 @@ bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified,
   dd.known_count = (uint32_t)known.size();
   dd.flags = (have_graph ? 1u : 0u) | (patch_mode == 1 ? AM_DOC_WANT_PATCH : 0u) | (patch_mode == 2 ? AM_DOC_WANT_DIFF : 0u) |
              extra_flags;
+  dd.meta_chunk = 0;
+  if (meta && patch_mode == 2) {
+    dd.flags |= AM_DOC_META;
+    if (!meta->empty()) {
+      dd.meta_chunk = (uint32_t)cds.size() + 1;
+      cds.push_back({arena.size(), (uint32_t)meta->size(), AM_CHUNK_RAW});
+      arena.insert(arena.end(), meta->begin(), meta->end());
+    }
+  }
   am_batch* b = scratch_batch(e);
   am_error ce;
   for (;;) {
@@ -1128,6 +1145,18 @@ bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified,
     if (am_batch_doc_patch(b, 0, res.patch.data(), plen, &plen)) {
       err = {AM_U_CAPACITY, false, "automerge_amd: patch copy failed"};
       return false;
+    }
+    // the objectMeta blob after the stream goes to res.meta; the log keeps header + stream
+    res.meta.clear();
+    if (res.patch.size() >= sizeof(PatchHdr2)) {
+      PatchHdr2 h;
+      std::memcpy(&h, res.patch.data(), sizeof h);
+      if (h.meta_bytes && sizeof h + h.nbytes + h.meta_bytes == res.patch.size()) {
+        res.meta.assign(res.patch.begin() + sizeof h + h.nbytes, res.patch.end());
+        res.patch.resize(sizeof h + h.nbytes);
+        h.meta_bytes = 0;
+        std::memcpy(res.patch.data(), &h, sizeof h);
+      }
     }
   }
   return true;
@@ -1313,6 +1342,20 @@ static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* le
   for (size_t i = 0; i < n; i++) orig.emplace_back(bufs[i], bufs[i] + lens[i]);
   for (auto& q : d->queue) orig.push_back(q);
   const std::vector<std::vector<uint8_t>>& staged = orig;
+  // objectMeta moves on in every call, with or without a patch: loadChanges runs the same
+  // BackendDoc.applyChanges (backend.js:116-121), whose updatePatchProperty calls refresh the
+  // children snapshots and raise its errors. So every call replays the patch (P8) with the
+  // handle's snapshots; loadChanges only drops the log.
+  if (patch && d->meta_lost) {
+    to_c(Err{AM_U_VALUE, false,
+             "automerge_amd: unsupported: this handle's objectMeta was not followed through an earlier "
+             "loadChanges whose patch shape the engine does not restate"},
+         err);
+    return 1;
+  }
+  const bool track = !d->meta_lost;
+  const int pmode = track ? 2 : 0;
+  const std::vector<uint8_t>* meta = track ? &d->meta : nullptr;
   std::vector<am_known_hash> known;
   auto fill_known = [&]() {
     known.clear();
@@ -1327,33 +1370,40 @@ static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* le
   fill_known();
   OneResult res;
   std::vector<uint8_t> arena;
-  if (!run_one(d->eng, d->state.empty() ? nullptr : &d->state, false, staged, known, d->have_hash_graph, res, arena, e,
-               patch ? 2 : 0)) {
+  if (!run_one(d->eng, d->state.empty() ? nullptr : &d->state, false, staged, known, d->have_hash_graph, res, arena, e, pmode,
+               0, meta)) {
     // a loaded document without its hash graph: compute it and run again (new.js:1826-1832)
     if (e.code != AM_U_HASH_GRAPH || d->have_hash_graph) { to_c(e, err); return 1; }
     if (am_doc_compute_hash_graph(d, err)) return 1;
     fill_known();
     e = Err{};
-    if (!run_one(d->eng, &d->state, false, staged, known, true, res, arena, e, patch ? 2 : 0)) {
+    if (!run_one(d->eng, &d->state, false, staged, known, true, res, arena, e, pmode, 0, meta)) {
       to_c(e, err);
       return 1;
     }
   }
   // a patch larger than the pools sized from the row counts: run again with 8x pools (the engine's
   // limit, not a reference error; the reference would return the patch)
-  if (patch && res.patch.size() >= sizeof(PatchHdr2)) {
+  if (track && res.patch.size() >= sizeof(PatchHdr2)) {
     PatchHdr2 ph;
     std::memcpy(&ph, res.patch.data(), sizeof ph);
     if (ph.status == AM_U_CAPACITY && !run_one(d->eng, d->state.empty() ? nullptr : &d->state, false, staged, known,
-                                               d->have_hash_graph, res, arena, e, 2, AM_DOC_PATCH_ROOM)) {
+                                               d->have_hash_graph, res, arena, e, 2, AM_DOC_PATCH_ROOM, meta)) {
       to_c(e, err);
       return 1;
     }
   }
-  // the patch is part of the call: an error in it throws before the document changes (new.js:1838)
-  if (patch) {
-    if (patch_log_error(res.patch, e)) { to_c(e, err); return 1; }
-    patch->swap(res.patch);
+  // the patch is part of the call: an error in it throws before the document changes (new.js:1838);
+  // loadChanges throws the reference's errors too, and only loses objectMeta on an input the patch
+  // replay does not restate (AM_U_*)
+  bool lost = false;
+  if (track) {
+    Err pe;
+    if (patch_log_error(res.patch, pe)) {
+      if (patch || pe.code < AM_U_HASH_GRAPH) { to_c(pe, err); return 1; }
+      lost = true;
+    }
+    if (patch) patch->swap(res.patch);
   }
   // commit (new.js:1838-1860)
   const size_t base = d->state.empty() ? 0 : 1;
@@ -1377,6 +1427,11 @@ static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* le
   d->binary.clear();
   d->nchanges = res.r.nchanges;
   if (res.r.max_op > d->max_op) d->max_op = res.r.max_op;
+  if (track) {
+    d->meta_lost = lost;
+    if (lost) d->meta.clear();
+    else d->meta = std::move(res.meta);
+  }
   if (err) err->code = 0;
   return 0;
 }

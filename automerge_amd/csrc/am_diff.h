@@ -1154,10 +1154,88 @@ struct Diff {
     return true;
   }
 
+  // ---- objectMeta carried across calls on one handle (new.js:1812, 1857) ----
+  // The reference keeps objectMeta per BackendDoc: documentPatch fills it at load (new.js:1748),
+  // then every applyChanges call updates the children snapshots of the keys its
+  // updatePatchProperty calls visit. A handle that has run a call hands its snapshots back in
+  // (meta_restore); the objects themselves (parent, parentKey, type) follow from the make ops.
+  AM_PHD bool build_objects() {
+    if (obj_new(-1, -1, 0) < 0) return false;
+    for (uint32_t i = 0; i < s.nb(); i++) {
+      const int32_t r = (int32_t)i;
+      const int64_t a = s.action(r);
+      if (a < 0 || a % 2) continue;
+      if (a >= 8) return fail(PATCH_U_VALUE);  // a make-like action of a future version (type null)
+      if (obj_find(s.id_ctr(r), s.id_actor(r)) >= 0) continue;
+      const int32_t oa = s.obj_actor(r);
+      const int32_t ob = obj_find(oa < 0 ? -1 : s.obj_ctr(r), oa);
+      if (ob < 0) return fail(PATCH_U_VALUE);
+      const int32_t nm = obj_new(s.id_ctr(r), s.id_actor(r), obj_type_of_action(a));
+      if (nm < 0) return false;
+      w.obj[nm].parent = ob;
+      w.obj[nm].pk_row = r;
+    }
+    return true;
+  }
+  AM_PHD static bool meta_uleb(const uint8_t* m, uint32_t len, uint32_t& off, uint32_t& v) {
+    v = 0;
+    for (uint32_t sh = 0; sh < 35; sh += 7) {
+      if (off >= len) return false;
+      const uint8_t b = m[off++];
+      v |= (uint32_t)(b & 0x7f) << sh;
+      if (!(b & 0x80)) return true;
+    }
+    return false;
+  }
+  // the blob of diff_meta_pack: "AMM1", uleb count, per key: uleb object (0 _root, else 1 + row of
+  // its make op), uleb row of the key (its elemId), uleb n, n x uleb row of a visible op. Rows are
+  // base rows: the document order of the call that wrote the blob.
+  AM_PHD bool meta_restore(const uint8_t* m, uint32_t len) {
+    if (len < 4 || m[0] != 'A' || m[1] != 'M' || m[2] != 'M' || m[3] != '1') return fail(PATCH_U_VALUE);
+    uint32_t off = 4, nk;
+    if (!meta_uleb(m, len, off, nk)) return fail(PATCH_U_VALUE);
+    for (uint32_t k = 0; k < nk; k++) {
+      uint32_t orow, erow, n;
+      if (!meta_uleb(m, len, off, orow) || !meta_uleb(m, len, off, erow) || !meta_uleb(m, len, off, n) || erow >= s.nb() ||
+          orow > s.nb())
+        return fail(PATCH_U_VALUE);
+      const int32_t ob = orow == 0 ? 0 : obj_find(s.id_ctr((int32_t)orow - 1), s.id_actor((int32_t)orow - 1));
+      if (ob < 0) return fail(PATCH_U_VALUE);
+      const int32_t kd = kid_find(ob, (int32_t)erow, true);
+      if (kd < 0) return false;
+      w.kid[kd].head = -1;
+      w.kid[kd].n = 0;
+      for (uint32_t q = 0; q < n; q++) {
+        uint32_t vr;
+        if (!meta_uleb(m, len, off, vr) || vr >= s.nb()) return fail(PATCH_U_VALUE);
+        const int32_t r = (int32_t)vr;
+        const int64_t a = s.action(r);
+        if (a == 1) {
+          if (!kv_set(kd, s.id_ctr(r), s.id_actor(r), 1, r)) return false;
+        } else if (a >= 0 && a < 8 && a % 2 == 0) {
+          const int32_t co = obj_find(s.id_ctr(r), s.id_actor(r));
+          if (co < 0) return fail(PATCH_U_VALUE);
+          if (!kv_set(kd, s.id_ctr(r), s.id_actor(r), 2, co)) return false;
+        } else {
+          return fail(PATCH_U_VALUE);
+        }
+      }
+    }
+    return off == len || fail(PATCH_U_VALUE);
+  }
+
+  const uint8_t* meta_in = nullptr;  // the handle's snapshots, null: documentPatch's (load / init)
+  uint32_t meta_len = 0;
+  bool meta_mode = false;
+
   AM_PHD bool run() {
     for (uint32_t r = 0; r < s.nrows(); r++) w.fpos[r] = -1;
     for (uint32_t f = 0; f < s.nout(); f++) w.fpos[s.frow((int32_t)f)] = (int32_t)f;
-    if (!build_meta()) return false;
+    if (meta_mode && meta_in) {
+      if (!build_objects() || !meta_restore(meta_in, meta_len)) return false;
+    } else if (!build_meta()) {
+      return false;
+    }
     fast_init();
     uint32_t pos = 0;
     const uint32_t nstream = s.nrows() - s.nb();
@@ -1171,11 +1249,53 @@ struct Diff {
   }
 };
 
+// meta: the call keeps objectMeta for its handle (restored from meta_in when given, documentPatch's
+// otherwise); diff_meta_pack then writes what the call leaves.
 template <class Src>
-AM_PHD inline bool diff_scan(const Src& src, PatchOut& o, DiffScratch& w) {
+AM_PHD inline bool diff_scan(const Src& src, PatchOut& o, DiffScratch& w, bool meta = false, const uint8_t* meta_in = nullptr,
+                             uint32_t meta_len = 0) {
   o.nrec = o.nmval = o.nheap = 0;
   o.status = 0;
   o.arg0 = o.arg1 = 0;
   Diff<Src> d(src, w, o);
+  d.meta_mode = meta;
+  d.meta_in = meta_in;
+  d.meta_len = meta_len;
   return d.run();
+}
+
+// The children snapshots objectMeta holds after a successful diff_scan, as the blob meta_restore
+// reads (rows = positions in this call's merged document order, the next call's base rows).
+// Returns the bytes written, 0 when cap is too small or a snapshot names a row the merged document
+// does not keep.
+template <class Src>
+AM_PHD inline uint64_t diff_meta_pack(const Src& s, const DiffScratch& w, uint8_t* dst, uint64_t cap) {
+  uint64_t n = 4;
+  bool ok = true;
+  auto put = [&](uint64_t v) {
+    const uint32_t l = pk_uleb_len(v);
+    if (n + l > cap) { ok = false; return; }
+    pk_uleb(dst + n, v);
+    n += l;
+  };
+  auto frow = [&](int32_t row) -> uint64_t {
+    const int32_t f = row >= 0 && (uint32_t)row < s.nrows() ? w.fpos[row] : -1;
+    if (f < 0) ok = false;
+    return f < 0 ? 0 : (uint64_t)f;
+  };
+  if (cap < 4) return 0;
+  dst[0] = 'A'; dst[1] = 'M'; dst[2] = 'M'; dst[3] = '1';
+  uint64_t nk = 0;
+  for (uint32_t ob = 0; ob < w.nobj; ob++)
+    for (int32_t k = w.obj[ob].kids; k >= 0; k = w.kid[k].next) nk++;
+  put(nk);
+  for (uint32_t ob = 0; ob < w.nobj && ok; ob++)
+    for (int32_t k = w.obj[ob].kids; k >= 0 && ok; k = w.kid[k].next) {
+      put(w.obj[ob].actor < 0 ? 0 : 1 + frow(w.obj[ob].pk_row));
+      put(frow(w.kid[k].elem_row));
+      put((uint64_t)w.kid[k].n);
+      for (int32_t e = w.kid[k].head; e >= 0 && ok; e = w.kv[e].next)
+        put(frow(w.kv[e].kind == 2 ? w.obj[w.kv[e].ref].pk_row : w.kv[e].ref));
+    }
+  return ok ? n : 0;
 }

@@ -124,7 +124,7 @@ __host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t n
 }
 
 __host__ __device__ inline bool fast_eligible(const DocBounds& b, const am_doc_desc& dd) {
-  if (dd.flags & (AM_DOC_WANT_PATCH | AM_DOC_FIX_UTF8 | AM_DOC_PATCH_ROOM)) return false;  // getPatch: k_doc (P7); applyChanges patches: fast_diff
+  if (dd.flags & (AM_DOC_WANT_PATCH | AM_DOC_FIX_UTF8 | AM_DOC_PATCH_ROOM | AM_DOC_META)) return false;  // getPatch: k_doc (P7); applyChanges patches: fast_diff
   if (b.B == 0 || doc_scattered(b) || b.UC) return false;
   if (dd.base_chunk < 0 && dd.chg_count == 0) return false;
   if (b.span_hi - b.span_lo > FD_SPAN_MAX) return false;
@@ -868,7 +868,7 @@ __device__ __forceinline__ bool fast_diff(const uint8_t* IN, uint8_t* PS, uint32
   }
   if (l == 0) {
     PatchHdr2 h;
-    h.magic = AM_PATCH_MAGIC; h.status = 0; h.arg0 = 0; h.arg1 = 0; h.max_op = 0; h.nbytes = base; h.pad = 0;
+    h.magic = AM_PATCH_MAGIC; h.status = 0; h.arg0 = 0; h.arg1 = 0; h.max_op = 0; h.nbytes = base; h.meta_bytes = 0;
     *reinterpret_cast<PatchHdr2*>(out) = h;
   }
   return true;

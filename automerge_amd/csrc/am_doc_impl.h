@@ -1973,8 +1973,30 @@ __global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* _
       DiffSrc src{rows, ents, sr, succ_cnt, outent, reinterpret_cast<const int32_t*>(wsg + L.etime),
                   reinterpret_cast<const uint32_t*>(wsg + L.passend), s.npass, s.nb, s.nrows, NOUT, NSUCC, actors,
                   s.nactors, chg, NC, A};
-      diff_scan(src, po, dw);
-      wire_out(po, 0, wsg + L.pwire, L.pwire_cap);
+      // objectMeta of the handle (AM_DOC_META): the snapshots its previous call left, if any
+      const bool meta = (dd.flags & AM_DOC_META) != 0;
+      const uint8_t* mi = nullptr;
+      uint32_t ml = 0;
+      if (meta && dd.meta_chunk) {
+        const am_chunk_desc mc = chunks[dd.meta_chunk - 1];
+        mi = arena + mc.off;
+        ml = mc.len;
+      }
+      diff_scan(src, po, dw, meta, mi, ml);
+      uint8_t* const pw = wsg + L.pwire;
+      const uint64_t wl = patch_pack(po, 0, pw, L.pwire_cap);
+      if (!wl) {
+        wire_out(po, 0, pw, L.pwire_cap);
+      } else if (meta && !po.status) {
+        // the snapshots this call leaves, after the stream (PatchHdr2.meta_bytes)
+        const uint64_t mb = diff_meta_pack(src, dw, pw + wl, L.pwire_cap - wl);
+        if (!mb) {
+          po.status = PATCH_U_CAPACITY;
+          patch_pack(po, 0, pw, L.pwire_cap);
+        } else {
+          for (int q = 0; q < 8; q++) pw[offsetof(PatchHdr2, meta_bytes) + q] = (uint8_t)(mb >> (8 * q));
+        }
+      }
     }
     // heads for the host (hot region may be LDS): mirror into the global workspace
     if (kHotLds)

@@ -538,10 +538,18 @@ __global__ void __launch_bounds__(256) k_chunks(const uint8_t* __restrict__ aren
   __shared__ __attribute__((aligned(16))) uint8_t stage[4][KC_STAGE + 16];
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const bool valid = i < nchunks;
+  bool valid = i < nchunks;
   am_chunk_desc cd;
   cd.off = 0; cd.len = 0; cd.flags = 0;
   if (valid) cd = chunks[i];
+  // an objectMeta blob (AM_CHUNK_RAW) is not a container: no documents' chunk, nothing to parse
+  if (valid && (cd.flags & AM_CHUNK_RAW)) {
+    ChunkInfo& ci = info[i];
+    ci.status = AM_OK; ci.type = 0xff; ci.nops = ci.nents = ci.nchg = ci.ndeps = ci.nactors = ci.strbytes = 0;
+    ci.nheads = ci.nunk = 0; ci.arg0 = 0;
+    valid = false;
+    cd.off = 0; cd.len = 0; cd.flags = 0;
+  }
   // span of the wave's chunks
   uint64_t lo = valid ? cd.off : ~0ull, hi = valid ? cd.off + cd.len : 0ull;
 #pragma unroll

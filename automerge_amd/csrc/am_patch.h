@@ -91,7 +91,7 @@ struct PatchHdr2 {  // 48 bytes
   int64_t arg0, arg1; // error arguments (counter increment: ctr, actor index)
   int64_t max_op;     // documentPatch's maxOp (getPatch logs)
   uint64_t nbytes;    // stream bytes after the header
-  uint64_t pad;
+  uint64_t meta_bytes;  // AM_DOC_META: bytes of the objectMeta blob after the stream (am_diff.h diff_meta_pack)
 };
 
 AM_PHD inline uint32_t pk_uleb_len(uint64_t v) {
@@ -166,7 +166,7 @@ AM_PHD inline uint64_t patch_pack(const PatchOut& o, int64_t max_op, uint8_t* ds
   h.arg0 = o.arg0;
   h.arg1 = o.arg1;
   h.max_op = max_op;
-  h.pad = 0;
+  h.meta_bytes = 0;
   uint64_t n = 0;
   if (!o.status) {
     uint64_t mv = 0;

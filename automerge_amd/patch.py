@@ -10,7 +10,7 @@ import struct
 import numpy as np
 
 HDR_DT = np.dtype([("magic", "<u4"), ("status", "<u4"), ("arg0", "<i8"), ("arg1", "<i8"), ("max_op", "<i8"),
-                   ("nbytes", "<u8"), ("pad", "<u8")])
+                   ("nbytes", "<u8"), ("meta_bytes", "<u8")])
 assert HDR_DT.itemsize == 48
 MAGIC = 0x32504D41
 

@@ -84,7 +84,9 @@ typedef struct am_chunk_desc {      // one binary chunk in the input arena
   uint64_t off;
   uint32_t len;
   uint32_t flags;           // bit0: checksum already verified by the host stage (inflated input)
+                            // bit1: AM_CHUNK_RAW -- not a container: a document's objectMeta blob
 } am_chunk_desc;
+#define AM_CHUNK_RAW 2u
 typedef struct am_doc_desc {
   int64_t base_chunk;       // chunk index of the base document, -1 for Backend.init()
   uint32_t chg_begin, chg_count;   // change chunks [chg_begin, chg_begin + chg_count)
@@ -92,12 +94,19 @@ typedef struct am_doc_desc {
   uint32_t flags;           // bit0: haveHashGraph (fresh doc, or host knows all change hashes)
                             // bit1: AM_DOC_WANT_PATCH -- also write the getPatch() log of the result
                             // bit2: AM_DOC_WANT_DIFF -- also write the patch applyChanges returns
-  uint32_t pad;
+                            // AM_DOC_META -- the handle keeps objectMeta across calls (below)
+  uint32_t meta_chunk;      // with AM_DOC_META: 1 + index of the AM_CHUNK_RAW chunk holding the objectMeta
+                            // children the handle's previous call left; 0: documentPatch's (load / init)
 } am_doc_desc;
 #define AM_DOC_WANT_PATCH 2u
 #define AM_DOC_WANT_DIFF 4u
 #define AM_DOC_PATCH_ROOM 16u /* 8x the applyChanges-patch pools (a rerun after a patch capacity report) */
 #define AM_DOC_FIX_UTF8 8u   /* k_doc reserves room for U+FFFD replacements of invalid UTF-8 (encoding.js:15-17) */
+/* With AM_DOC_WANT_DIFF: objectMeta as the reference carries it on one BackendDoc from call to call
+ * (new.js:884-931 children snapshots, 1812/1857): the patch log's header field meta_bytes counts the
+ * blob of snapshots this call leaves, stored after the log's stream; the next call of the same handle
+ * passes it back through meta_chunk. The per-document calls (am_doc_*) do this themselves. */
+#define AM_DOC_META 32u
 typedef struct am_known_hash {      // changeIndexByHash entry supplied by the host
   uint8_t hash[32];
   int64_t index;

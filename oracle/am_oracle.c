@@ -761,7 +761,33 @@ struct oc_doc {
   uint8_t **queue; size_t *queue_n; size_t nqueue; /* enqueued change buffers */
   size_t nops; int64_t max_op;
   size_t nchanges;
+  /* objectMeta children carried across applyChanges calls (new.js:1812, 1857; see
+   * am_apply_patch_oracle.inc): 0 = as documentPatch leaves them (load / init), 1 = pm[], 2 = not
+   * tracked (after a patchless oc_doc_apply) */
+  int meta_mode;
+  struct pm_key *pm; size_t npm;
 };
+typedef struct { int64_t ctr, actor; int kind; } pm_val; /* children[elemId][opId]: 1 set op, 2 object */
+typedef struct pm_key {
+  int64_t octr, oactor;                                      /* the object (-1, -1: _root) */
+  int is_str; uint8_t *key; uint32_t keyn; int64_t ec, ea;  /* elemId */
+  size_t n; pm_val *v;
+} pm_key;
+static void pm_free(pm_key *pm, size_t n) {
+  for (size_t i = 0; i < n; i++) { free(pm[i].key); free(pm[i].v); }
+  free(pm);
+}
+static pm_key *pm_copy(const pm_key *pm, size_t n) {
+  pm_key *d = (pm_key *)calloc(n + 1, sizeof(pm_key));
+  for (size_t i = 0; i < n; i++) {
+    d[i] = pm[i];
+    d[i].key = (uint8_t *)malloc(pm[i].keyn + 1);
+    if (pm[i].keyn) memcpy(d[i].key, pm[i].key, pm[i].keyn);
+    d[i].v = (pm_val *)malloc(sizeof(pm_val) * (pm[i].n + 1));
+    if (pm[i].n) memcpy(d[i].v, pm[i].v, sizeof(pm_val) * pm[i].n);
+  }
+  return d;
+}
 
 typedef struct {
   size_t nactors; const uint8_t **actors; uint32_t *actor_lens;
@@ -1077,7 +1103,12 @@ static void apply_changes(ctx_t *c, oc_doc *doc, docst_t *st, const uint8_t *con
     memcpy(copy, bufs[i], lens[i]);
     decode_change(c, copy, lens[i], &chs[i]);
   }
-  for (size_t i = 0; i < doc->nqueue; i++) decode_change(c, doc->queue[i], doc->queue_n[i], &chs[n + i]);
+  /* the queue's buffers are replaced at commit; the patch keeps pointers into the decoded bytes */
+  for (size_t i = 0; i < doc->nqueue; i++) {
+    uint8_t *copy = (uint8_t *)amalloc(c, doc->queue_n[i] + 1);
+    memcpy(copy, doc->queue[i], doc->queue_n[i]);
+    decode_change(c, copy, doc->queue_n[i], &chs[n + i]);
+  }
 
   /* changeIndexByHash (mutable copy) */
   hidx_t *hidx = (hidx_t *)amalloc(c, sizeof(hidx_t) * (doc->nhidx + total + 1));
@@ -1534,6 +1565,7 @@ oc_doc *oc_doc_clone(const oc_doc *s) {
     memcpy(d->queue[i], s->queue[i], s->queue_n[i]);
     d->queue_n[i] = s->queue_n[i];
   }
+  d->pm = s->npm ? pm_copy(s->pm, s->npm) : NULL;
   return d;
 }
 
@@ -1541,6 +1573,7 @@ void oc_doc_free(oc_doc *d) {
   if (!d) return;
   for (size_t i = 0; i < d->nqueue; i++) free(d->queue[i]);
   free(d->queue); free(d->queue_n); free(d->hidx); free(d->state); free(d->binary);
+  pm_free(d->pm, d->npm);
   free(d);
 }
 
@@ -1554,6 +1587,7 @@ int oc_doc_apply(oc_doc *doc, const uint8_t *const *bufs, const size_t *lens, si
   docst_t st;
   load_state(&c, doc, &st);
   apply_changes(&c, doc, &st, bufs, lens, n);
+  doc->meta_mode = 2; /* the reference's objectMeta moved on too (updatePatchProperty runs in every applyChanges) */
   afree_all(&c);
   return 0;
 }

@@ -6,7 +6,7 @@ import json
 import os
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-FILES = ["sync", "sync_random", "backend", "test", "text", "table", "errors"]
+FILES = ["sync", "sync_random", "objmeta", "backend", "test", "text", "table", "errors"]
 # Scenarios where this engine knowingly differs from the reference, with the reason. Each must still
 # fail loudly with an "automerge_amd: unsupported" error (never a silently different result).
 KNOWN_DIVERGENT = {

@@ -32,3 +32,9 @@ def codecs():
 @pytest.fixture(scope="session")
 def docs():
     return golden("docs.json")["scenarios"]
+
+
+@pytest.fixture(scope="session")
+def objmeta():
+    """multi-call applyChanges histories over concurrently created objects (tests/golden/gen/make_objmeta.js)"""
+    return golden("objmeta.json")["scenarios"]

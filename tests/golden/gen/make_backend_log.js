@@ -6,7 +6,8 @@
 // automerge_amd/js/backend.js and compares every result.
 //   NODE_PATH=tests/golden/gen/node_modules node tests/golden/gen/make_backend_log.js
 // AM_LOG_FILES=sync_random AM_LOG_MAX=4000 records the randomized sync sessions instead
-// (backend_log_sync_random.json).
+// (backend_log_sync_random.json); AM_LOG_FILES=objmeta AM_LOG_MAX=4000 the concurrent-object sessions
+// (backend_log_objmeta.json).
 // Clock and randomness are pinned (Date without arguments = epoch, seeded randomBytes and
 // Math.random), so a re-run reproduces the committed tests/golden/backend_log_*.json byte for byte.
 'use strict'
@@ -131,10 +132,10 @@ function randomSyncTests() {
   for (let k = 0; k < 36; k++) {
     tests.push({name: 'random sync session ' + k, before: [], after: [], fn: () => {
       const big = k % 6 === 5
-      // the list / text / map objects come from one shared first change: two peers creating the same
-      // root key concurrently make the patches depend on new.js's per-pass objectMeta.children
-      // snapshot (DESIGN.md §1, residual divergences), which this log is not about
-      const shared = 1 + (rnd(3) ? rnd(big ? 60 : 15) : 0)
+      // shared = 0: both peers create the list / text / map objects concurrently, so later patches
+      // read the root keys' conflicts from the objectMeta.children snapshots earlier calls left
+      // (new.js:884-931, 1461-1528)
+      const shared = rnd(3) ? rnd(big ? 60 : 15) : 0
       const na = rnd(big ? 150 : 12), nb = rnd(big ? 150 : 12)
       let a = Automerge.init((0xa000 + k).toString(16) + 'aa'), b = Automerge.init((0xb000 + k).toString(16) + 'bb')
       for (let i = 0; i < shared; i++) a = edit(a, i)
@@ -163,11 +164,61 @@ function randomSyncTests() {
   return tests
 }
 
+// ---- concurrent objects under one root key (objectMeta carried across calls, new.js:884-931,
+// 1461-1528, 1812/1857) ----
+// Two to four peers each create `items` (list, map or text) in their first change, most of them
+// also setting other root keys; they exchange changes a few at a time (Automerge.applyChanges of
+// getChanges, so every delivery is one Backend.applyChanges call on the receiving handle), edit
+// inside whichever object wins for them, and end with a full merge and more edits inside.
+function objmetaTests() {
+  const tests = []
+  let s = 0x0b1e
+  const rnd = n => { s = (Math.imul(s, 1103515245) + 12345) >>> 0; return (s >>> 8) % n }
+  const mk = k => k === 0 ? [] : k === 1 ? {} : new Automerge.Text()
+  const inside = (d) => {
+    const o = d.items
+    if (o instanceof Automerge.Text) o.insertAt(rnd(o.length + 1), String.fromCharCode(97 + rnd(26)))
+    else if (Array.isArray(o)) { if (o.length && rnd(4) === 0) o.deleteAt(rnd(o.length)); else o.insertAt(rnd(o.length + 1), rnd(100)) }
+    else if (o && typeof o === 'object') o['p' + rnd(3)] = rnd(100)
+    else d.items = mk(rnd(3))
+  }
+  const keys = ['a', 'b', 'title', 'z']
+  for (let k = 0; k < 24; k++) {
+    tests.push({name: 'objmeta session ' + k, before: [], after: [], fn: () => {
+      const n = 2 + rnd(3)
+      let docs = []
+      for (let i = 0; i < n; i++) docs.push(Automerge.init((0xc000 + 16 * k + i).toString(16) + 'cc'))
+      docs = docs.map(d => Automerge.change(d, {time: 0}, x => {
+        for (let q = rnd(3); q > 0; q--) x[keys[rnd(4)]] = rnd(50)
+        x.items = mk(rnd(3))
+        for (let q = rnd(3); q > 0; q--) x[keys[rnd(4)]] = 'v' + rnd(50)
+      }))
+      for (let round = 0; round < 4; round++) {
+        for (let i = 0; i < n; i++) {
+          if (rnd(2)) docs[i] = Automerge.change(docs[i], {time: 0}, x => { inside(x); if (rnd(3) === 0) x[keys[rnd(4)]] = rnd(9) })
+          const j = rnd(n)
+          if (j !== i) {
+            const bs = d => Automerge.Frontend.getBackendState(d)
+            const missing = Automerge.Backend.getChangesAdded(bs(docs[i]), bs(docs[j]))
+            const cut = 1 + rnd(Math.max(1, missing.length))
+            docs[i] = Automerge.applyChanges(docs[i], missing.slice(0, cut))[0]
+            if (cut < missing.length) docs[i] = Automerge.applyChanges(docs[i], missing.slice(cut))[0]
+          }
+        }
+      }
+      for (let i = 1; i < n; i++) docs[0] = Automerge.merge(docs[0], docs[i])
+      for (let i = 1; i < n; i++) docs[i] = Automerge.merge(docs[i], docs[0])
+      for (let i = 0; i < n; i++) docs[i] = Automerge.change(docs[i], {time: 0}, inside)
+    }})
+  }
+  return tests
+}
+
 const MAX_ENTRIES = +(process.env.AM_LOG_MAX || 400)
 function run(file) {
   const scenarios = []
   let passed = 0, failed = 0, skipped = 0
-  for (const t of (file === 'sync_random' ? randomSyncTests() : harness(file))) {
+  for (const t of (file === 'sync_random' ? randomSyncTests() : file === 'objmeta' ? objmetaTests() : harness(file))) {
     if (t.fn.length > 0) { skipped++; continue }  // callback-style tests
     handles = new Map()
     nextHandle = 0

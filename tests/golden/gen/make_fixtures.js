@@ -619,4 +619,4 @@ function main() {
 }
 
 if (require.main === module) main()
-else module.exports = {c4Doc, c2Doc, lcg}
+else module.exports = {c4Doc, c2Doc, lcg, runBackend, jsonPatch, hex, randomActor, randomValue, safeChange, changeHash}

@@ -52,6 +52,61 @@ def test_apply_patch_per_step_matches_reference(docs):
     assert not bad, (len(bad), bad[:10])
 
 
+def _replay_handle(sc, loadchanges_every=0):
+    """One backend handle through the scenario's steps; yields (step, expected, got patch, saved hex,
+    heads). With loadchanges_every = k, every k-th apply step goes through loadChanges (no patch;
+    objectMeta moves on all the same, backend.js:116-121)."""
+    from automerge_amd import _native as N
+    from automerge_amd import backend as B
+    st = None
+    napply = 0
+    for i, (step, exp) in enumerate(zip(sc["steps"], sc["results"])):
+        if step["op"] == "load":
+            st = B.load(bytes.fromhex(step["bytes"]))
+            continue
+        if st is None:
+            st = B.init()
+        napply += 1
+        changes = [bytes.fromhex(c) for c in step["changes"]]
+        try:
+            if loadchanges_every and napply % loadchanges_every == 0:
+                st, got = B.loadChanges(st, changes), None
+            else:
+                st, patch = B.applyChanges(st, changes)
+                got = _jsonable(patch)
+        except N.AutomergeError as e:
+            got = {"error": str(e)}
+        yield i, exp, got, (B.save(st).hex() if not (got and "error" in got) else None), \
+            (B.getHeads(st) if not (got and "error" in got) else None)
+        if got and "error" in got:
+            return
+
+
+@pytest.mark.parametrize("every", [0, 3])
+def test_apply_patch_objectmeta_across_calls(objmeta, every):
+    """objectMeta's children snapshots carried from call to call on one handle (new.js:884-931,
+    1461-1528, 1812/1857): concurrent same-key makeMap / makeList / makeText from 2-4 actors with
+    other-key edits, delivered in several calls (tests/golden/objmeta.json, recorded from the
+    reference). Every patch, saved document and heads after every step match the reference's; with
+    every=3 each third call is a loadChanges, which must move objectMeta on as well."""
+    n, bad = 0, []
+    for sc in objmeta:
+        for i, exp, got, saved, heads in _replay_handle(sc, every):
+            if "error" in exp:
+                if not got or got.get("error") != exp["error"]["message"]:
+                    bad.append((sc["name"], i, "error", got))
+                break
+            n += 1
+            if got is not None and got != exp["patch"]:
+                bad.append((sc["name"], i, "patch", (got or {}).get("error")))
+                break
+            if saved != exp["save"] or heads != exp["heads"]:
+                bad.append((sc["name"], i, "save/heads"))
+                break
+    assert n > 600
+    assert not bad, (len(bad), bad[:10])
+
+
 def _steps(docs):
     """(base saved bytes | None, changes, expected patch) of every apply step whose previous state
     had no queued changes."""

@@ -401,7 +401,7 @@ uint64_t layout(std::vector<DocOut>& outs, uint8_t* arena, uint64_t cap, am_chun
     docs[d].known_begin = 0;
     docs[d].known_count = 0;
     docs[d].flags = o.base.empty() ? 1u : 0u;  // fresh documents have the full hash graph
-    docs[d].pad = 0;
+    docs[d].meta_chunk = 0;
     for (auto& c : o.changes) {
       chunks[ci++] = {off, (uint32_t)c.size(), 0};
       memcpy(arena + off, c.data(), c.size());
