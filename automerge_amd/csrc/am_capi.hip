@@ -942,8 +942,10 @@ extern "C" int am_pipe_submit(am_pipe* p, const uint8_t* arena, uint64_t arena_l
   am_launch_doc(d, s);
   (void)hipEventRecord(sl->ev_d1, s);
   am_launch_out_hash(d, s);
-  am_launch_pipe_compact(d, sl->olen.p, sl->ooff.p, sl->plen.p, sl->poff.p, sl->tmp.p, sl->totals.p, sl->dout.p, c.out_bytes,
-                         sl->dpatch.p, c.patch_bytes, sl->summ.p, s);
+  // documents past the caller's buffers (or the device arenas) report AM_U_CAPACITY
+  am_launch_pipe_compact(d, sl->olen.p, sl->ooff.p, sl->plen.p, sl->poff.p, sl->tmp.p, sl->totals.p, sl->dout.p,
+                         std::min<uint64_t>(c.out_bytes, out ? out_cap : 0), sl->dpatch.p,
+                         std::min<uint64_t>(c.patch_bytes, patches ? patch_cap : 0), sl->summ.p, s);
   if (hipMemcpyAsync(sl->h_totals, sl->totals.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s) != hipSuccess)
     return fail("automerge_amd: D2H failed");
   if (hipEventRecord(sl->ev_comp, s) != hipSuccess || hipGetLastError() != hipSuccess) return fail("automerge_amd: kernel launch failed");

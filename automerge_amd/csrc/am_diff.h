@@ -356,7 +356,14 @@ struct Diff {
     if (elem_str(i)) return s.key_eq(i, j);
     return elem_ctr(i) == elem_ctr(j) && elem_actor(i) == elem_actor(j);
   }
-  AM_PHD static uint32_t obj_type_of_action(int64_t a) { return a == 2 ? 1u : a == 4 ? 2u : a == 6 ? 3u : 0u; }
+  // make-like ops: `op[actionIdx] % 2 === 0` (new.js:894, 909, 923, 972) holds for every even action
+  // and for a null action (null % 2 === 0); s.action() reads null as -1
+  AM_PHD static bool is_make(int64_t a) { return a < 0 || a % 2 == 0; }
+  // their object type (new.js:886, 924): OBJECT_TYPE[ACTIONS[a]] -- undefined (4) for a null action,
+  // null (5) for an action beyond ACTIONS; 0 map 1 list 2 text 3 table
+  AM_PHD static uint32_t obj_type_of_action(int64_t a) {
+    return a < 0 ? 4u : a == 2 ? 1u : a == 4 ? 2u : a == 6 ? 3u : a >= 8 ? 5u : 0u;
+  }
 
   // ---- objectMeta / patches ----
   AM_PHD int32_t obj_find(int64_t ctr, int32_t actor) const {
@@ -558,14 +565,13 @@ struct Diff {
   AM_PHD bool update_property(int32_t ob, int32_t row, int32_t f, int64_t lim, int64_t list_index, bool has_old,
                               uint32_t old_succ, bool whole_doc) {
     const int64_t action = s.action(row);
-    // an unknown odd action carries no value and no object (like link); make* actions beyond the
-    // known types would need objectMeta entries of type null (not supported)
-    if (action < 0 || (action >= 8 && action % 2 == 0)) return fail(PATCH_U_VALUE);
+    // an unknown odd action carries no value and no object (like link); a null or unknown even action
+    // is make-like, its object of type undefined / null (emptyObjectPatch gives it props)
     const int64_t idc = s.id_ctr(row);
     const int32_t ida = s.id_actor(row);
     const uint32_t cur_succ = has_old ? nsucc_at(f, lim) : 0u;
     // a new make* op: objectMeta[opId] and children[elemId][opId] (new.js:894-897)
-    if (action % 2 == 0 && obj_find(idc, ida) < 0) {
+    if (is_make(action) && obj_find(idc, ida) < 0) {
       const int32_t nm = obj_new(idc, ida, obj_type_of_action(action));
       if (nm < 0) return false;
       w.obj[nm].parent = ob;
@@ -589,7 +595,7 @@ struct Diff {
       if (w.pst[ps].vis_tail >= 0) w.vis[w.pst[ps].vis_tail].next = (int32_t)w.nvis;
       else w.pst[ps].vis_head = (int32_t)w.nvis;
       w.pst[ps].vis_tail = (int32_t)w.nvis++;
-      if (action % 2 == 0) w.pst[ps].has_child = 1;
+      if (is_make(action)) w.pst[ps].has_child = 1;
     }
     const int32_t prev = kid_find(ob, row, false);
     if (w.pst[ps].has_child || (prev >= 0 && w.kid[prev].n > 0)) {
@@ -602,7 +608,7 @@ struct Diff {
         const int64_t va = s.action(vr);
         if (va == 1) {
           if (!kv_set(kd, s.id_ctr(vr), s.id_actor(vr), 1, vr)) return false;
-        } else if (va >= 0 && va < 8 && va % 2 == 0) {
+        } else if (is_make(va)) {
           const int32_t co = obj_find(s.id_ctr(vr), s.id_actor(vr));
           if (co < 0) return fail(PATCH_U_VALUE);
           if (!kv_set(kd, s.id_ctr(vr), s.id_actor(vr), 2, co)) return false;
@@ -661,7 +667,7 @@ struct Diff {
         if (!row_val(row, pv)) return false;
         have_pv = true;
         pk_c = idc; pk_a = ida;
-      } else if (action % 2 == 0) {
+      } else if (is_make(action)) {
         const int32_t co = obj_find(idc, ida);
         if (co < 0) return fail(PATCH_U_VALUE);
         patch_on(co);
@@ -672,7 +678,9 @@ struct Diff {
     }
     patch_on(ob);
     if (!s.has_key(row)) {
-      // list / text object (new.js:983-1033)
+      // list / text object (new.js:983-1033); the patch of an object of type undefined / null has no
+      // edits array (emptyObjectPatch, new.js:726-732), where the reference stops with a TypeError
+      if (w.obj[ob].type >= 4) return fail(PATCH_U_VALUE);
       const int64_t ec = elem_ctr(row);
       const int32_t ea = elem_actor(row);
       if (has_old && old_succ == 0 && w.pst[ps].action == 1) {
@@ -1004,7 +1012,7 @@ struct Diff {
     int64_t list_index = 0;
     int32_t ob = 0;
     w.npst = 0; w.nvis = 0; w.ncs = 0; w.ncm = 0;
-    for (uint32_t i = 0; i < s.nb(); i++) {
+    for (uint32_t i = 0; i < s.nmeta_rows(); i++) {
       const int32_t r = (int32_t)i;
       const int64_t oc = s.obj_ctr(r);
       const int32_t oa = s.obj_actor(r);
@@ -1161,11 +1169,10 @@ struct Diff {
   // (meta_restore); the objects themselves (parent, parentKey, type) follow from the make ops.
   AM_PHD bool build_objects() {
     if (obj_new(-1, -1, 0) < 0) return false;
-    for (uint32_t i = 0; i < s.nb(); i++) {
+    for (uint32_t i = 0; i < s.nmeta_rows(); i++) {
       const int32_t r = (int32_t)i;
       const int64_t a = s.action(r);
-      if (a < 0 || a % 2) continue;
-      if (a >= 8) return fail(PATCH_U_VALUE);  // a make-like action of a future version (type null)
+      if (!is_make(a)) continue;
       if (obj_find(s.id_ctr(r), s.id_actor(r)) >= 0) continue;
       const int32_t oa = s.obj_actor(r);
       const int32_t ob = obj_find(oa < 0 ? -1 : s.obj_ctr(r), oa);
@@ -1212,7 +1219,7 @@ struct Diff {
         const int64_t a = s.action(r);
         if (a == 1) {
           if (!kv_set(kd, s.id_ctr(r), s.id_actor(r), 1, r)) return false;
-        } else if (a >= 0 && a < 8 && a % 2 == 0) {
+        } else if (is_make(a)) {
           const int32_t co = obj_find(s.id_ctr(r), s.id_actor(r));
           if (co < 0) return fail(PATCH_U_VALUE);
           if (!kv_set(kd, s.id_ctr(r), s.id_actor(r), 2, co)) return false;

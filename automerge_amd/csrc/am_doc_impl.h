@@ -402,9 +402,13 @@ __device__ static void decode_stream(DocShared& s, uint32_t item, int64_t* cells
   ColDec d;
   cd_init(d, type, AV(s) + off, si.clen[col]);
   const int64_t sbase = (int64_t)(off - s.b.span_lo);
+  // the base document's action column ends the op sequence for readNextDocOp (new.js:658-670): a
+  // column that runs out early (the all-null column RLEEncoder writes as no bytes, encoding.js:778-782)
+  const bool track_act = !si.is_change && col == OC_ACTION;
   for (uint32_t i = 0; i < n; i++) {
     int64_t v;
     uint32_t e;
+    if (track_act && cd_done(d) && s.nb_act == 0xffffffffu) s.nb_act = i;
     if (type == DT_BOOL) {
       bool bv;
       e = cd_next_bool(d, bv);
@@ -817,8 +821,9 @@ struct RowSrc {
   const ChgRow* chg;
   uint32_t nc;
   APtr A;
+  uint32_t nscan;  // ops documentPatch reads: nout, or 0 for a document whose action column is empty
   __device__ const Row& r(uint32_t i) const { return rows[sr[i].row]; }
-  __device__ uint32_t n() const { return nout; }
+  __device__ uint32_t n() const { return nscan; }
   __device__ int64_t obj_ctr(uint32_t i) const { const int64_t v = r(i).obj_ctr; return v == AM_NULL64 ? -1 : v; }
   __device__ int32_t obj_actor(uint32_t i) const { return r(i).obj_actor; }
   __device__ bool has_key(uint32_t i) const { return r(i).key_len != AM_NOSTR; }
@@ -881,12 +886,14 @@ struct DiffSrc {
   const int32_t* etime;  // stream time of each final succ entry's op
   const uint32_t* pend;
   uint32_t np, nbase, nr, nf, nsucc_total;
+  uint32_t nmeta;  // base ops documentPatch reads for objectMeta: nbase, 0 for an empty action column
   const ActorRef* actors;
   uint32_t na;
   const ChgRow* chg;
   uint32_t nc;
   APtr A;
   __device__ uint32_t nb() const { return nbase; }
+  __device__ uint32_t nmeta_rows() const { return nmeta; }
   __device__ uint32_t nrows() const { return nr; }
   __device__ uint32_t nout() const { return nf; }
   __device__ int32_t frow(int32_t f) const { return sr[f].row; }
@@ -1196,6 +1203,7 @@ __global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* _
     s.nb = s.nbe = s.nbc = s.nbd = 0;
     s.napplied = s.nqueued = s.nactors = s.nheads = 0;
     s.npass = 0;
+    s.nb_act = 0xffffffffu;
     s.nrows = s.nents = s.nchg = s.ndeps = s.nout = s.nnew = 0;
     s.max_op = 0;
     s.out_len = 0;
@@ -1305,6 +1313,11 @@ __global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* _
       const SrcInfo si = src_info(s, src);
       if (si.nr == 0 && si.ne != 0) set_err(s, AM_U_VALUE);  // group entries without ops
     }
+    __syncthreads();
+    // a base document whose action column holds fewer values than it has ops: the reference reads
+    // no ops from it when the column is empty (every action null: documentPatch / getPatch see an
+    // empty document); merging changes into it, or a column that stops part-way, is not restated
+    if (t == 0 && s.has_base && s.nb_act < s.nb && (s.nb_act != 0 || s.napplied > 0)) set_err(s, AM_U_VALUE);
     // actor ranks (lexicographic order of the hex ids)
     for (uint32_t i = t; i < s.nactors; i += T) {
       uint32_t rank = 0;
@@ -1332,8 +1345,9 @@ __global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* _
     // (documentPatch, new.js:1627-1630 -> this.maxOp, new.js:1749); applied changes raise it
     {
       int64_t m = 0;
-      for (uint32_t i = t; i < s.nb; i += T) m = rows[i].id_ctr > m ? rows[i].id_ctr : m;
-      for (uint32_t j = t; j < s.nbe; j += T) m = ents[j].ctr > m ? ents[j].ctr : m;
+      const bool read_all = s.nb_act >= s.nb;  // else no op is read (above)
+      for (uint32_t i = t; i < s.nb && read_all; i += T) m = rows[i].id_ctr > m ? rows[i].id_ctr : m;
+      for (uint32_t j = t; j < s.nbe && read_all; j += T) m = ents[j].ctr > m ? ents[j].ctr : m;
       for (int o = 32; o > 0; o >>= 1) {
         const int64_t x = __shfl_xor(m, o, 64);
         m = x > m ? x : m;
@@ -1360,7 +1374,6 @@ __global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* _
         set_err(s, AM_E_MISMATCH_KEY, r.key_ctr, r.key_actor);
         continue;
       }
-      if (r.action == AM_NULL64) { set_err(s, AM_U_VALUE); continue; }
       if (r.is_del && r.ps_cnt == 0 && r.key_len != AM_NOSTR) {
         // a del without pred disappears once an op of its key with a lower id has been merged
         // (mergeDocChangeOps drops dels whose preds were all seen, new.js:1199-1212); otherwise the
@@ -1955,7 +1968,7 @@ __global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* _
       po.heap = pbase + 64 + 64 * L.patch_nrec + 32 * L.patch_nmval;
       po.cap_rec = L.patch_nrec; po.cap_mval = L.patch_nmval; po.cap_heap = L.patch_heap;
       po.arg0 = po.arg1 = 0;
-      RowSrc src{rows, sr, succ_cnt, outent, NOUT, NSUCC, actors, s.nactors, chg, NC, A};
+      RowSrc src{rows, sr, succ_cnt, outent, NOUT, NSUCC, actors, s.nactors, chg, NC, A, s.nb_act < s.nb ? 0u : NOUT};
       int64_t pmax = 0;
       patch_scan(src, po, w, pmax);
       wire_out(po, pmax, wsg + L.pwire, L.pwire_cap);
@@ -1971,8 +1984,8 @@ __global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* _
       DiffScratch dw;
       diff_scratch_bind(wsg + L.dscr, s.b.R, s.b.E, dw, (s.b.U & 2) ? 8 : 1);
       DiffSrc src{rows, ents, sr, succ_cnt, outent, reinterpret_cast<const int32_t*>(wsg + L.etime),
-                  reinterpret_cast<const uint32_t*>(wsg + L.passend), s.npass, s.nb, s.nrows, NOUT, NSUCC, actors,
-                  s.nactors, chg, NC, A};
+                  reinterpret_cast<const uint32_t*>(wsg + L.passend), s.npass, s.nb, s.nrows, NOUT, NSUCC,
+                  s.nb_act < s.nb ? 0u : s.nb, actors, s.nactors, chg, NC, A};
       // objectMeta of the handle (AM_DOC_META): the snapshots its previous call left, if any
       const bool meta = (dd.flags & AM_DOC_META) != 0;
       const uint8_t* mi = nullptr;

@@ -42,7 +42,8 @@ enum : uint32_t {
   PV_COUNTER,    // v0, datatype 'counter'
   PV_TIMESTAMP,  // v0, datatype 'timestamp'
   PV_BYTES,      // heap [v0, v0 + v1) as Uint8Array, datatype = dt (7 bytes, 0..2 / 10..15 unknown)
-  PV_CHILD,      // child object patch: objectId (v0, actor v1), type dt (0 map 1 list 2 text 3 table)
+  PV_CHILD,      // child object patch: objectId (v0, actor v1), type dt (0 map 1 list 2 text 3 table
+                 // 4 undefined 5 null)
 };
 // multi-insert datatype codes (dt of PR_MULTI): 0 none, else 1 + (vtag - PV_UINT) for named ones,
 // 100 + n for a numeric datatype n
@@ -304,6 +305,11 @@ AM_PHD inline uint32_t pv_dtcode(uint32_t vtag, uint32_t dt) {
   return 0;
 }
 AM_PHD inline bool pv_dt_truthy(uint32_t code) { return code != 0 && code != 100; }
+// object type of a make-like action (OBJECT_TYPE[ACTIONS[a]], new.js:886): 0 map 1 list 2 text
+// 3 table, 4 undefined (null action), 5 null (an even action beyond ACTIONS); a = -1 for null
+AM_PHD inline uint32_t pv_obj_type(int64_t a) {
+  return a < 0 ? 4u : a == 2 ? 1u : a == 4 ? 2u : a == 6 ? 3u : a >= 8 ? 5u : 0u;
+}
 
 // ---- the scan ----
 // Src interface (all indexes are positions in document order):
@@ -477,7 +483,8 @@ AM_PHD inline bool patch_scan(const Src& src, PatchOut& o, PatchScratch& w, int6
     if (has_key && src.key_len(i) == 0) { o.status = PATCH_U_VALUE; return false; }  // '' key (falsy in JS)
     const int64_t ec = ins ? idc : src.key_ctr(i);
     const int32_t ea = ins ? ida : src.key_actor(i);
-    const bool is_make = action >= 0 && action < 8 && (action % 2) == 0;
+    // make-like: `op[actionIdx] % 2 === 0` (new.js:894, 972), every even action and a null one
+    const bool is_make = action < 0 || (action % 2) == 0;
     if (is_make) {  // objectMeta[opId]; reachable (visible make op of a reachable object) + type bits
       bool known = false;
       for (uint32_t k = 0; k < nmk && !known; k++) known = w.mk_ctr[k] == idc && w.mk_actor[k] == ida;
@@ -557,7 +564,7 @@ AM_PHD inline bool patch_scan(const Src& src, PatchOut& o, PatchScratch& w, int6
       } else if (is_make) {
         have_pv = true;
         vtag = PV_CHILD;
-        vdt = action == 0 ? 0 : action == 2 ? 1 : action == 4 ? 2 : 3;
+        vdt = pv_obj_type(action);
         v0 = idc; v1 = ida;
         pk_c = idc; pk_a = ida;
       }

@@ -412,10 +412,12 @@ void gen_finish(Gen& g) {
     h.bloom = g.bloom;
     m.have.push_back(std::move(h));
   }
+  // membership through a hash set: a first sync of a long history sends every change
+  std::unordered_set<Hash32, Hash32Hasher> sent(s.sent_hashes.begin(), s.sent_hashes.end());
   std::vector<Hash32> new_hashes;
   for (size_t i : g.to_send) {
     ChangeRef c = change_at(g.doc, i);
-    if (contains(s.sent_hashes, c.hash)) continue;
+    if (sent.count(c.hash)) continue;
     m.changes.push_back({c.data, c.len});
     new_hashes.push_back(c.hash);
   }
@@ -424,7 +426,7 @@ void gen_finish(Gen& g) {
   if (!m.changes.empty()) {  // sentHashes = copyObject(sentHashes) + the hashes sent
     s.sent_is_array = false;
     for (const Hash32& h : new_hashes)
-      if (!contains(s.sent_hashes, h)) s.sent_hashes.push_back(h);
+      if (sent.insert(h).second) s.sent_hashes.push_back(h);
   }
   s.last_sent_heads = g.our_heads;
 }

@@ -79,7 +79,7 @@ function loadChanges(backend, changes) {
 const PR = {ACTOR: 1, CLOCK: 2, OBJ: 3, KEY: 4, PROP: 5, INSERT: 6, MULTI: 7, UPDATE: 8, REMOVE: 9}
 const PV = {NULL: 1, FALSE: 2, TRUE: 3, STR: 4, UINT: 5, INT: 6, F64: 7, COUNTER: 8, TIMESTAMP: 9, BYTES: 10, CHILD: 11}
 const NAMED_DT = {5: 'uint', 6: 'int', 7: 'float64', 8: 'counter', 9: 'timestamp'}
-const OBJ_TYPES = ['map', 'list', 'text', 'table']
+const OBJ_TYPES = ['map', 'list', 'text', 'table', undefined, null]  // 4: null action, 5: unknown even action
 const utf8 = new TextDecoder('utf-8')
 
 // Wire form (am_patch.h): PatchHdr2 (48 B: magic, status, arg0, arg1, maxOp, nbytes, pad) + stream

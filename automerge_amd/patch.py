@@ -18,7 +18,7 @@ PR_ACTOR, PR_CLOCK, PR_OBJ, PR_KEY, PR_PROP, PR_INSERT, PR_MULTI, PR_UPDATE, PR_
 (PV_NULL, PV_FALSE, PV_TRUE, PV_STR, PV_UINT, PV_INT, PV_F64, PV_COUNTER, PV_TIMESTAMP, PV_BYTES,
  PV_CHILD) = range(1, 12)
 NAMED_DT = {PV_UINT: "uint", PV_INT: "int", PV_F64: "float64", PV_COUNTER: "counter", PV_TIMESTAMP: "timestamp"}
-OBJ_TYPES = ("map", "list", "text", "table")
+OBJ_TYPES = ("map", "list", "text", "table", None, None)  # 4: undefined (null action), 5: null (unknown even action)
 
 # errors getPatch throws (am_patch.h PATCH_*)
 PATCH_E_FLOAT_LEN, PATCH_E_UNKNOWN_COUNTER = 31, 32

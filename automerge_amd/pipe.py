@@ -2,11 +2,14 @@
 Backend.load + Backend.applyChanges per document, from host memory back to host memory. The H2D
 copy of the next batch and the D2H copy of the previous one overlap the kernels of the current one.
 
-    caps = pipe.caps_for(batch_staged_with_Batch, docs=..., ...)   # sizes from a representative batch
-    p = Pipeline(caps)
-    for arena, chunks, docs in batches:                            # pinned inputs (pinned())
-        p.submit(arena, chunks, docs, summary, out, patches)       # pinned outputs
+    p = Pipeline(arena_bytes, chunks, docs, ws_bytes, out_bytes, patch_bytes, fast_lds, slots=3)
+    for arena, chunks, docs in batches:                            # pinned inputs (pinned_copy)
+        p.submit(arena, chunks, docs, summary, out, patches)       # pinned outputs (Pinned views)
     totals = p.drain()                                             # every batch is home
+
+The capacities are per batch (bench.py sizes them from one staged batch: Batch.workspace_bytes()
+and the output lengths of a run, with headroom). A document whose merged chunk or patch log does
+not fit the device arenas or the caller's `out` / `patches` reports AM_U_CAPACITY in its summary.
 
 Each document's merged chunk is out[s.out_off : s.out_off + s.out_len] and its patch log (wire form,
 automerge_amd/patch.py) patches[s.patch_off : s.patch_off + s.patch_len] for its summary s.

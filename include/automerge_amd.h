@@ -257,7 +257,11 @@ void am_host_free(void *p);
 am_pipe *am_pipe_create(am_engine *eng, const am_pipe_caps *caps, am_error *err);
 void am_pipe_destroy(am_pipe *p);
 /* Enqueues batch `ticket` (returned in *ticket): H2D, the pipeline of am_batch_run, compaction and
- * D2H into summary[ndocs], out[..] and patches[..]. Blocks only while every slot is in flight. */
+ * D2H into summary[ndocs], out[..] and patches[..]. The output arenas hold min(out_cap, caps.out_bytes)
+ * and min(patch_cap, caps.patch_bytes) bytes: a document whose chunk or log does not fit reports
+ * AM_U_CAPACITY in its summary. Blocking: the submit queues the copies home of the previous batch,
+ * which waits on the host for that batch's kernels (their output sizes); when every slot is in
+ * flight it also waits for the oldest batch's copies home before reusing its slot. */
 int am_pipe_submit(am_pipe *p, const uint8_t *arena, uint64_t arena_len, const am_chunk_desc *chunks, uint32_t nchunks,
                    const am_doc_desc *docs, uint32_t ndocs, am_doc_summary *summary, uint8_t *out, uint64_t out_cap,
                    uint8_t *patches, uint64_t patch_cap, uint64_t *ticket, am_error *err);

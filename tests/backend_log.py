@@ -9,12 +9,7 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 FILES = ["sync", "sync_random", "objmeta", "backend", "test", "text", "table", "errors"]
 # Scenarios where this engine knowingly differs from the reference, with the reason. Each must still
 # fail loudly with an "automerge_amd: unsupported" error (never a silently different result).
-KNOWN_DIVERGENT = {
-    # a null action: the reference encodes the all-null action column as no bytes, so its document
-    # then reads as having no ops at all (readNextDocOp, new.js:675-677; RLEEncoder.finish,
-    # encoding.js:778-782) and the applyChanges patch holds an object of type undefined
-    ("errors", "null action"),
-}
+KNOWN_DIVERGENT = set()  # none: the last one (a null action) is restated since round 4
 PURE = {"encodeSyncMessage", "decodeSyncMessage", "encodeSyncState", "decodeSyncState", "initSyncState"}
 UNDEF = object()
 

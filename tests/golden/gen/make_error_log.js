@@ -203,6 +203,26 @@ scenario('unknown columns in a change', () => applySeq(B.init(), [[change({actor
     [0xa2, [0x7f, 5]], [0xb5, [0x7f].concat(str('zz'))]]}))]})]]))
 scenario('uint value of 2^40 and startOp beyond 2^31', () => applySeq(B.init(), [[setKey({v: 2 ** 40, startOp: 2 ** 32 + 5})]]))
 
+// make-like actions without a known type: `op[actionIdx] % 2 === 0` holds for a null action (type
+// undefined) and for an even action beyond ACTIONS (type null), new.js:886-897, 972-976
+const twoOps = (act, o = {}) => change(Object.assign({actor: A, seq: 1, startOp: 1, cols: [
+  [0x15, sleb(-2).concat(str('a'), str('k'))], [0x34, [2]], [0x42, act], [0x56, [0x7e, 0x13, 0]], [0x57, [5]],
+  [0x70, [2, 0]]]}, o))
+const inObj = (prev, ctr, o = {}) => change(Object.assign({actor: A, seq: 2, startOp: 3, deps: [chash(prev)], cols: [
+  [0x01, [0x7f, 0]], [0x02, [0x7f, ctr]], [0x15, [0x7f].concat(str('p'))], [0x34, [1]], [0x42, [0x7f, 1]],
+  [0x56, [0x7f, 0x13]], [0x57, [9]], [0x70, [0x7f, 0]]]}, o))
+scenario('null action next to a set, then a key inside its object', () => {
+  const c1 = twoOps([0x7f, 1, 0, 1])
+  const d = applySeq(B.init(), [[c1], [inObj(c1, 2)]])
+  B.getPatch(B.load(B.save(d)))
+})
+scenario('unknown even action, then a key inside its object', () => {
+  const c1 = twoOps([0x7e, 1, 8])
+  const d = applySeq(B.init(), [[c1], [inObj(c1, 2)]])
+  B.getPatch(B.load(B.save(d)))
+})
+scenario('unknown even action alone', () => { const d = applySeq(B.init(), [[withAction([0x7f, 10], 1)]]); B.getPatch(B.load(B.save(d))) })
+
 // load() of malformed documents
 const doc1 = () => { const d = Real.applyChanges(Real.init(), [good1])[0]; return Real.save(d) }
 scenario('load: change chunk instead of a document', () => { B.load(good1) })

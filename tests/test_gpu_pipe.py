@@ -89,3 +89,18 @@ def test_pipeline_capacities():
     short.drain(1)
     st = sm["status"]
     assert (st == 0).sum() > 50 and (st == 106).sum() > 50
+    # caller buffers smaller than the device arenas: the documents past them report AM_U_CAPACITY,
+    # and every document reported as merged lies inside the buffers with the batch path's bytes
+    roomy = pipe.Pipeline(len(a), len(c), len(d), ws, 1 << 20, 1 << 20, kinfo["k_doc_fast_lds_per_doc"], slots=2)
+    small_out, small_patch = pipe.Pinned(64 * 1024), pipe.Pinned(24 * 1024)
+    roomy.submit(pa.arr, pc.arr, pd.arr, sm, small_out.u8, small_patch.u8)
+    roomy.drain(1)
+    st = sm["status"]
+    assert (st == 0).sum() > 20 and (st == 106).sum() > 20 and set(np.unique(st)) <= {0, 106}
+    ref.run()
+    ref.sync()
+    res = ref.results()
+    for i in np.flatnonzero(st == 0):
+        o, n = int(sm["out_off"][i]), int(sm["out_len"][i])
+        assert o + n <= 64 * 1024 and int(sm["patch_off"][i]) + int(sm["patch_len"][i]) <= 24 * 1024
+        assert bytes(small_out.u8[o:o + n]) == ref.doc_output(int(i), res[i])
