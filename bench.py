@@ -32,25 +32,71 @@ HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
 CPU_REF_JSON = os.path.join(ROOT, "profiles", "cpu_reference_node.json")
 
 
-def cpu_baseline(arena, chunks, docs, seconds=12.0, ops_per_doc=60, name="C4"):
-    """The oracle (CPU restatement of the reference algorithm, oracle/) timed on one host core over
-    a bounded sample of the same documents: ops merged per second (load + applyChanges + save)."""
+def _oracle_sample(args):
+    """load + applyChanges + save of documents [lo, hi) of the bench's arrays by the oracle for at most
+    `seconds`; returns (documents done, seconds)."""
+    arena, chunks, docs, lo, hi, seconds = args
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as O
     import workload
     n = 0
-    ops = 0
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds and n < len(docs):
-        base, changes = workload.doc_chunks(arena, chunks, docs, n)
+    while time.perf_counter() - t0 < seconds and lo + n < hi:
+        base, changes = workload.doc_chunks(arena, chunks, docs, lo + n)
         d = O.Doc.load(base) if base else O.Doc.init()
         d.apply(changes)
         d.save()
-        ops += ops_per_doc
         n += 1
-    dt = time.perf_counter() - t0
-    return {"value": ops / dt, "unit": "ops/s", "cores": 1, "kind": "port", "host_cpus": os.cpu_count(),
-            "sample": "%d %s documents (load + applyChanges + save) by oracle/liboracle.so, 1 thread, %.1f s" % (n, name, dt)}
+    return n, time.perf_counter() - t0
+
+
+def cpu_baseline(arena, chunks, docs, seconds=6.0, ops_per_doc=60, name="C4", procs=None):
+    """The oracle (CPU restatement of the reference algorithm, oracle/) timed on the host over a
+    bounded sample of the same documents: ops merged per second (load + applyChanges + save), on one
+    core and on `procs` cores at once (one process each, disjoint documents)."""
+    import multiprocessing as mp
+    procs = procs or min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16 per GPU
+    n1, t1 = _oracle_sample((arena, chunks, docs, 0, len(docs), seconds))
+    per = max(1, len(docs) // procs)
+    with mp.get_context("fork").Pool(procs) as pool:
+        res = pool.map(_oracle_sample, [(arena, chunks, docs, k * per, (k + 1) * per, seconds) for k in range(procs)])
+    nall = sum(r[0] for r in res)
+    tall = max(r[1] for r in res)
+    return {"value": n1 * ops_per_doc / t1, "unit": "ops/s", "cores": 1, "kind": "port", "host_cpus": os.cpu_count(),
+            "sample": "%d %s documents (load + applyChanges + save) by oracle/liboracle.so, 1 thread, %.1f s" % (n1, name, t1),
+            "all_cores": {"value": nall * ops_per_doc / tall, "unit": "ops/s", "cores": procs,
+                          "sample": "%d %s documents on %d processes at once, %.1f s" % (nall, name, procs, tall)}}
+
+
+def pinned_digest(docs):
+    """The digest of the whole C4 job of `docs` documents computed by the oracle in the build
+    container (tools/pin_c4_digest.py -> tests/golden/c4_digest.json), or None."""
+    try:
+        rec = json.load(open(os.path.join(ROOT, "tests", "golden", "c4_digest.json")))
+    except (OSError, ValueError):
+        return None
+    r = rec.get(str(docs))
+    return int(r["digest"]) if r else None
+
+
+def decode_alg_bytes(arena, chunks, docs, sample=256):
+    """Algorithmic decode bytes of SURVEY 8(d) per document, over a sample: the encoded input read
+    plus the SoA written -- 44 B per op row (11 u32 fields), 1 B insert flag, 8 B per pred/succ
+    entry and the raw value bytes (the decode's rows and entries are the merged document's ops and
+    succ entries: C4 has no deletions). Returns (input bytes, SoA bytes) per document."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    import workload
+    n = min(sample, len(docs))
+    inb = soa = 0
+    for i in range(n):
+        base, changes = workload.doc_chunks(arena, chunks, docs, i)
+        inb += (len(base) if base else 0) + sum(len(c) for c in changes)
+        d = O.Doc.load(base) if base else O.Doc.init()
+        d.apply(changes)
+        e = O.export(d.save())
+        soa += 45 * e["nops"] + 8 * e["nsucc"] + e["val_bytes"]
+    return inb / n, soa / n
 
 
 def kernel_source_digest():
@@ -121,14 +167,21 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # AM_BENCH_DEVICE / AM_DIST_BACKEND=gloo: every rank on one GPU with a CPU exchange (the N>1
+    # rehearsal of tests/test_gpu_bench_ranks.py; RCCL refuses two ranks on one device)
+    local = int(os.environ.get("AM_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    backend = os.environ.get("AM_DIST_BACKEND", "nccl")
     import numpy as np
     import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend=backend)
     torch.cuda.set_device(local)
+    xdev = "cuda" if backend == "nccl" else "cpu"
 
     from automerge_amd import shard
     from automerge_amd.batch import WANT_DIFF, Batch
@@ -276,7 +329,7 @@ def main():
             return o, (p if not args.no_patch else None)
 
     nerr = int((statuses != 0).sum())
-    tot, _ = shard.exchange(dist, [D, ops_rank, nerr, out_bytes, digest or 0], "cuda")
+    tot, _ = shard.exchange(dist, [D, ops_rank, nerr, out_bytes, digest or 0], xdev)
     # correctness spot check against the oracle (outside the timed region): merged bytes and patch
     checked = 0
     if args.check and rank == 0:
@@ -306,11 +359,23 @@ def main():
     achieved = alg_launch / (t_doc * 1e-3) / 1e9 if t_doc else None
     tr = (measured_traffic(extra.get("batch_docs")) if args.mode == "pipe" and args.workload == "c4" and not args.no_patch
           else None)
-    if tr is not None and t_doc:
-        # decode GB/s: HBM bytes the document kernel fetches per launch / its time
-        extra["decode_GBps"] = 2 * tr["fetch_size_kib"] * 1024 / (t_doc * 1e-3) / 1e9
+    if t_doc:
+        # decode GB/s: algorithmic decode bytes of one launch (encoded input read + SoA
+        # written, per document from an oracle-decoded sample) / the document kernel's time; the
+        # kernel does the merge, encode and patch in the same time, so this is a lower bound
+        din, dsoa = decode_alg_bytes(arena, chunks, docs)
+        per_launch = (D / (nb if args.mode == "pipe" else 1)) * (din + dsoa)
+        extra["decode_GBps"] = per_launch / (t_doc * 1e-3) / 1e9
         extra["decode_frac_of_hbm_peak"] = extra["decode_GBps"] / HBM_PEAK_GBPS
+        extra["decode_bytes_per_doc"] = {"input": din, "soa": dsoa}
+    if tr is not None and t_doc:
+        extra["fetch_GBps"] = 2 * tr["fetch_size_kib"] * 1024 / (t_doc * 1e-3) / 1e9  # measured HBM reads (PMC)
     cpu = None if args.no_cpu_baseline else cpu_baseline(arena, chunks, docs, ops_per_doc=per_doc, name=args.workload.upper())
+    # the whole job against the oracle's digest of every document (tests/golden/c4_digest.json)
+    want = pinned_digest(tot[0]) if args.workload == "c4" and digest is not None else None
+    if want is not None:
+        extra["digest_pinned"] = {"expected": want, "match": tot[4] == want,
+                                  "how": "oracle load + applyChanges + save of all %d documents (tools/pin_c4_digest.py)" % tot[0]}
     wl = {"c4": "C4 1M-document job: load base doc + applyChanges of 12 concurrent changes (4 actors x 3), 60 ops/doc",
           "c2": "C2: applyChanges of 3 changes (10 map/counter/string sets + 2 concurrent inc/overwrite), 14 ops/doc"}
     what = "H2D + merge + applyChanges patch + D2H (pipelined)" if args.mode == "pipe" else "kernels, inputs resident in HBM"
@@ -338,6 +403,8 @@ def main():
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+    if want is not None and tot[4] != want:
+        sys.exit("bench: the job's digest %d differs from the oracle's %d" % (tot[4], want))
 
 
 if __name__ == "__main__":

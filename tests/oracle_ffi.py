@@ -257,3 +257,35 @@ def sync_select(hashes, deps, filters):
     out = C.create_string_buffer(max(n, 1))
     lib().oc_sync_select(n, b"".join(hashes), off.ctypes.data, idx.ctypes.data, len(filters), fl, fn, out)
     return list(out.raw[:n])
+
+
+# ---- flat export of a saved document (oc_doc_export) ----
+class _OcOp(C.Structure):
+    _fields_ = [("obj_ctr", C.c_int64), ("key_ctr", C.c_int64), ("id_ctr", C.c_int64), ("action", C.c_int64),
+                ("val_len", C.c_int64), ("obj_actor", C.c_int32), ("key_actor", C.c_int32), ("id_actor", C.c_int32),
+                ("insert", C.c_int32), ("key_len", C.c_int32), ("val_n", C.c_uint32), ("nsucc", C.c_uint32),
+                ("succ_off", C.c_uint32), ("key", C.c_void_p), ("val", C.c_void_p)]
+
+
+class _OcExport(C.Structure):
+    _fields_ = [("nops", C.c_size_t), ("ops", C.POINTER(_OcOp)), ("succ_ctr", C.c_void_p), ("succ_actor", C.c_void_p),
+                ("nactors", C.c_size_t), ("actors", C.c_void_p), ("actor_lens", C.c_void_p), ("nchg", C.c_size_t),
+                ("chg_actor", C.c_void_p), ("chg_seq", C.c_void_p), ("priv", C.c_void_p)]
+
+
+def export(data):
+    """Counts of a saved document's ops: {nops, nsucc, val_bytes, nchg} (oc_doc_export)."""
+    L = lib()
+    L.oc_doc_export.restype = C.POINTER(_OcExport)
+    L.oc_doc_export.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
+    L.oc_export_free.argtypes = [C.POINTER(_OcExport)]
+    err = C.create_string_buffer(256)
+    e = L.oc_doc_export(bytes(data), len(data), err, 256)
+    if not e:
+        raise OracleError(err.value.decode(errors="replace"))
+    x = e.contents
+    out = {"nops": int(x.nops), "nchg": int(x.nchg),
+           "nsucc": sum(int(x.ops[i].nsucc) for i in range(x.nops)),
+           "val_bytes": sum(int(x.ops[i].val_n) for i in range(x.nops))}
+    L.oc_export_free(e)
+    return out
