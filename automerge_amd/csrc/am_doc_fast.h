@@ -53,6 +53,7 @@
 #define FD_LDS_CAP (24 * 1024)
 #define FD_DOCS_PER_WG 4
 #define FD_NULL ((int32_t)0x80000000)
+#define FD_DIFF_SCRATCH 1216  // fast_diff's tables in the cells region
 
 // misc region (byte offsets). Tables whose phases never overlap share a union slot:
 //   U1: {BHIDX, KIDX} (headers .. heads) | {IDT} (opId sort .. list elements) | {NSORT, BENT} (succ)
@@ -117,6 +118,7 @@ __host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t n
   // (a larger image fails the encoder's capacity check: the document then goes to k_doc)
   const uint32_t out = 64 + 40 * b.A + 42 * b.H + 25 * 12 + span;
   if (out > cells) cells = out;
+  if (b.P == 2 && cells < FD_DIFF_SCRATCH) cells = FD_DIFF_SCRATCH;  // fast_diff's tables
   F.cells = take(cells);
   F.cells_cap = cells;
   F.total = o;
@@ -638,14 +640,46 @@ __device__ __forceinline__ bool fd_value(const uint8_t* in, int32_t vlen, uint32
   return true;
 }
 
+// Row values of the merge that fast_diff reads back after the encode, in misc tables whose phases
+// are over by then (U1, U2: opId sort .. succ merge; OWN .. DPC: refs .. entries; FC .. LON: RGA and
+// succ merge; DEPD, DOWN: queue). FM_OPR (opId rank of each row) and FM_RANKDP stay as they are.
+struct FdRec {
+  uint32_t* key; int32_t* objc; int32_t* idc; int32_t* vlen;  // U1: 4 x 256 B
+  uint16_t* voff;                                             // U2 + 0
+  uint8_t *krow, *sck, *sok;                                  // U2 + 128 / 192 / 256 (by output position)
+  int8_t* obja; uint8_t *ida, *krank;                         // U2 + 320 / 384 / 448
+  uint32_t* bcs;                                              // OWN .. DPC (256 B): base change row -> seq
+  int8_t* elem; uint8_t *act, *flags;                         // FC / NS / LON
+  uint8_t *bca, *adp;                                         // DEPD: base change row -> actor; DOWN: change -> author
+};
+__device__ __forceinline__ FdRec fd_rec(uint8_t* M) {
+  FdRec P;
+  P.key = reinterpret_cast<uint32_t*>(M + FM_U1);
+  P.objc = reinterpret_cast<int32_t*>(M + FM_U1 + 256);
+  P.idc = reinterpret_cast<int32_t*>(M + FM_U1 + 512);
+  P.vlen = reinterpret_cast<int32_t*>(M + FM_U1 + 768);
+  P.voff = reinterpret_cast<uint16_t*>(M + FM_U2);
+  P.krow = M + FM_U2 + 128; P.sck = M + FM_U2 + 192; P.sok = M + FM_U2 + 256;
+  P.obja = reinterpret_cast<int8_t*>(M + FM_U2 + 320); P.ida = M + FM_U2 + 384; P.krank = M + FM_U2 + 448;
+  P.bcs = reinterpret_cast<uint32_t*>(M + FM_OWN);
+  P.elem = reinterpret_cast<int8_t*>(M + FM_FC); P.act = M + FM_NS; P.flags = M + FM_LON;
+  P.bca = M + FM_DEPD; P.adp = M + FM_DOWN;
+  return P;
+}
+static_assert(FM_CANON == FM_OWN + 64 && FM_RANKC == FM_CANON + 64 && FM_DPC == FM_RANKC + 64, "bcs spans OWN .. DPC");
+static_assert(FM_U2 + 512 <= FM_OUTC, "U2 records");
+
 // The patch Backend.applyChanges returns (new.js:1796-1871), written by the whole wave in wire form
-// (am_patch.h) for the common shape of a batch of concurrent edits: every applied op is a `set` of
-// a map key of the root object, or a `set` that inserts a list element into one list/text object
-// whose make op is the only visible value of its root key. For that shape the serial replay of
-// am_diff.h reduces to closed forms:
-//   * a touched key's props are its visible ops in the merged document (each mergeDocChangeOps
-//     call over a key rewrites props[key] from every op of the key, new.js:884-1040, and the last
-//     call sees the final set);
+// (am_patch.h) for the common shape of a batch of concurrent edits: every applied op is a `set` or
+// an `inc` of a map key of the root object, or a `set` that inserts a list element into one
+// list/text object whose make op is the only visible value of its root key. For that shape the
+// serial replay of am_diff.h reduces to closed forms:
+//   * props[key] comes from the last mergeDocChangeOps call over the key (each call resets it at the
+//     key's first op, new.js:1037): the key's ops in opId order, except that when the call goes on
+//     to a later key of the same change stream (new.js:1125-1128), the key's doc ops with an opId
+//     above its last change op are taken without updatePatchProperty (new.js:1225-1230);
+//   * of those ops a `set` without succ is a value; a counter `set` whose succs are all `inc` ops of
+//     the key taken in that call is its value plus theirs (counterStates, new.js:937-965);
 //   * an insert's index is the number of visible elements of the list that precede it in the
 //     merged order and exist when it applies (base elements with a row without succ, earlier
 //     inserts of the call): a popcount over row masks;
@@ -654,36 +688,75 @@ __device__ __forceinline__ bool fd_value(const uint8_t* in, int32_t vlen, uint32
 //     type -- a segmented run over the insert lanes;
 //   * setupPatches links the list to the root through its key (new.js:1461-1528).
 // Anything else returns false before any result is committed and the document goes to k_doc,
-// whose lane-0 replay covers every shape. Scratch: 320 bytes at PS (the output image has left).
+// whose lane-0 replay covers every shape. Scratch: FD_DIFF_SCRATCH bytes at PS (the output image has
+// left).
 __device__ __forceinline__ bool fast_diff(const uint8_t* IN, uint8_t* PS, uint32_t ps_cap, uint8_t* out, uint64_t out_cap,
-                                          uint32_t R, uint32_t nb, uint32_t NOUT, uint32_t NA, uint32_t NC, uint32_t nbc,
-                                          uint32_t k_row, uint32_t sc_k, bool r_chg, int32_t r_act, bool keyed, int32_t r_key,
-                                          uint32_t r_krank, int32_t r_objc, int32_t r_obja, uint64_t r_objkey, bool r_ins,
-                                          int32_t r_idc, int32_t r_ida, int32_t r_vlen, uint32_t r_voff, int32_t r_elem,
-                                          uint32_t a_len, uint32_t a_off, uint32_t bc_actor, int64_t bc_seq, uint32_t a_dp,
+                                          uint8_t* M, uint32_t R, uint32_t nb, uint32_t NOUT, uint32_t NA, uint32_t NC,
+                                          uint32_t nbc, uint32_t N, const int32_t* OUTC, const uint8_t* OUTA, const uint32_t* RO,
                                           const ChgHdrC* chh) {
+  const FdRec P = fd_rec(M);
   const uint32_t l = lane();
-  bool pbad = ps_cap < 512;
+  const bool isrow_ = l < R;
+  const int32_t r_key = isrow_ ? (int32_t)P.key[l] : FD_NULL, r_objc = isrow_ ? P.objc[l] : FD_NULL;
+  const int32_t r_idc = isrow_ ? P.idc[l] : 0, r_vlen = isrow_ ? P.vlen[l] : FD_NULL;
+  const uint32_t r_voff = isrow_ ? P.voff[l] : 0u;
+  const int32_t r_obja = isrow_ ? P.obja[l] : -1, r_ida = isrow_ ? P.ida[l] : 0;
+  const uint32_t r_krank = isrow_ ? P.krank[l] : 0u, r_opr = isrow_ ? M[FM_OPR + l] : 0u;
+  const int32_t r_elem = isrow_ ? P.elem[l] : -1, r_act = isrow_ ? (int32_t)P.act[l] : 0;
+  const uint32_t fl = isrow_ ? P.flags[l] : 0u;
+  const bool r_chg = fl & 1, r_ins = (fl & 2) != 0, keyed = (fl & 4) != 0;
+  const uint64_t r_objkey = (!isrow_ || r_objc == FD_NULL) ? 0ull
+                                                          : (((uint64_t)(uint32_t)r_objc + 1) << 6) | (r_obja < 0 ? 0u : M[FM_RANKDP + r_obja]);
+  const uint32_t k_row = l < NOUT ? P.krow[l] : 0u, sc_k = l < NOUT ? P.sck[l] : 0u, so_k = l < NOUT ? P.sok[l] : 0u;
+  const uint32_t bc_actor = l < nbc ? P.bca[l] : 0u;
+  const int64_t bc_seq = l < nbc ? (int64_t)P.bcs[l] : 0;
+  const uint32_t a_dp = l < N ? P.adp[l] : 0u;
+  const uint32_t a_off = l < NA ? RO[2 * M[FM_DP2REF + l]] : 0u, a_len = l < NA ? RO[2 * M[FM_DP2REF + l] + 1] : 0u;
+  bool pbad = ps_cap < FD_DIFF_SCRATCH;
   if (__any(pbad)) return false;
   uint8_t* const POS = PS;        // row -> output position
   uint8_t* const SCR = PS + 64;   // row -> succ count in the merged document
   uint8_t* const EV = PS + 128;   // element (insert row) -> visible
-  uint8_t* const TCH = PS + 192;  // key rank -> set by a change op of the call
+  uint8_t* const TCH = PS + 192;  // key rank -> set / inc by a change op of the call
   uint32_t* const LASTC = reinterpret_cast<uint32_t*>(PS + 256);  // doc actor -> its last change row
+  uint32_t* const LASTK = reinterpret_cast<uint32_t*>(PS + 512);  // key rank -> 1 + its last change row
+  uint8_t* const CONT = PS + 768;  // key rank -> its last call goes on to a later key
+  uint8_t* const LOPR = PS + 832;  // key rank -> opId rank of its last change op
+  uint32_t* const COV = reinterpret_cast<uint32_t*>(PS + 896);  // row -> counter sets whose succ lists name it
   const bool isrow = l < R;
   EV[l] = 0;
   TCH[l] = 0;
   LASTC[l] = 0;
+  LASTK[l] = 0;
+  CONT[l] = 0;
+  COV[l] = 0;
   wsync();
   if (l < NOUT) { POS[k_row] = (uint8_t)l; SCR[k_row] = (uint8_t)(sc_k > 255 ? 255 : sc_k); }
-  const bool set_root = r_chg && r_act == 1 && keyed && r_objc == FD_NULL;
+  const bool mod_root = r_chg && (r_act == 1 || r_act == 5) && keyed && r_objc == FD_NULL;
   const bool list_ins = r_chg && r_act == 1 && !keyed && r_ins;
-  pbad |= r_chg && !(set_root || list_ins);
-  if (set_root) TCH[r_krank] = 1;
+  pbad |= r_chg && !(mod_root || list_ins);
+  if (mod_root) {
+    TCH[r_krank] = 1;
+    atomicMax(&LASTK[r_krank], l + 1);
+  }
   wsync();
   if (__any(pbad)) return false;
+  // the call that holds a key's last change op goes on to the next change row (its stream successor)
+  // when that row is by the same author, in the root, not an insert, with a greater key
+  {
+    const uint32_t nx = (l + 1) & 63;
+    const int32_t n_ida = __shfl(r_ida, nx, 64), n_objc = __shfl(r_objc, nx, 64);
+    const uint32_t n_kr = __shfl(r_krank, nx, 64);
+    const int32_t n_chg = __shfl((int32_t)r_chg, nx, 64), n_ins = __shfl((int32_t)r_ins, nx, 64);
+    const int32_t n_keyed = __shfl((int32_t)keyed, nx, 64);
+    if (mod_root && LASTK[r_krank] == l + 1) {
+      CONT[r_krank] = (l + 1 < R && n_chg && n_ida == r_ida && !n_ins && n_objc == FD_NULL && n_keyed && n_kr > r_krank) ? 1 : 0;
+      LOPR[r_krank] = (uint8_t)r_opr;
+    }
+  }
   // visible elements: an element is visible while one of its rows has no succ (new.js:50-192)
   if (isrow && !r_chg && r_elem >= 0 && SCR[l] == 0) EV[r_elem] = 1;
+  wsync();
   // the list object of the inserts: exactly one
   const uint64_t mli = __ballot(list_ins);
   const uint32_t f0 = mli ? ctz64(mli) : 0u;
@@ -702,9 +775,78 @@ __device__ __forceinline__ bool fast_diff(const uint8_t* IN, uint8_t* PS, uint32
                        (m_act != 2 && m_act != 4) || SCR[mrow] != 0 || TCH[m_kr]);
     pbad |= isrow && r_objc == FD_NULL && keyed && r_krank == m_kr && l != mrow && SCR[l] == 0;
   }
-  // the rows of a touched key are plain sets (no child objects, no increments), keys non-empty
+  // the rows of a touched key are sets and increments (no child objects), keys non-empty
   const bool touched = isrow && keyed && r_objc == FD_NULL && TCH[r_krank];
-  pbad |= touched && (r_act != 1 || (r_key & 255) == 0);
+  pbad |= touched && ((r_act != 1 && r_act != 5) || (r_key & 255) == 0);
+  // ops of a touched key that its last call hands to updatePatchProperty
+  const bool taken = touched && !(CONT[r_krank] && r_opr > LOPR[r_krank]);
+  if (__any(pbad)) return false;
+
+  // ---- counters (new.js:937-965): lane per succ entry of the merged document (entry q of output
+  // position p = OWNE[q]); a counter set taken by its key's last call shows its value plus its
+  // increments when every succ is an increment of the key that the call takes ----
+  uint8_t* const OWNE = PS + 1152;  // succ entry -> output position of its owner
+  const bool any_inc = __any(touched && r_act == 5);
+  const uint32_t kr = k_row;        // output lane: its row
+  const int32_t k_act = __shfl(r_act, kr, 64), k_vlen = __shfl(r_vlen, kr, 64);
+  const int32_t k_touched = __shfl((int32_t)touched, kr, 64), k_taken = __shfl((int32_t)taken, kr, 64);
+  const bool k_counter = l < NOUT && k_touched && k_taken && k_act == 1 && sc_k > 0 && k_vlen != FD_NULL && (k_vlen & 15) == 8;
+  int64_t cnt_sum = 0;
+  bool cnt_done = false;
+  if (any_inc) {
+    uint32_t nsucc_all;
+    excl_add(l < NOUT ? sc_k : 0u, nsucc_all);
+    if (l < NOUT)
+      for (uint32_t j = 0; j < sc_k; j++) OWNE[so_k + j] = (uint8_t)l;
+    wsync();
+    const bool isent = l < nsucc_all;
+    const uint32_t own = isent ? OWNE[l] : 0u;
+    const int32_t ec = isent ? OUTC[l] : 0;
+    const int32_t ea = isent ? (int32_t)OUTA[l] : -1;
+    int32_t tgt = -1;  // the row with the entry's opId
+    for (uint32_t j = 0; j < R; j++) {
+      const int32_t jc = wave::bcast(r_idc, (int)j), ja = wave::bcast(r_ida, (int)j);
+      if (isent && jc == ec && ja == ea) tgt = (int32_t)j;
+    }
+    pbad |= isent && tgt < 0;
+    const uint32_t tu = tgt < 0 ? 0u : (uint32_t)tgt;
+    const int32_t o_counter = __shfl((int32_t)k_counter, own, 64);
+    const uint32_t o_kr = __shfl(r_krank, __shfl(kr, own, 64), 64);
+    const int32_t t_act = __shfl(r_act, tu, 64), t_vlen = __shfl(r_vlen, tu, 64), t_taken = __shfl((int32_t)taken, tu, 64);
+    const uint32_t t_kr = __shfl(r_krank, tu, 64), t_voff = __shfl(r_voff, tu, 64);
+    const int32_t t_keyed = __shfl((int32_t)keyed, tu, 64), t_objc = __shfl(r_objc, tu, 64);
+    const bool inc_of_key = isent && tgt >= 0 && t_act == 5 && t_keyed && t_objc == FD_NULL && t_kr == o_kr;
+    if (isent && o_counter && inc_of_key) atomicAdd(&COV[tu], 1u);
+    int64_t iv = 0;
+    bool ok = isent && o_counter && inc_of_key && t_taken;
+    if (ok) {
+      uint32_t vt, dt;
+      int64_t v1;
+      const uint32_t t15 = t_vlen == FD_NULL ? 0u : ((uint32_t)t_vlen & 15);
+      ok = (t15 == 3 || t15 == 4 || t15 == 8 || t15 == 9) && fd_value(IN, t_vlen, t_voff, vt, dt, iv, v1);
+      pbad |= !ok;  // a non-integer increment (JS adds it as it is): k_doc replays it
+    }
+    // per counter owner: the sum of its increments, and whether any entry is not one (segmented
+    // over the entry lanes of each owner)
+    uint64_t owners = __ballot(k_counter);
+    while (owners) {
+      const uint32_t p = (uint32_t)__builtin_ctzll(owners);
+      owners &= owners - 1;
+      const bool mine = isent && own == p;
+      int64_t sv = mine && ok ? iv : 0;
+      uint32_t sb = mine && !ok ? 1u : 0u;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        sv += __shfl_xor(sv, o, 64);
+        sb += __shfl_xor(sb, o, 64);
+      }
+      if (l == p) { cnt_sum = sv; cnt_done = sb == 0; }
+    }
+  }
+  wsync();
+  // every increment the last call takes is named by exactly one counter set of its key (else:
+  // increment operation for unknown counter, or counterStates rebound -- k_doc replays it)
+  pbad |= taken && r_act == 5 && COV[l] != 1;
   if (__any(pbad)) return false;
 
   // ---- record sizes; segments in stream order: actors, clock, root object, root keys, list ----
@@ -729,21 +871,27 @@ __device__ __forceinline__ bool fast_diff(const uint8_t* IN, uint8_t* PS, uint32
   // root keys (PR_KEY / PR_PROP), output lane p holds the row at position p
   const uint32_t r = k_row;
   const bool outl = l < NOUT;
-  const int32_t k_objc = __shfl(r_objc, r, 64), k_key = __shfl(r_key, r, 64), k_vlen = __shfl(r_vlen, r, 64);
+  const int32_t k_objc = __shfl(r_objc, r, 64), k_key = __shfl(r_key, r, 64);
   const uint32_t k_kr = __shfl(r_krank, r, 64), k_voff = __shfl(r_voff, r, 64);
   const int32_t k_idc = __shfl(r_idc, r, 64), k_ida = __shfl(r_ida, r, 64);
   const bool k_keyed = outl && k_key != FD_NULL && k_objc == FD_NULL;
+  const bool is_m = outl && mli && r == mrow;
   const bool k_tch = k_keyed && (TCH[k_kr] || (mli && k_kr == m_kr));
   const uint32_t p_kr = wave::up1(k_kr, ~0u);
   const bool p_tch = wave::up1((uint32_t)k_tch, 0u) != 0;
   const bool emit_key = k_tch && !(l > 0 && p_tch && p_kr == k_kr);
-  const bool emit_prop = k_tch && SCR[r] == 0;
-  const bool is_m = mli && r == mrow;
+  // the list's make op (the only visible value of its untouched key); a set without succ, or a
+  // counter completed by its increments, that the key's last call takes
+  const bool emit_prop = is_m ? SCR[r] == 0
+                              : k_tch && k_taken && ((k_act == 1 && SCR[r] == 0) || (k_counter && cnt_done));
   uint32_t pvt = 0, pdt = 0;
   int64_t pv0 = 0, pv1 = 0;
   if (emit_prop) {
     if (is_m) { pvt = PV_CHILD; pdt = m_act == 2 ? 1u : 2u; pv0 = lc; pv1 = la; }
-    else pbad |= !fd_value(IN, k_vlen, k_voff, pvt, pdt, pv0, pv1);
+    else {
+      pbad |= !fd_value(IN, k_vlen, k_voff, pvt, pdt, pv0, pv1);
+      if (k_counter) pv0 += cnt_sum;  // {type: 'value', datatype: 'counter', value} (new.js:962-963)
+    }
   }
   const uint32_t klen = (uint32_t)k_key & 255;
   const uint32_t b_key = (emit_key ? 1u + pk_uleb_len(klen) + klen : 0u) +
@@ -1733,6 +1881,24 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   bad |= NSUCC > FD_MAX;
   wsync();
   FD_CHECK();
+  // the row values fast_diff reads after the encode, parked in misc tables the merge is done with
+  // (registers would stay live through the encode and spill)
+  if (kDiff && b.P == 2) {
+    const FdRec P = fd_rec(M);
+    if (isrow) {
+      P.key[l] = (uint32_t)r_key; P.objc[l] = r_objc; P.idc[l] = r_idc; P.vlen[l] = r_vlen;
+      P.voff[l] = (uint16_t)r_voff; P.obja[l] = (int8_t)r_obja; P.ida[l] = (uint8_t)r_ida; P.krank[l] = (uint8_t)r_krank;
+      P.elem[l] = (int8_t)r_elem; P.act[l] = (uint8_t)(r_act < 0 || r_act > 255 ? 255 : r_act);
+      P.flags[l] = (uint8_t)((r_chg ? 1u : 0u) | (r_ins ? 2u : 0u) | (keyed ? 4u : 0u));
+    }
+    if (l < NOUT) { P.krow[l] = (uint8_t)k_row; P.sck[l] = (uint8_t)sc_k; P.sok[l] = (uint8_t)so_k; }
+    if (l < nbc) { P.bca[l] = (uint8_t)bc_actor; P.bcs[l] = (uint32_t)bc_seq; }
+    if (l < N) P.adp[l] = (uint8_t)a_dp;
+    bad |= isrow && r_voff > 0xffff;
+    bad |= l < nbc && (bc_seq < 0 || bc_seq > 0xffffffffLL);
+  }
+  wsync();
+  FD_CHECK();
 
   FPH(10);
   // ---- canonical re-encode into the output image (cells are dead) ----
@@ -1961,9 +2127,8 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   }
   FPH(13);
   if (!kDiff && b.P == 2) return;  // launched without the patch writer: k_doc replays the patch
-  if (kDiff && b.P == 2 && !fast_diff(IN, S + F.cells, F.cells_cap, wsg + L.pwire, L.pwire_cap, R, nb, NOUT, NA, NC, nbc, k_row, sc_k,
-                             r_chg, r_act, keyed, r_key, r_krank, r_objc, r_obja, r_objkey, r_ins, r_idc, r_ida, r_vlen,
-                             r_voff, r_elem, a_len, l < NA ? RO[2 * M[FM_DP2REF + l]] : 0u, bc_actor, bc_seq, a_dp, chh))
+  if (kDiff && b.P == 2 && !fast_diff(IN, S + F.cells, F.cells_cap, wsg + L.pwire, L.pwire_cap, M, R, nb, NOUT, NA, NC, nbc, N,
+                                     OUTC, OUTA, RO, chh))
     return;  // outside the shapes fast_diff covers: k_doc replays the patch (am_diff.h)
   FPH(14);
   if (l < N) chg_state[dd.chg_begin + l] = (int32_t)l;

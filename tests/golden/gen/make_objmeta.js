@@ -165,6 +165,38 @@ function handScenarios() {
   return out
 }
 
+// One change touching several root keys in ascending order is one mergeDocChangeOps call: a doc op
+// of an earlier key with a greater opId than the change's op of that key is taken without
+// updatePatchProperty once the call has moved on to the later key (new.js:1125-1128, 1225-1230);
+// counter increments of concurrent changes, in both actor orders (new.js:937-965).
+function multiKeyScenarios() {
+  const col = require(path.join(REF, 'backend/columnar'))
+  const H = c => col.decodeChangeMeta(col.encodeChange(c), true).hash
+  const out = []
+  const set = (key, value, pred, datatype = 'uint') => ({action: 'set', obj: '_root', key, datatype, value, pred})
+  const inc = (key, value, pred) => ({action: 'inc', obj: '_root', key, datatype: 'int', value, pred})
+  for (const [a, b] of [['aa', 'bb'], ['bb', 'aa']]) {
+    const c0 = {actor: '01', seq: 1, startOp: 1, time: 0, deps: [], ops: [set('a', 1, []), set('cnt', 5, [], 'counter'), set('k1', 1, [])]}
+    const X = {actor: a, seq: 1, startOp: 4, time: 0, deps: [H(c0)], ops: [set('a', 2, ['1@01']), set('b', 3, [])]}
+    const Y = {actor: b, seq: 1, startOp: 4, time: 0, deps: [H(c0)], ops: [set('a', 4, ['1@01'])]}
+    const A = {actor: a, seq: 1, startOp: 4, time: 0, deps: [H(c0)], ops: [inc('cnt', 2, ['2@01']), set('k1', 2, ['3@01'])]}
+    const B = {actor: b, seq: 1, startOp: 4, time: 0, deps: [H(c0)], ops: [inc('cnt', 3, ['2@01']), set('k1', 3, ['3@01'])]}
+    const B2 = {actor: b, seq: 2, startOp: 6, time: 0, deps: [H(B)], ops: [inc('cnt', 7, ['2@01']), set('z', 1, [])]}
+    const e = cs => cs.map(c => col.encodeChange(c))
+    const saved = cs => Backend.save(Backend.applyChanges(Backend.init(), e(cs))[0])
+    const tag = a + b
+    out.push({name: `multikey/${tag}/one-call`, steps: [{op: 'apply', changes: e([c0, Y, X])}]})
+    out.push({name: `multikey/${tag}/load+apply`, steps: [{op: 'load', bytes: saved([c0, Y])}, {op: 'apply', changes: e([X])}]})
+    out.push({name: `counter/${tag}/one-call`, steps: [{op: 'apply', changes: e([c0, A, B])}]})
+    out.push({name: `counter/${tag}/load+apply`, steps: [{op: 'load', bytes: saved([c0, A])}, {op: 'apply', changes: e([B])}]})
+    out.push({name: `counter/${tag}/load+apply2`, steps: [{op: 'load', bytes: saved([c0, A])}, {op: 'apply', changes: e([B, B2])}]})
+    out.push({name: `counter/${tag}/steps`, steps: [{op: 'apply', changes: e([c0])}, {op: 'apply', changes: e([B])},
+      {op: 'apply', changes: e([A, B2])}]})
+  }
+  return out
+}
+const Backend = require(path.join(REF, 'backend'))
+
 function record(sc) {
   return {name: sc.name,
           steps: sc.steps.map(s => s.op === 'load' ? {op: 'load', bytes: hex(s.bytes)} : {op: 'apply', changes: s.changes.map(hex)}),
@@ -172,7 +204,7 @@ function record(sc) {
 }
 
 function main() {
-  const scen = handScenarios().concat(randomScenarios(40, 7001)).map(record)
+  const scen = handScenarios().concat(multiKeyScenarios(), randomScenarios(40, 7001)).map(record)
   const file = path.join(OUT, 'objmeta.json')
   fs.writeFileSync(file, JSON.stringify({scenarios: scen}) + '\n')
   const steps = scen.reduce((a, s) => a + s.results.length, 0)

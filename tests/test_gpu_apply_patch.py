@@ -165,7 +165,53 @@ def test_workload_apply_patch_matches_oracle(kind, first, n):
         assert got == want, i
 
 
-def test_fast_and_general_patch_writers_agree(docs):
+def _first_steps(scenarios):
+    """(base saved bytes | None, changes, expected) of the first apply step of each scenario (after
+    init or load, objectMeta is documentPatch's, so the step stands alone as a batch document)."""
+    out = []
+    for sc in scenarios:
+        prev = None
+        for step, exp in zip(sc["steps"], sc["results"]):
+            if step["op"] == "load":
+                prev = exp
+                continue
+            if "patch" in exp and not (prev and prev.get("pending")):
+                base = bytes.fromhex(prev["save"]) if prev else None
+                out.append((base, [bytes.fromhex(c) for c in step["changes"]], exp, sc["name"]))
+            break
+    return out
+
+
+def test_apply_patch_first_calls_one_batch(objmeta):
+    """The first applyChanges of every objmeta scenario as one batch (k_doc_fast's wave-parallel
+    patch writer where the shape allows, k_doc's replay otherwise) against the reference: concurrent
+    same-key objects, one change over several root keys (the doc ops of an earlier key past the
+    change's op are not in the patch, new.js:1125-1128, 1225-1230), concurrent counter increments
+    in both actor orders (new.js:937-965)."""
+    from automerge_amd import patch as P
+    from automerge_amd.batch import WANT_DIFF, Batch
+    steps = _first_steps(objmeta)
+    b = Batch()
+    b.stage_docs([(base, ch) for base, ch, _, _ in steps], flags=WANT_DIFF)
+    b.run()
+    b.sync()
+    res = b.results()
+    flags = b.fast_flags()
+    bad, graph = [], 0
+    for i, (_, _, exp, name) in enumerate(steps):
+        if int(res[i]["status"]) == 100:  # AM_U_HASH_GRAPH: deps below the loaded heads (per-document path)
+            graph += 1
+            continue
+        assert int(res[i]["status"]) == 0, (name, int(res[i]["status"]))
+        got = _jsonable(P.materialize(b.doc_patch(i), exp["heads"], exp["pending"], exp["patch"]["maxOp"]))
+        if got != exp["patch"]:
+            bad.append((name, bool(flags[i])))
+    fast_hand = [bool(flags[i]) for i, s in enumerate(steps) if s[3].startswith(("multikey/", "counter/"))]
+    assert len(steps) - graph > 100 and sum(fast_hand) >= 4, (graph, fast_hand)
+    assert not bad, (len(bad), bad[:10])
+
+
+def test_fast_and_general_patch_writers_agree(docs, objmeta):
     """The wave-parallel patch writer of k_doc_fast (fast_diff, am_doc_fast.h) against k_doc's serial
     replay (am_diff.h): every golden apply step and seeded C4 / C2 documents staged with WANT_DIFF,
     once with the fast kernel and once without it (AM_FAST=0); the materialized patches must be
@@ -174,7 +220,7 @@ def test_fast_and_general_patch_writers_agree(docs):
     from automerge_amd import patch as P
     import workload
     from automerge_amd.batch import WANT_DIFF, Batch
-    items = [(base, ch) for base, ch, _ in _steps(docs)]
+    items = [(base, ch) for base, ch, _ in _steps(docs)] + [(base, ch) for base, ch, _, _ in _first_steps(objmeta)]
     nc4 = 600
     for kind, first in (("c4", 11), ("c2", 7)):
         arena, chunks, dd, _ = getattr(workload, kind)(first, nc4)
@@ -203,6 +249,7 @@ def test_fast_and_general_patch_writers_agree(docs):
     rg, pg, og, gflags = run(False)
     assert not gflags.any()
     assert flags[-2 * nc4:-nc4].all(), "every C4 document must take the fast patch writer"
+    assert flags[-nc4:].all(), "every C2 document (counters) must take the fast patch writer"
     bad = [i for i in range(len(items)) if pf[i] != pg[i] or of[i] != og[i] or rf[i]["status"] != rg[i]["status"]]
     assert not bad, (int(flags.sum()), bad[:10])
     print("fast patch writer took %d of %d documents" % (int(flags.sum()), len(items)))
