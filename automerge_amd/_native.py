@@ -47,6 +47,18 @@ class DocSummary(C.Structure):
                 ("out_off", C.c_uint64), ("patch_off", C.c_uint64)]
 
 
+class CallInfo(C.Structure):
+    _fields_ = [("max_op", C.c_int64), ("pending", C.c_uint32), ("nheads", C.c_uint32), ("heads", C.c_void_p)]
+
+    def take(self):
+        """(maxOp, heads hex list, pending); frees the heads."""
+        raw = C.string_at(self.heads, 32 * self.nheads) if self.heads else b""
+        if self.heads:
+            lib.am_free(self.heads)
+            self.heads = None
+        return self.max_op, [raw[32 * i:32 * i + 32].hex() for i in range(len(raw) // 32)], self.pending
+
+
 class PipeCaps(C.Structure):
     _fields_ = [("arena_bytes", C.c_uint64), ("chunks", C.c_uint32), ("docs", C.c_uint32), ("ws_bytes", C.c_uint64),
                 ("out_bytes", C.c_uint64), ("patch_bytes", C.c_uint64), ("fast_lds", C.c_uint32), ("slots", C.c_uint32)]
@@ -85,6 +97,7 @@ _sigs = {
     "am_batch_stage_times": (C.c_int, [P, C.POINTER(C.c_float)]),
     "am_batch_workspace_bytes": (C.c_uint64, [P]),
     "am_batch_kernel_info": (C.c_int, [P, P]),
+    "am_batch_doc_plan": (C.c_int, [P, C.c_uint32, P]),
     "am_batch_digest": (C.c_int, [P, C.c_uint64, C.POINTER(C.c_uint64)]),
     "am_batch_fast_flags": (C.c_int, [P, P]),
     "am_doc_init": (P, [P]),
@@ -128,13 +141,19 @@ _sigs = {
                                             C.POINTER(u8p), C.POINTER(C.c_size_t), P, P, C.POINTER(C.c_int),
                                             C.POINTER(Error)]),
     "am_bloom_check": (C.c_int, [C.c_char_p, C.c_uint64, C.POINTER(Error)]),
-    "am_sync_generate": (C.c_int, [C.c_size_t, P, P, P, P, P, P, P, P]),
+    "am_sync_generate": (C.c_int, [C.c_size_t, P, P, P, P, P, P, P, P, P]),
     "am_sync_receive": (C.c_int, [P, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.POINTER(u8p),
                                   C.POINTER(C.c_size_t), C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
+    "am_sync_receive_batch": (C.c_int, [C.c_size_t, P, P, P, P, P, P, P, P, P, P, P, P]),
     "am_sync_encode_message": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
     "am_sync_decode_messages": (C.c_int, [C.c_size_t, P, P, C.POINTER(C.POINTER(Span)), P, P, P]),
     "am_sync_encode_state": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
     "am_sync_decode_state": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
+    "am_doc_load_batch": (C.c_int, [P, C.c_size_t, P, P, P, P, P]),
+    "am_doc_apply_changes_batch": (C.c_int, [C.c_size_t, P, P, P, P, P, P, P, P, P]),
+    "am_doc_get_patch_batch": (C.c_int, [C.c_size_t, P, P, P, P, P, P]),
+    "am_doc_save_batch": (C.c_int, [C.c_size_t, P, P, P, P, P]),
+    "am_doc_compute_hash_graph_batch": (C.c_int, [C.c_size_t, P, P, P]),
     "am_host_alloc": (P, [C.c_size_t]),
     "am_host_free": (None, [P]),
     "am_pipe_create": (P, [P, C.POINTER(PipeCaps), C.POINTER(Error)]),
@@ -175,6 +194,20 @@ def error_for(err):
 
 def raise_for(err):
     raise error_for(err)
+
+
+def batch_errors(n, codes, msgs):
+    """Per call of a batched per-handle call (include/automerge_amd.h): None, or its AutomergeError
+    (bit 31 of the code: the reference throws a TypeError). Frees the messages."""
+    out = [None] * n
+    for i in range(n):
+        if codes[i]:
+            m = C.string_at(msgs[i]).decode("utf-8", "replace") if msgs[i] else ""
+            c = int(codes[i])
+            out[i] = AutomergeError(m, c & 0x7FFFFFFF, "TypeError" if c & 0x80000000 else "RangeError")
+        if msgs[i]:
+            lib.am_free(msgs[i])
+    return out
 
 
 _engines = {}

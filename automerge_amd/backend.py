@@ -149,6 +149,132 @@ def maxOp(backend):
     return N.lib.am_doc_max_op(_backend_state(backend).ptr)
 
 
+# ---- the same calls over many documents in one GPU batch (am_doc_*_batch, include/automerge_amd.h):
+# per document the result the single call gives, or its error in its place ----
+def _prepare(n, fn):
+    """fn(i) for every item; an item whose fn raises (an outdated handle, a bad argument) gets that
+    exception as its result. Returns (indexes that go to the engine, their values, results)."""
+    idx, vals, out = [], [], [None] * n
+    for i in range(n):
+        try:
+            v = fn(i)
+        except (RuntimeError, TypeError, ValueError, N.AutomergeError) as e:
+            out[i] = e
+            continue
+        idx.append(i)
+        vals.append(v)
+    return idx, vals, out
+
+
+def _codes(n):
+    return (C.c_uint32 * max(n, 1))(), (C.c_void_p * max(n, 1))()
+
+
+def _take_all(bufs, lens, n):
+    out = []
+    for i in range(n):
+        out.append(C.string_at(bufs[i], lens[i]) if bufs[i] else None)
+        if bufs[i]:
+            N.lib.am_free(bufs[i])
+    return out
+
+
+def loadBatch(datas, device=0):
+    """Backend.load() of many documents in one GPU batch: [BackendState or AutomergeError]."""
+    n = len(datas)
+    bufs = [bytes(d) for d in datas]
+    arr = (C.c_char_p * max(n, 1))(*bufs)
+    lens = (C.c_size_t * max(n, 1))(*[len(b) for b in bufs])
+    docs = (C.c_void_p * max(n, 1))()
+    codes, msgs = _codes(n)
+    N.lib.am_doc_load_batch(N.engine(device), n, arr, lens, docs, codes, msgs)
+    errs = N.batch_errors(n, codes, msgs)
+    out = []
+    for i in range(n):
+        if errs[i]:
+            out.append(errs[i])
+        else:
+            d = _Doc(docs[i])
+            out.append(BackendState(d, d.heads()))
+    return out
+
+
+def _apply_batch(backends, changes_lists, want_patch):
+    from . import patch as P
+    idx, states, out = _prepare(len(backends), lambda i: _backend_state(backends[i]))
+    n = len(idx)
+    ptrs = (C.c_void_p * max(n, 1))(*[s.ptr for s in states])
+    lists = [[bytes(c) for c in changes_lists[i]] for i in idx]
+    flat = [c for cl in lists for c in cl]
+    off = [0]
+    for cl in lists:
+        off.append(off[-1] + len(cl))
+    arr = (C.c_char_p * max(len(flat), 1))(*flat)
+    lens = (C.c_size_t * max(len(flat), 1))(*[len(b) for b in flat])
+    offs = (C.c_size_t * (n + 1))(*off)
+    pats, plens = ((N.u8p * max(n, 1))(), (C.c_size_t * max(n, 1))()) if want_patch else (None, None)
+    info = (N.CallInfo * max(n, 1))()
+    codes, msgs = _codes(n)
+    N.lib.am_doc_apply_changes_batch(n, ptrs, offs, arr, lens, pats, plens, info, codes, msgs)
+    errs = N.batch_errors(n, codes, msgs)
+    blobs = _take_all(pats, plens, n) if want_patch else [None] * n
+    for k, i in enumerate(idx):
+        if errs[k]:
+            out[i] = errs[k]
+            continue
+        max_op, heads, pending = info[k].take()  # as of this call (a handle may appear again later)
+        backends[i].frozen = True
+        new = BackendState(states[k], heads)
+        out[i] = (new, P.materialize(blobs[k], heads, pending, max_op)) if want_patch else new
+    return out
+
+
+def applyChangesBatch(backends, changes_lists):
+    """Backend.applyChanges() of many documents in one GPU batch: [(state, patch) or error]."""
+    return _apply_batch(backends, changes_lists, True)
+
+
+def loadChangesBatch(backends, changes_lists):
+    """Backend.loadChanges() of many documents in one GPU batch: [state or error]."""
+    return _apply_batch(backends, changes_lists, False)
+
+
+def saveBatch(backends):
+    """Backend.save() of many documents (one GPU SHA-256 launch for their checksums)."""
+    idx, states, out = _prepare(len(backends), lambda i: _backend_state(backends[i]))
+    n = len(idx)
+    ptrs = (C.c_void_p * max(n, 1))(*[s.ptr for s in states])
+    bufs, lens = (N.u8p * max(n, 1))(), (C.c_size_t * max(n, 1))()
+    codes, msgs = _codes(n)
+    N.lib.am_doc_save_batch(n, ptrs, bufs, lens, codes, msgs)
+    errs = N.batch_errors(n, codes, msgs)
+    data = _take_all(bufs, lens, n)
+    for k, i in enumerate(idx):
+        out[i] = errs[k] or data[k]
+    return out
+
+
+def getPatchBatch(backends):
+    """Backend.getPatch() of many documents in one GPU batch."""
+    from . import patch as P
+    idx, states, out = _prepare(len(backends), lambda i: _backend_state(backends[i]))
+    n = len(idx)
+    ptrs = (C.c_void_p * max(n, 1))(*[s.ptr for s in states])
+    bufs, lens = (N.u8p * max(n, 1))(), (C.c_size_t * max(n, 1))()
+    info = (N.CallInfo * max(n, 1))()
+    codes, msgs = _codes(n)
+    N.lib.am_doc_get_patch_batch(n, ptrs, bufs, lens, info, codes, msgs)
+    errs = N.batch_errors(n, codes, msgs)
+    data = _take_all(bufs, lens, n)
+    for k, i in enumerate(idx):
+        if errs[k]:
+            out[i] = errs[k]
+            continue
+        max_op, heads, pending = info[k].take()
+        out[i] = P.materialize(data[k], heads, pending, max_op)
+    return out
+
+
 def _hash_graph(s):
     # computeHashGraph (new.js:1879-1904) for a loaded document, once
     err = N.Error()
@@ -474,30 +600,36 @@ def generateSyncMessages(backends, sync_states):
     """generateSyncMessage for many documents in one call (am_sync_generate): their Bloom filters
     are built in one k_bloom_build launch and their change selections run in one k_sync_select
     launch. Returns [(state, message or None) or AutomergeError]."""
-    n = len(backends)
-    ptrs = (C.c_void_p * max(n, 1))(*[_backend_state(b).ptr for b in backends])
-    packed = [_pack_state(s) for s in sync_states]
+    def prep(i):
+        if not backends[i]:
+            raise N.AutomergeError("generateSyncMessage called with no Automerge document", kind="Error")
+        if not sync_states[i]:
+            raise N.AutomergeError("generateSyncMessage requires a syncState, which can be created with "
+                                   "initSyncState()", kind="Error")
+        return _backend_state(backends[i]), _pack_state(sync_states[i])
+    idx, vals, res = _prepare(len(backends), prep)
+    n = len(idx)
+    ptrs = (C.c_void_p * max(n, 1))(*[v[0].ptr for v in vals])
+    packed = [v[1] for v in vals]
     st = (C.c_char_p * max(n, 1))(*packed)
     sl = (C.c_size_t * max(n, 1))(*[len(p) for p in packed])
     ost, osl = (N.u8p * max(n, 1))(), (C.c_size_t * max(n, 1))()
     msg, ml = (N.u8p * max(n, 1))(), (C.c_size_t * max(n, 1))()
-    errs = (N.Error * max(n, 1))()
-    N.lib.am_sync_generate(n, ptrs, st, sl, ost, osl, msg, ml, errs)
-    out = []
-    for i in range(n):
-        if errs[i].code:
-            e = errs[i]
-            out.append(N.AutomergeError(e.message.decode("utf-8", "replace"), e.code,
-                                        "TypeError" if e.is_type_error else "RangeError"))
+    codes, msgs = _codes(n)
+    N.lib.am_sync_generate(n, ptrs, st, sl, ost, osl, msg, ml, codes, msgs)
+    errs = N.batch_errors(n, codes, msgs)
+    for k, i in enumerate(idx):
+        if errs[k]:
+            res[i] = errs[k]
             continue
-        blob = N.take(ost[i], osl[i])
-        m = N.take(msg[i], ml[i]) if msg[i] else None
-        if m is None or blob == packed[i]:
-            out.append((sync_states[i], m))
+        blob = N.take(ost[k], osl[k])
+        m = N.take(msg[k], ml[k]) if msg[k] else None
+        if m is None or blob == packed[k]:
+            res[i] = (sync_states[i], m)
         else:
             nxt = _unpack_state(blob)
-            out.append((dict(sync_states[i], lastSentHeads=nxt["lastSentHeads"], sentHashes=nxt["sentHashes"]), m))
-    return out
+            res[i] = (dict(sync_states[i], lastSentHeads=nxt["lastSentHeads"], sentHashes=nxt["sentHashes"]), m)
+    return res
 
 
 def generateSyncMessage(backend, sync_state):
@@ -541,3 +673,60 @@ def receiveSyncMessage(backend, old_sync_state, message):
     sent = st["sentHashes"] if isinstance(st["sentHashes"], list) else old_sync_state.get("sentHashes")
     return backend, {"sharedHeads": st["sharedHeads"], "lastSentHeads": st["lastSentHeads"], "theirHave": msg["have"],
                      "theirHeads": msg["heads"], "theirNeed": msg["need"], "sentHashes": sent}, patch
+
+
+def receiveSyncMessages(backends, old_sync_states, messages):
+    """receiveSyncMessage for many documents in one call (am_sync_receive_batch): every message's
+    changes go through ONE batched applyChanges. Returns [(backend, syncState, patch or None) or
+    AutomergeError], each as receiveSyncMessage returns it."""
+    from . import patch as P
+    n = len(backends)
+    decoded = [None] * n
+
+    def prep(i):
+        if not backends[i]:
+            raise N.AutomergeError("generateSyncMessage called with no Automerge document", kind="Error")
+        if not old_sync_states[i]:
+            raise N.AutomergeError("generateSyncMessage requires a syncState, which can be created with "
+                                   "initSyncState()", kind="Error")
+        msg = decoded[i] = decodeSyncMessage(messages[i])
+        s = _backend_state(backends[i]) if (msg["changes"] or msg["heads"]) else backends[i].state
+        return s, _pack_state(old_sync_states[i]), bytes(messages[i])
+    idx, vals, out = _prepare(n, prep)
+    ptrs = [v[0] for v in vals]
+    blobs = [v[1] for v in vals]
+    mbufs = [v[2] for v in vals]
+    m = len(idx)
+    hp = (C.c_void_p * max(m, 1))(*[s.ptr for s in ptrs])
+    sb = (C.c_char_p * max(m, 1))(*blobs)
+    sl = (C.c_size_t * max(m, 1))(*[len(b) for b in blobs])
+    mb = (C.c_char_p * max(m, 1))(*mbufs)
+    mlen = (C.c_size_t * max(m, 1))(*[len(b) for b in mbufs])
+    ost, osl = (N.u8p * max(m, 1))(), (C.c_size_t * max(m, 1))()
+    pa, pl = (N.u8p * max(m, 1))(), (C.c_size_t * max(m, 1))()
+    info = (N.CallInfo * max(m, 1))()
+    codes, msgs = _codes(m)
+    N.lib.am_sync_receive_batch(m, hp, sb, sl, mb, mlen, ost, osl, pa, pl, info, codes, msgs)
+    errs = N.batch_errors(m, codes, msgs)
+    states = _take_all(ost, osl, m)
+    logs = _take_all(pa, pl, m)
+    for k, i in enumerate(idx):
+        msg, backend, s = decoded[i], backends[i], ptrs[k]
+        if errs[k]:
+            if errs[k].code & 0x40000000:  # the changes were applied before the error
+                backend.frozen = True
+            errs[k].code &= 0x3FFFFFFF
+            out[i] = errs[k]
+            continue
+        st = _unpack_state(states[k])
+        patch = None
+        if msg["changes"]:
+            max_op, heads, pending = info[k].take()
+            backend.frozen = True
+            backend = BackendState(s, heads)
+            patch = P.materialize(logs[k], heads, pending, max_op)
+        sent = st["sentHashes"] if isinstance(st["sentHashes"], list) else old_sync_states[i].get("sentHashes")
+        out[i] = (backend, {"sharedHeads": st["sharedHeads"], "lastSentHeads": st["lastSentHeads"],
+                            "theirHave": msg["have"], "theirHeads": msg["heads"], "theirNeed": msg["need"],
+                            "sentHashes": sent}, patch)
+    return out

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "am_graph.h"
@@ -271,12 +272,19 @@ std::vector<uint8_t> make_chunk(const uint8_t checksum[4], uint8_t type, const s
 // =============================================================================================
 // engine / batch
 // =============================================================================================
+// device arenas the batched per-handle calls compact their outputs into (k_pipe_compact)
+struct CollectBufs {
+  DevBuf<uint64_t> olen, ooff, plen, poff, tmp, totals;
+  DevBuf<am_doc_summary> summ;
+  DevBuf<uint8_t> out, pat;
+};
 struct am_engine {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev[5] = {};
   am_batch* scratch = nullptr;  // batch reused by the per-document API
   void* hist = nullptr;         // device buffers of the history batches (am_hist.hip)
+  CollectBufs* coll = nullptr;  // the batched per-handle calls
 };
 
 struct am_batch {
@@ -355,6 +363,7 @@ extern "C" void am_engine_destroy(am_engine* eng) {
   set_device(eng);
   am_batch_destroy(eng->scratch);
   am_hist_cache_free(eng->hist);
+  delete eng->coll;
   for (auto& ev : eng->ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(eng->stream);
   delete eng;
@@ -694,6 +703,23 @@ extern "C" int am_batch_kernel_info(am_batch* b, uint64_t* out3) {
   out3[0] = b->lds_bytes;
   out3[1] = b->fast_lds;
   out3[2] = b->max_hot_v;
+  return 0;
+}
+
+// workspace plan of document `doc` of the staged batch (diagnostics): [0] R, [1] E, [2] P,
+// [3] hot working set, [4] workspace bytes, [5] its offset, [6] span_lo, [7] span_hi,
+// [8] 1 when the document runs from LDS (k_doc lds_mode), [9] input bytes B
+extern "C" int am_batch_doc_plan(am_batch* b, uint32_t doc, uint64_t* out10) {
+  if (!set_device(b->eng) || doc >= b->ndocs) return 1;
+  DocBounds db;
+  uint64_t off = 0;
+  if (hipMemcpy(&db, b->bounds.p + doc, sizeof db, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(&off, b->ws_off.p + doc, sizeof off, hipMemcpyDeviceToHost) != hipSuccess)
+    return 1;
+  const WsLayout L = ws_layout(db);
+  out10[0] = db.R; out10[1] = db.E; out10[2] = db.P; out10[3] = L.hot_total; out10[4] = L.total; out10[5] = off;
+  out10[6] = db.span_lo; out10[7] = db.span_hi; out10[8] = (L.hot_total <= b->lds_bytes && !(db.span_hi == db.span_lo && db.B > 0)) ? 1 : 0;
+  out10[9] = db.B;
   return 0;
 }
 
@@ -1063,6 +1089,21 @@ struct OneResult {
   std::vector<uint8_t> meta;   // AM_DOC_META: the objectMeta blob the call leaves
 };
 
+// The objectMeta blob after a patch log's stream (AM_DOC_META) goes to res.meta; the log keeps
+// header + stream.
+void split_meta(OneResult& res) {
+  res.meta.clear();
+  if (res.patch.size() < sizeof(PatchHdr2)) return;
+  PatchHdr2 h;
+  std::memcpy(&h, res.patch.data(), sizeof h);
+  if (h.meta_bytes && sizeof h + h.nbytes + h.meta_bytes == res.patch.size()) {
+    res.meta.assign(res.patch.begin() + sizeof h + h.nbytes, res.patch.end());
+    res.patch.resize(sizeof h + h.nbytes);
+    h.meta_bytes = 0;
+    std::memcpy(res.patch.data(), &h, sizeof h);
+  }
+}
+
 // Runs one document (optional base chunk + change list) through the GPU pipeline.
 // With `meta` (patch_mode 2): the handle's objectMeta snapshots go in (empty: documentPatch's) and
 // res.meta receives what the call leaves.
@@ -1148,18 +1189,162 @@ bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified,
       err = {AM_U_CAPACITY, false, "automerge_amd: patch copy failed"};
       return false;
     }
-    // the objectMeta blob after the stream goes to res.meta; the log keeps header + stream
-    res.meta.clear();
-    if (res.patch.size() >= sizeof(PatchHdr2)) {
-      PatchHdr2 h;
-      std::memcpy(&h, res.patch.data(), sizeof h);
-      if (h.meta_bytes && sizeof h + h.nbytes + h.meta_bytes == res.patch.size()) {
-        res.meta.assign(res.patch.begin() + sizeof h + h.nbytes, res.patch.end());
-        res.patch.resize(sizeof h + h.nbytes);
-        h.meta_bytes = 0;
-        std::memcpy(res.patch.data(), &h, sizeof h);
+    split_meta(res);
+  }
+  return true;
+}
+
+// heads of a document chunk (decodeDocumentHeader: actors, then the sorted heads)
+bool chunk_heads(const std::vector<uint8_t>& chunk, std::vector<std::array<uint8_t, 32>>& heads) {
+  Container c;
+  if (!read_container(chunk.data(), chunk.size(), c)) return false;
+  HRd r{chunk.data() + c.data_off, c.data_len, 0};
+  const uint64_t na = r.u();
+  for (uint64_t i = 0; i < na && r.ok; i++) r.raw(r.u());
+  const uint64_t nh = r.u();
+  const uint8_t* h = r.raw(32 * nh);
+  if (!r.ok) return false;
+  heads.resize(nh);
+  for (uint64_t i = 0; i < nh; i++) std::memcpy(heads[i].data(), h + 32 * i, 32);
+  return true;
+}
+
+// Every document's merged chunk and patch log of the last run of batch b, densely in two host
+// arenas (k_pipe_lens / k_pipe_compact: a sizing pass, then the copies; one D2H each).
+bool batch_collect(am_batch* b, std::vector<am_doc_summary>& summ, std::vector<uint8_t>& out, std::vector<uint8_t>& pat) {
+  am_engine* e = b->eng;
+  if (!e->coll) e->coll = new CollectBufs();
+  CollectBufs& c = *e->coll;
+  const uint32_t nd = b->ndocs;
+  if (!c.olen.ensure(nd) || !c.ooff.ensure(nd) || !c.plen.ensure(nd) || !c.poff.ensure(nd) ||
+      !c.tmp.ensure(am_scan_tmp_elems(nd)) || !c.totals.ensure(2) || !c.summ.ensure(nd))
+    return false;
+  hipStream_t s = e->stream;
+  BatchDev d = b->dev();
+  uint64_t tot[2] = {0, 0};
+  am_launch_pipe_compact(d, c.olen.p, c.ooff.p, c.plen.p, c.poff.p, c.tmp.p, c.totals.p, nullptr, 0, nullptr, 0, c.summ.p, s);
+  if (hipMemcpyAsync(tot, c.totals.p, sizeof tot, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return false;
+  if (!c.out.ensure(tot[0] + 16) || !c.pat.ensure(tot[1] + 16)) return false;
+  am_launch_pipe_compact(d, c.olen.p, c.ooff.p, c.plen.p, c.poff.p, c.tmp.p, c.totals.p, c.out.p, tot[0], c.pat.p, tot[1],
+                         c.summ.p, s);
+  summ.resize(nd);
+  out.resize(tot[0]);
+  pat.resize(tot[1]);
+  if (nd && hipMemcpyAsync(summ.data(), c.summ.p, sizeof(am_doc_summary) * nd, hipMemcpyDeviceToHost, s) != hipSuccess) return false;
+  if (tot[0] && hipMemcpyAsync(out.data(), c.out.p, tot[0], hipMemcpyDeviceToHost, s) != hipSuccess) return false;
+  if (tot[1] && hipMemcpyAsync(pat.data(), c.pat.p, tot[1], hipMemcpyDeviceToHost, s) != hipSuccess) return false;
+  return hipStreamSynchronize(s) == hipSuccess && hipGetLastError() == hipSuccess;
+}
+
+// One GPU batch for many documents (the batched per-handle calls): per document its base chunk
+// and changes (adjacent in the arena), its known hashes and its objectMeta blob; per document the
+// result run_one gives, or the error the document raised.
+struct ManyJob {
+  const std::vector<uint8_t>* base = nullptr;
+  bool base_verified = false;
+  const std::vector<std::vector<uint8_t>>* chg = nullptr;
+  const std::vector<am_known_hash>* known = nullptr;
+  bool have_graph = false;
+  int patch_mode = 0;
+  const std::vector<uint8_t>* meta = nullptr;  // patch_mode 2: the handle's objectMeta blob
+};
+struct ManyOut {
+  OneResult res;
+  Err err;
+  bool ok = false;
+};
+bool run_many(am_engine* e, const std::vector<ManyJob>& jobs, std::vector<ManyOut>& outs, Err& err) {
+  const size_t n = jobs.size();
+  outs.assign(n, ManyOut());
+  if (!n) return true;
+  std::vector<uint8_t> arena;
+  std::vector<am_chunk_desc> cds;
+  std::vector<am_doc_desc> dds(n);
+  std::vector<am_known_hash> known;
+  std::vector<uint32_t> c0(n), cn(n);
+  for (size_t i = 0; i < n; i++) {
+    const ManyJob& j = jobs[i];
+    am_doc_desc dd{};
+    dd.base_chunk = -1;
+    c0[i] = (uint32_t)cds.size();
+    if (j.base && !j.base->empty()) {
+      dd.base_chunk = (int64_t)cds.size();
+      cds.push_back({arena.size(), (uint32_t)j.base->size(), j.base_verified ? 1u : 0u});
+      arena.insert(arena.end(), j.base->begin(), j.base->end());
+    }
+    dd.chg_begin = (uint32_t)cds.size();
+    dd.chg_count = j.chg ? (uint32_t)j.chg->size() : 0u;
+    if (j.chg)
+      for (auto& c : *j.chg) {
+        cds.push_back({arena.size(), (uint32_t)c.size(), 0});
+        arena.insert(arena.end(), c.begin(), c.end());
+      }
+    cn[i] = (uint32_t)cds.size() - c0[i];
+    dd.known_begin = (uint32_t)known.size();
+    dd.known_count = j.known ? (uint32_t)j.known->size() : 0u;
+    if (j.known) known.insert(known.end(), j.known->begin(), j.known->end());
+    dd.flags = (j.have_graph ? 1u : 0u) | (j.patch_mode == 1 ? AM_DOC_WANT_PATCH : 0u) | (j.patch_mode == 2 ? AM_DOC_WANT_DIFF : 0u);
+    dd.meta_chunk = 0;
+    dds[i] = dd;
+  }
+  for (size_t i = 0; i < n; i++)  // objectMeta blobs after every document's chunks
+    if (jobs[i].meta && jobs[i].patch_mode == 2) {
+      dds[i].flags |= AM_DOC_META;
+      if (!jobs[i].meta->empty()) {
+        dds[i].meta_chunk = (uint32_t)cds.size() + 1;
+        cds.push_back({arena.size(), (uint32_t)jobs[i].meta->size(), AM_CHUNK_RAW});
+        arena.insert(arena.end(), jobs[i].meta->begin(), jobs[i].meta->end());
       }
     }
+  am_batch* b = scratch_batch(e);
+  am_error ce;
+  if (am_batch_stage(b, arena.data(), arena.size(), cds.data(), (uint32_t)cds.size(), dds.data(), (uint32_t)n, known.data(),
+                     (uint32_t)known.size(), &ce) ||
+      am_batch_run(b) || am_batch_sync(b, &ce)) {
+    err = {AM_U_CAPACITY, false, std::string("automerge_amd: GPU pipeline failed: ") + ce.message};
+    return false;
+  }
+  std::vector<am_doc_result> rr(n);
+  std::vector<uint8_t> hs(32 * cds.size());
+  std::vector<int32_t> cst(cds.size());
+  std::vector<uint32_t> st(cds.size());
+  std::vector<am_doc_summary> summ;
+  std::vector<uint8_t> out, pat;
+  if (am_batch_results(b, rr.data()) || (!cds.empty() && am_batch_chunk_results(b, hs.data(), cst.data(), st.data())) ||
+      !batch_collect(b, summ, out, pat)) {
+    err = {AM_U_CAPACITY, false, "automerge_amd: result copy failed"};
+    return false;
+  }
+  for (size_t i = 0; i < n; i++) {
+    ManyOut& o = outs[i];
+    OneResult& res = o.res;
+    res.r = rr[i];
+    res.chg_state.assign(cst.begin() + c0[i], cst.begin() + c0[i] + cn[i]);
+    res.hashes.resize(cn[i]);
+    for (uint32_t k = 0; k < cn[i]; k++) std::memcpy(res.hashes[k].data(), hs.data() + 32ull * (c0[i] + k), 32);
+    if (rr[i].status) {
+      std::string actor;
+      if (rr[i].arg_actor_len && rr[i].arg_actor_off + rr[i].arg_actor_len <= arena.size())
+        actor = hexs(arena.data() + rr[i].arg_actor_off, rr[i].arg_actor_len);
+      o.err = {rr[i].status, false, message_for(rr[i].status, rr[i].arg0, rr[i].arg1, actor)};
+      continue;
+    }
+    const am_doc_summary& sm = summ[i];
+    if (sm.status || sm.out_len != rr[i].out_len) {
+      o.err = {AM_U_CAPACITY, false, "automerge_amd: output compaction failed"};
+      continue;
+    }
+    res.out.assign(out.begin() + sm.out_off, out.begin() + sm.out_off + sm.out_len);
+    if (!chunk_heads(res.out, res.heads)) {
+      o.err = {AM_U_VALUE, false, "automerge_amd: corrupt merged document"};
+      continue;
+    }
+    if (jobs[i].patch_mode) {
+      res.patch.assign(pat.begin() + sm.patch_off, pat.begin() + sm.patch_off + sm.patch_len);
+      split_meta(res);
+    }
+    o.ok = true;
   }
   return true;
 }
@@ -1335,6 +1520,9 @@ static bool patch_log_error(const std::vector<uint8_t>& log, Err& e) {
 
 extern "C" int am_doc_compute_hash_graph(am_doc* d, am_error* err);
 
+static int apply_finish(am_doc* d, std::vector<std::vector<uint8_t>>& orig, bool track, OneResult& res,
+                        std::vector<uint8_t>* patch, am_error* err);
+
 static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* lens, size_t n, std::vector<uint8_t>* patch,
                   am_error* err) {
   Err e;
@@ -1395,9 +1583,15 @@ static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* le
       return 1;
     }
   }
-  // the patch is part of the call: an error in it throws before the document changes (new.js:1838);
-  // loadChanges throws the reference's errors too, and only loses objectMeta on an input the patch
-  // replay does not restate (AM_U_*)
+  return apply_finish(d, orig, track, res, patch, err);
+}
+
+// The end of an applyChanges call whose GPU run succeeded: the patch's errors (an error in it throws
+// before the document changes, new.js:1838; loadChanges throws the reference's errors too, and only
+// loses objectMeta on an input the patch replay does not restate, AM_U_*), then the commit
+// (new.js:1838-1860).
+static int apply_finish(am_doc* d, std::vector<std::vector<uint8_t>>& orig, bool track, OneResult& res,
+                        std::vector<uint8_t>* patch, am_error* err) {
   bool lost = false;
   if (track) {
     Err pe;
@@ -1462,7 +1656,10 @@ extern "C" int am_doc_apply_changes_patch(am_doc* d, const uint8_t* const* bufs,
 // save() bytes of a merged document chunk as k_doc writes it (columns uncompressed): DEFLATE of
 // columns >= 256 bytes (deflateColumn, columnar.js:1052-1059, DEFLATE_MIN_SIZE :32) is the host
 // stage; the container checksum of the compressed form is computed on the GPU.
-static bool save_bytes(am_engine* eng, const std::vector<uint8_t>& state, std::vector<uint8_t>& bytes, Err& err) {
+// save_prepare: the bytes with the checksum still to fill in when *need_hash (the SHA-256 runs on
+// the GPU, one launch for every document of a batched save).
+static bool save_prepare(const std::vector<uint8_t>& state, std::vector<uint8_t>& bytes, bool& need_hash, Err& err) {
+  need_hash = false;
   Container c;
   DocParts parts;
   if (!read_container(state.data(), state.size(), c) || !split_doc(state.data() + c.data_off, c.data_len, parts)) {
@@ -1483,6 +1680,14 @@ static bool save_bytes(am_engine* eng, const std::vector<uint8_t>& state, std::v
   std::vector<uint8_t> body = join_doc(parts);
   uint8_t zero[4] = {0, 0, 0, 0};
   bytes = make_chunk(zero, 0, body);
+  need_hash = true;
+  return true;
+}
+
+static bool save_bytes(am_engine* eng, const std::vector<uint8_t>& state, std::vector<uint8_t>& bytes, Err& err) {
+  bool need = false;
+  if (!save_prepare(state, bytes, need, err)) return false;
+  if (!need) return true;
   std::vector<std::array<uint8_t, 32>> h;
   if (!gpu_sha256(eng, {&bytes}, 8, h)) { err = {AM_U_CAPACITY, false, "automerge_amd: GPU hash failed"}; return false; }
   std::memcpy(bytes.data() + 4, h[0].data(), 4);
@@ -1605,6 +1810,366 @@ extern "C" int am_doc_get_patch(am_doc* d, uint8_t** out, size_t* len, am_error*
   std::memcpy(*out, log.data(), log.size());
   *len = log.size();
   return 0;
+}
+
+// ---- the per-handle calls over many handles in one GPU batch ----
+// Per call: codes[i] (0 = ok; bit 31 set when the reference throws a TypeError) and, when msgs is
+// given, msgs[i] = the error text (malloc'd, am_free; nullptr for a call that succeeded).
+static uint8_t* dup_bytes(const std::vector<uint8_t>& v) {
+  uint8_t* p = static_cast<uint8_t*>(std::malloc(v.size() ? v.size() : 1));
+  if (p && !v.empty()) std::memcpy(p, v.data(), v.size());
+  return p;
+}
+static void call_info(const am_doc* d, am_call_info* info) {
+  if (!info) return;
+  info->max_op = d->max_op;
+  info->pending = (uint32_t)d->queue.size();
+  info->nheads = (uint32_t)d->heads.size();
+  info->heads = static_cast<uint8_t*>(std::malloc(32 * (d->heads.size() ? d->heads.size() : 1)));
+  if (info->heads)
+    for (size_t k = 0; k < d->heads.size(); k++) std::memcpy(info->heads + 32 * k, d->heads[k].data(), 32);
+}
+static Err from_c(const am_error& e) { return Err{e.code, e.is_type_error != 0, e.message}; }
+static int publish(const std::vector<Err>& E, uint32_t* codes, char** msgs) {
+  int bad = 0;
+  for (size_t i = 0; i < E.size(); i++) {
+    codes[i] = E[i].code | (E[i].code && E[i].type_error ? 0x80000000u : 0u);
+    if (msgs) {
+      msgs[i] = nullptr;
+      if (E[i].code) {
+        msgs[i] = static_cast<char*>(std::malloc(E[i].msg.size() + 1));
+        if (msgs[i]) std::memcpy(msgs[i], E[i].msg.c_str(), E[i].msg.size() + 1);
+      }
+    }
+    bad += E[i].code != 0;
+  }
+  return bad;
+}
+
+// computeHashGraph (new.js:1879-1904) of the given loaded handles, k_history batches of 4096
+static void hash_graphs(const std::vector<am_doc*>& ds, std::vector<Err>& E) {
+  E.assign(ds.size(), Err{});
+  const size_t G = 4096;  // am_history carries an am_error per document: bounded host memory
+  for (size_t g0 = 0; g0 < ds.size(); g0 += G) {
+    const size_t g1 = std::min(ds.size(), g0 + G);
+    std::vector<const uint8_t*> ptr;
+    std::vector<size_t> len;
+    for (size_t k = g0; k < g1; k++) { ptr.push_back(ds[k]->state.data()); len.push_back(ds[k]->state.size()); }
+    std::vector<am_history> h(g1 - g0);
+    am_document_changes_batch(ds[g0]->eng, ptr.data(), len.data(), g1 - g0, h.data());
+    for (size_t k = g0; k < g1; k++) {
+      am_doc* d = ds[k];
+      am_history& x = h[k - g0];
+      if (x.err.code) {
+        E[k] = from_c(x.err);
+      } else {
+        d->changes.clear();
+        d->hashes.clear();
+        d->graph.clear();
+        for (size_t i = 0; i < x.nchanges; i++) {
+          d->changes.emplace_back(x.changes + x.offs[i], x.changes + x.offs[i + 1]);
+          std::array<uint8_t, 32> hh;
+          std::memcpy(hh.data(), x.hashes32 + 32 * i, 32);
+          d->hashes.push_back(hh);
+        }
+        d->have_hash_graph = true;
+      }
+      std::free(x.changes);
+      std::free(x.offs);
+      std::free(x.hashes32);
+    }
+  }
+}
+
+// computeHashGraph of n handles (all of one engine): one k_history batch per 4096
+extern "C" int am_doc_compute_hash_graph_batch(size_t n, am_doc* const* docs, uint32_t* codes, char** msgs) {
+  std::vector<Err> E(n);
+  std::vector<am_doc*> need;
+  std::vector<size_t> at;
+  std::unordered_set<am_doc*> seen;
+  for (size_t i = 0; i < n; i++)
+    if (!docs[i]->have_hash_graph && seen.insert(docs[i]).second) {
+      if (docs[i]->eng != docs[0]->eng) {
+        am_error tmp;
+        if (am_doc_compute_hash_graph(docs[i], &tmp)) E[i] = from_c(tmp);
+        continue;
+      }
+      need.push_back(docs[i]);
+      at.push_back(i);
+    }
+  std::vector<Err> ge;
+  hash_graphs(need, ge);
+  for (size_t k = 0; k < at.size(); k++) E[at[k]] = ge[k];
+  return publish(E, codes, msgs);
+}
+
+// Backend.load of n documents (backend.js:104-107) in one GPU batch: docs[i] = the handle, or
+// nullptr with codes[i] / msgs[i] set. Returns the number that failed.
+extern "C" int am_doc_load_batch(am_engine* eng, size_t n, const uint8_t* const* data, const size_t* lens, am_doc** docs,
+                                 uint32_t* codes, char** msgs) {
+  std::vector<Err> E(n);
+  std::vector<std::vector<uint8_t>> staged(n);
+  std::vector<ManyJob> jobs;
+  std::vector<size_t> at;
+  for (size_t i = 0; i < n; i++) {
+    docs[i] = nullptr;
+    bool v = false;
+    if (!stage_doc(eng, std::vector<uint8_t>(data[i], data[i] + lens[i]), staged[i], v, E[i])) continue;
+    ManyJob j;
+    j.base = &staged[i];
+    j.base_verified = v;
+    jobs.push_back(j);
+    at.push_back(i);
+  }
+  std::vector<ManyOut> outs;
+  Err e;
+  if (!run_many(eng, jobs, outs, e)) {
+    for (size_t i : at) E[i] = e;
+    at.clear();
+  }
+  for (size_t k = 0; k < at.size(); k++) {
+    const size_t i = at[k];
+    if (!outs[k].ok) {
+      if (outs[k].err.code == AM_U_UTF8) {  // room for the U+FFFD replacements: the single path
+        am_error tmp;
+        docs[i] = am_doc_load(eng, data[i], lens[i], &tmp);
+        if (!docs[i]) E[i] = from_c(tmp);
+      } else {
+        E[i] = outs[k].err;
+      }
+      continue;
+    }
+    OneResult& res = outs[k].res;
+    am_doc* d = new am_doc();
+    d->eng = eng;
+    d->state = std::move(res.out);
+    d->binary.assign(data[i], data[i] + lens[i]);
+    d->has_binary = true;
+    d->have_hash_graph = false;
+    d->heads = res.heads;
+    d->load_heads = res.heads;
+    d->nchanges = res.r.nchanges;
+    d->max_op = res.r.max_op;
+    docs[i] = d;
+  }
+  return publish(E, codes, msgs);
+}
+
+// Backend.applyChanges / loadChanges (backend.js:27-32, 115-120) of n handles in one GPU batch:
+// handle i gets the changes bufs[off[i] .. off[i+1]). patches != nullptr: applyChanges, patches[i]
+// (malloc'd) / patch_lens[i] as am_doc_apply_changes_patch; otherwise loadChanges. A handle that
+// appears more than once takes its later calls after the batch, in order; the handles whose call
+// needs the hash graph (loaded documents, new.js:1826-1832) have it computed in one batch and run
+// again. Returns the number of calls that failed (the handle unchanged).
+extern "C" int am_doc_apply_changes_batch(size_t n, am_doc* const* docs, const size_t* off, const uint8_t* const* bufs,
+                                          const size_t* lens, uint8_t** patches, size_t* patch_lens, am_call_info* info,
+                                          uint32_t* codes, char** msgs) {
+  struct Call {
+    size_t i;
+    std::vector<std::vector<uint8_t>> orig;
+    bool track;
+    std::vector<am_known_hash> known;
+  };
+  std::vector<Err> E(n);
+  std::vector<Call> calls;
+  std::vector<size_t> single;  // calls taken one at a time after the batch, in call order
+  std::unordered_set<am_doc*> seen;
+  am_engine* eng = n ? docs[0]->eng : nullptr;
+  auto known_of = [](am_doc* d, std::vector<am_known_hash>& known) {
+    known.clear();
+    if (!d->have_hash_graph) return;
+    known.resize(d->hashes.size());
+    for (size_t k = 0; k < d->hashes.size(); k++) {
+      std::memcpy(known[k].hash, d->hashes[k].data(), 32);
+      known[k].index = (int64_t)k;
+    }
+  };
+  for (size_t i = 0; i < n; i++) {
+    if (patches) { patches[i] = nullptr; patch_lens[i] = 0; }
+    if (info) info[i] = am_call_info{0, 0, 0, nullptr};
+    am_doc* d = docs[i];
+    const bool first = seen.insert(d).second;
+    if (d->eng != eng || !first || (patches && d->meta_lost)) { single.push_back(i); continue; }
+    Call c;
+    c.i = i;
+    for (size_t k = off[i]; k < off[i + 1]; k++) c.orig.emplace_back(bufs[k], bufs[k] + lens[k]);
+    for (auto& q : d->queue) c.orig.push_back(q);
+    c.track = !d->meta_lost;
+    known_of(d, c.known);
+    calls.push_back(std::move(c));
+  }
+  for (int round = 0; round < 2 && !calls.empty(); round++) {
+    std::vector<ManyJob> jobs(calls.size());
+    for (size_t k = 0; k < calls.size(); k++) {
+      am_doc* d = docs[calls[k].i];
+      ManyJob& j = jobs[k];
+      j.base = d->state.empty() ? nullptr : &d->state;
+      j.chg = &calls[k].orig;
+      j.known = &calls[k].known;
+      j.have_graph = d->have_hash_graph;
+      j.patch_mode = calls[k].track ? 2 : 0;
+      j.meta = calls[k].track ? &d->meta : nullptr;
+    }
+    std::vector<ManyOut> outs;
+    Err e;
+    if (!run_many(eng, jobs, outs, e)) {
+      for (auto& c : calls) E[c.i] = e;
+      calls.clear();
+      break;
+    }
+    std::vector<Call> graph;
+    for (size_t k = 0; k < calls.size(); k++) {
+      Call& c = calls[k];
+      am_doc* d = docs[c.i];
+      ManyOut& o = outs[k];
+      if (!o.ok) {
+        if (o.err.code == AM_U_HASH_GRAPH && !d->have_hash_graph) graph.push_back(std::move(c));
+        else if (o.err.code == AM_U_UTF8) single.push_back(c.i);
+        else E[c.i] = o.err;
+        continue;
+      }
+      if (c.track && o.res.patch.size() >= sizeof(PatchHdr2)) {
+        PatchHdr2 ph;
+        std::memcpy(&ph, o.res.patch.data(), sizeof ph);
+        if (ph.status == AM_U_CAPACITY) { single.push_back(c.i); continue; }  // 8x pools: the single path
+      }
+      std::vector<uint8_t> log;
+      am_error tmp;
+      if (apply_finish(d, c.orig, c.track, o.res, patches ? &log : nullptr, &tmp)) {
+        E[c.i] = from_c(tmp);
+        continue;
+      }
+      if (patches) {
+        patches[c.i] = dup_bytes(log);
+        patch_lens[c.i] = log.size();
+      }
+      call_info(d, info ? info + c.i : nullptr);
+    }
+    calls.clear();
+    if (!graph.empty()) {
+      std::vector<am_doc*> gd;
+      for (auto& c : graph) gd.push_back(docs[c.i]);
+      std::vector<Err> ge;
+      hash_graphs(gd, ge);
+      for (size_t k = 0; k < graph.size(); k++) {
+        if (ge[k].code) { E[graph[k].i] = ge[k]; continue; }
+        known_of(docs[graph[k].i], graph[k].known);
+        calls.push_back(std::move(graph[k]));
+      }
+    }
+  }
+  for (auto& c : calls) single.push_back(c.i);
+  std::sort(single.begin(), single.end());
+  for (size_t i : single) {
+    std::vector<uint8_t> log;
+    am_error tmp;
+    std::vector<const uint8_t*> b(bufs + off[i], bufs + off[i + 1]);
+    std::vector<size_t> l(lens + off[i], lens + off[i + 1]);
+    if (apply_changes(docs[i], b.data(), l.data(), b.size(), patches ? &log : nullptr, &tmp)) {
+      E[i] = from_c(tmp);
+      continue;
+    }
+    if (patches) {
+      patches[i] = dup_bytes(log);
+      patch_lens[i] = log.size();
+    }
+    call_info(docs[i], info ? info + i : nullptr);
+  }
+  return publish(E, codes, msgs);
+}
+
+// Backend.getPatch (backend.js:125-127) of n handles in one GPU batch; out[i] malloc'd.
+extern "C" int am_doc_get_patch_batch(size_t n, am_doc* const* docs, uint8_t** out, size_t* lens, am_call_info* info,
+                                      uint32_t* codes, char** msgs) {
+  std::vector<Err> E(n);
+  std::vector<ManyJob> jobs;
+  std::vector<size_t> at, single;
+  am_engine* eng = n ? docs[0]->eng : nullptr;
+  for (size_t i = 0; i < n; i++) {
+    out[i] = nullptr;
+    lens[i] = 0;
+    if (docs[i]->state.empty() || docs[i]->eng != eng) { single.push_back(i); continue; }
+    ManyJob j;
+    j.base = &docs[i]->state;
+    j.have_graph = docs[i]->have_hash_graph;
+    j.patch_mode = 1;
+    jobs.push_back(j);
+    at.push_back(i);
+  }
+  std::vector<ManyOut> outs;
+  Err e;
+  if (!run_many(eng, jobs, outs, e)) {
+    for (size_t i : at) E[i] = e;
+    at.clear();
+  }
+  for (size_t k = 0; k < at.size(); k++) {
+    const size_t i = at[k];
+    if (!outs[k].ok) {
+      if (outs[k].err.code == AM_U_UTF8) single.push_back(i);
+      else E[i] = outs[k].err;
+      continue;
+    }
+    if (patch_log_error(outs[k].res.patch, E[i])) continue;  // getPatch's RangeError (new.js:944)
+    out[i] = dup_bytes(outs[k].res.patch);
+    lens[i] = outs[k].res.patch.size();
+  }
+  for (size_t i : single) {
+    am_error tmp;
+    if (am_doc_get_patch(docs[i], out + i, lens + i, &tmp)) E[i] = from_c(tmp);
+  }
+  for (size_t i = 0; i < n && info; i++) {
+    info[i] = am_call_info{0, 0, 0, nullptr};
+    if (!E[i].code) call_info(docs[i], info + i);
+  }
+  return publish(E, codes, msgs);
+}
+
+// Backend.save (new.js:2025-2047) of n handles: the DEFLATE stage on the host, every checksum in one
+// GPU SHA-256 launch; out[i] malloc'd.
+extern "C" int am_doc_save_batch(size_t n, am_doc* const* docs, uint8_t** out, size_t* lens, uint32_t* codes, char** msgs) {
+  std::vector<Err> E(n);
+  std::vector<std::vector<uint8_t>> bytes(n);
+  std::vector<uint8_t> ready(n, 0);
+  std::vector<const std::vector<uint8_t>*> hmsg;
+  std::vector<size_t> hat;
+  am_engine* eng = nullptr;
+  for (size_t i = 0; i < n; i++) {
+    out[i] = nullptr;
+    lens[i] = 0;
+    am_doc* d = docs[i];
+    if (d->has_binary) { bytes[i] = d->binary; ready[i] = 1; continue; }
+    if (d->state.empty() || (eng && d->eng != eng)) {
+      am_error tmp;
+      uint8_t* p = nullptr;
+      size_t l = 0;
+      if (am_doc_save(d, &p, &l, &tmp)) { E[i] = from_c(tmp); continue; }
+      bytes[i].assign(p, p + l);
+      std::free(p);
+      ready[i] = 1;
+      continue;
+    }
+    eng = d->eng;
+    bool need = false;
+    if (!save_prepare(d->state, bytes[i], need, E[i])) continue;
+    if (need) { hmsg.push_back(&bytes[i]); hat.push_back(i); }
+    else ready[i] = 1;
+  }
+  if (!hmsg.empty()) {
+    std::vector<std::array<uint8_t, 32>> h;
+    if (!gpu_sha256(eng, hmsg, 8, h)) {
+      for (size_t i : hat) E[i] = Err{AM_U_CAPACITY, false, "automerge_amd: GPU hash failed"};
+    } else {
+      for (size_t k = 0; k < hat.size(); k++) { std::memcpy(bytes[hat[k]].data() + 4, h[k].data(), 4); ready[hat[k]] = 1; }
+    }
+  }
+  for (size_t i = 0; i < n; i++) {
+    if (!ready[i]) continue;
+    am_doc* d = docs[i];
+    if (!d->has_binary && !d->state.empty()) { d->binary = bytes[i]; d->has_binary = true; }
+    out[i] = dup_bytes(bytes[i]);
+    lens[i] = bytes[i].size();
+  }
+  return publish(E, codes, msgs);
 }
 
 extern "C" int am_doc_queued(const am_doc* d, size_t i, const uint8_t** data, size_t* len) {

@@ -1076,8 +1076,9 @@ __global__ void __launch_bounds__(256) k_pipe_lens(const am_doc_result* __restri
     if (b.P) {
       const WsLayout L = ws_layout(b);
       const PatchHdr2* h = reinterpret_cast<const PatchHdr2*>(ws + r.ws_off + L.pwire);
-      if (h->magic == AM_PATCH_MAGIC && sizeof(PatchHdr2) + h->nbytes <= L.pwire_cap)
-        p = (sizeof(PatchHdr2) + h->nbytes + 15) & ~15ull;
+      // (AM_DOC_META: the objectMeta blob follows the stream)
+      if (h->magic == AM_PATCH_MAGIC && sizeof(PatchHdr2) + h->nbytes + h->meta_bytes <= L.pwire_cap)
+        p = (sizeof(PatchHdr2) + h->nbytes + h->meta_bytes + 15) & ~15ull;
     }
   }
   olen[d] = o;
@@ -1115,7 +1116,8 @@ __global__ void __launch_bounds__(256) k_pipe_compact(const am_doc_result* __res
     uint32_t pl = 0;
     if (!sm.status && pn) {
       const WsLayout L = ws_layout(bounds[d]);
-      pl = (uint32_t)(sizeof(PatchHdr2) + reinterpret_cast<const PatchHdr2*>(ws + r.ws_off + L.pwire)->nbytes);
+      const PatchHdr2* h = reinterpret_cast<const PatchHdr2*>(ws + r.ws_off + L.pwire);
+      pl = (uint32_t)(sizeof(PatchHdr2) + h->nbytes + h->meta_bytes);
     }
     sm.patch_len = pl;
     sm.out_off = oo;

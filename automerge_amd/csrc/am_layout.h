@@ -154,7 +154,9 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   L.pscr = L.u0;
   const uint64_t pscr_end = L.u0 + (b.P == 1 ? 13 * (R + 1) + 24 * (R + 1) + 16 * (E + 1) + 16 * 10 : 0);
   if (pscr_end > uend) uend = pscr_end;
-  o = uend;
+  // every region (and every document's workspace, placed by an exclusive scan of L.total) starts
+  // 16-byte aligned: the global-mode hot set takes 64-bit atomics and the copies move 16-byte words
+  o = (uend + 15) & ~(uint64_t)15;
   L.hot_total = o;
   // column buffers: a value costs at most 8 LEB bytes plus 2 bytes of RLE headers
   uint64_t cap = 0;

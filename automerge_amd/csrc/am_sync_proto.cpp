@@ -447,8 +447,13 @@ Hashes sorted_unique(Hashes v) {
 
 extern "C" int am_sync_generate(size_t n, am_doc* const* docs, const uint8_t* const* states, const size_t* state_lens,
                                 uint8_t** out_states, size_t* out_state_lens, uint8_t** msgs, size_t* msg_lens,
-                                am_error* errs) {
+                                uint32_t* codes, char** errmsgs) {
   std::vector<Gen> gs(n);
+  {  // the hash graphs of loaded documents (computeHashGraph, new.js:1879-1904) in one batch
+    std::vector<am_doc*> gd(docs, docs + n);
+    std::vector<uint32_t> gc(n);
+    if (n) am_doc_compute_hash_graph_batch(n, gd.data(), gc.data(), nullptr);  // errors resurface below
+  }
   auto fail = [&](Gen& g, const SErr& e) {
     g.failed = true;
     g.err = e;
@@ -549,15 +554,54 @@ extern "C" int am_sync_generate(size_t n, am_doc* const* docs, const uint8_t* co
         fail(g, e);
       }
     }
+    codes[i] = 0;
+    if (errmsgs) errmsgs[i] = nullptr;
     if (g.failed) {
-      to_err(g.err, errs ? &errs[i] : nullptr);
+      codes[i] = (g.err.code ? g.err.code : (uint32_t)AM_E_LOCAL) | (g.err.type_error ? 0x80000000u : 0u);
+      if (errmsgs) {
+        errmsgs[i] = (char*)malloc(g.err.msg.size() + 1);
+        if (errmsgs[i]) memcpy(errmsgs[i], g.err.msg.c_str(), g.err.msg.size() + 1);
+      }
       nfail++;
-    } else if (errs) {
-      errs[i].code = 0;
     }
   }
   return nfail;
 }
+
+namespace {
+// receiveSyncMessage after the changes are applied (sync.js:430-473; advanceHeads :408-413)
+std::vector<uint8_t> recv_finish(am_doc* d, State& s, const Msg& m, const Hashes& before) {
+  if (!m.changes.empty()) {
+    const Hashes after = heads_of(d);
+    Hashes adv;
+    for (const Hash32& h : after)
+      if (!contains(before, h)) adv.push_back(h);
+    for (const Hash32& h : s.shared_heads)
+      if (contains(after, h)) adv.push_back(h);
+    s.shared_heads = sorted_unique(adv);
+  }
+  if (m.changes.empty() && same(m.heads, before)) s.last_sent_heads = m.heads;
+  Hashes known;
+  for (const Hash32& h : m.heads)
+    if (change_index(d, h) >= 0) known.push_back(h);
+  if (known.size() == m.heads.size()) {
+    s.shared_heads = m.heads;
+    if (m.heads.empty()) {  // the peer lost its data: full resync
+      s.last_sent_heads.clear();
+      s.sent_hashes.clear();
+      s.sent_is_array = true;
+    }
+  } else {
+    known.insert(known.end(), s.shared_heads.begin(), s.shared_heads.end());
+    s.shared_heads = sorted_unique(known);
+  }
+  s.has_their_have = s.has_their_heads = s.has_their_need = true;
+  s.their_have = m.have;
+  s.their_heads = m.heads;
+  s.their_need = m.need;
+  return write_state(s);
+}
+}  // namespace
 
 extern "C" int am_sync_receive(am_doc* d, const uint8_t* state, size_t state_len, const uint8_t* msg, size_t msg_len,
                                uint8_t** out_state, size_t* out_state_len, uint8_t** patch, size_t* patch_len,
@@ -576,35 +620,8 @@ extern "C" int am_sync_receive(am_doc* d, const uint8_t* state, size_t state_len
       am_error e;
       if (am_doc_apply_changes_patch(d, bufs.data(), lens.data(), bufs.size(), patch, patch_len, &e)) from_am(e);
       applied = true;
-      // advanceHeads (sync.js:408-413)
-      const Hashes after = heads_of(d);
-      Hashes adv;
-      for (const Hash32& h : after)
-        if (!contains(before, h)) adv.push_back(h);
-      for (const Hash32& h : s.shared_heads)
-        if (contains(after, h)) adv.push_back(h);
-      s.shared_heads = sorted_unique(adv);
     }
-    if (m.changes.empty() && same(m.heads, before)) s.last_sent_heads = m.heads;
-    Hashes known;
-    for (const Hash32& h : m.heads)
-      if (change_index(d, h) >= 0) known.push_back(h);
-    if (known.size() == m.heads.size()) {
-      s.shared_heads = m.heads;
-      if (m.heads.empty()) {  // the peer lost its data: full resync
-        s.last_sent_heads.clear();
-        s.sent_hashes.clear();
-        s.sent_is_array = true;
-      }
-    } else {
-      known.insert(known.end(), s.shared_heads.begin(), s.shared_heads.end());
-      s.shared_heads = sorted_unique(known);
-    }
-    s.has_their_have = s.has_their_heads = s.has_their_need = true;
-    s.their_have = m.have;
-    s.their_heads = m.heads;
-    s.their_need = m.need;
-    const std::vector<uint8_t> o = write_state(s);
+    const std::vector<uint8_t> o = recv_finish(d, s, m, before);
     *out_state = dup(o);
     *out_state_len = o.size();
   } catch (const SErr& e) {
@@ -617,6 +634,135 @@ extern "C" int am_sync_receive(am_doc* d, const uint8_t* state, size_t state_len
   }
   if (err) err->code = 0;
   return 0;
+}
+
+// receiveSyncMessage of n (document, state, message) triples: the messages' changes applied to their
+// documents in ONE batched applyChanges (am_doc_apply_changes_batch), the hash graphs the heads
+// lookups need computed in one batch, then the state updates. codes[i]: 0, or the error (bit 31:
+// TypeError; bit 30: the changes were applied before the error, as am_sync_receive's return 2).
+extern "C" int am_sync_receive_batch(size_t n, am_doc* const* docs, const uint8_t* const* states, const size_t* state_lens,
+                                     const uint8_t* const* msgs, const size_t* msg_lens, uint8_t** out_states,
+                                     size_t* out_state_lens, uint8_t** patches, size_t* patch_lens, am_call_info* info,
+                                     uint32_t* codes, char** errmsgs) {
+  struct R {
+    State s;
+    Msg m;
+    Hashes before;
+    bool failed = false, applied = false, single = false;
+    SErr err;
+  };
+  std::vector<R> rs(n);
+  std::unordered_set<am_doc*> seen;
+  for (size_t i = 0; i < n; i++) {
+    out_states[i] = nullptr;
+    out_state_lens[i] = 0;
+    patches[i] = nullptr;
+    patch_lens[i] = 0;
+    if (info) info[i] = am_call_info{0, 0, 0, nullptr};
+    R& r = rs[i];
+    if (!seen.insert(docs[i]).second) { r.single = true; continue; }  // after the batch, in order
+    try {
+      r.s = read_state(states[i], state_lens[i]);
+      r.m = decode_msg(msgs[i], msg_lens[i]);
+      r.before = heads_of(docs[i]);
+    } catch (const SErr& e) {
+      r.failed = true;
+      r.err = e;
+    }
+  }
+  // every message's changes: one batched applyChanges
+  std::vector<size_t> at, off{0};
+  std::vector<am_doc*> ad;
+  std::vector<const uint8_t*> bufs;
+  std::vector<size_t> lens;
+  for (size_t i = 0; i < n; i++) {
+    R& r = rs[i];
+    if (r.single || r.failed || r.m.changes.empty()) continue;
+    at.push_back(i);
+    ad.push_back(docs[i]);
+    for (auto& c : r.m.changes) { bufs.push_back(c.first); lens.push_back(c.second); }
+    off.push_back(bufs.size());
+  }
+  if (!at.empty()) {
+    std::vector<uint8_t*> pp(at.size());
+    std::vector<size_t> pl(at.size());
+    std::vector<uint32_t> cc(at.size());
+    std::vector<char*> mm(at.size());
+    std::vector<am_call_info> ci(at.size());
+    am_doc_apply_changes_batch(at.size(), ad.data(), off.data(), bufs.data(), lens.data(), pp.data(), pl.data(),
+                               info ? ci.data() : nullptr, cc.data(), mm.data());
+    if (info)
+      for (size_t k = 0; k < at.size(); k++) info[at[k]] = ci[k];
+    for (size_t k = 0; k < at.size(); k++) {
+      R& r = rs[at[k]];
+      if (cc[k]) {
+        r.failed = true;
+        r.err = SErr{(cc[k] & 0x80000000u) != 0, mm[k] ? mm[k] : "", cc[k] & 0x7fffffffu};
+      } else {
+        r.applied = true;
+        patches[at[k]] = pp[k];
+        patch_lens[at[k]] = pl[k];
+      }
+      if (mm[k]) am_free(mm[k]);
+    }
+  }
+  // the hash graphs the heads lookups need (loaded documents), in one batch
+  std::vector<am_doc*> gd;
+  for (size_t i = 0; i < n; i++)
+    if (!rs[i].single && !rs[i].failed && !rs[i].m.heads.empty()) gd.push_back(docs[i]);
+  if (!gd.empty()) {
+    std::vector<uint32_t> gc(gd.size());
+    am_doc_compute_hash_graph_batch(gd.size(), gd.data(), gc.data(), nullptr);  // errors resurface below
+  }
+  int nfail = 0;
+  for (size_t i = 0; i < n; i++) {
+    R& r = rs[i];
+    std::string msg;
+    uint32_t code = 0;
+    if (r.single) {
+      am_error e;
+      const int rc = am_sync_receive(docs[i], states[i], state_lens[i], msgs[i], msg_lens[i], out_states + i,
+                                     out_state_lens + i, patches + i, patch_lens + i, &e);
+      if (!rc && info && patches[i]) {
+        info[i].max_op = am_doc_max_op(docs[i]);
+        info[i].pending = (uint32_t)am_doc_pending(docs[i]);
+        info[i].nheads = (uint32_t)am_doc_get_heads(docs[i], nullptr, 0);
+        info[i].heads = (uint8_t*)malloc(32 * (info[i].nheads ? info[i].nheads : 1));
+        if (info[i].heads) am_doc_get_heads(docs[i], info[i].heads, info[i].nheads);
+      }
+      if (rc) {
+        code = e.code | (e.is_type_error ? 0x80000000u : 0u) | (rc == 2 ? 0x40000000u : 0u);
+        msg = e.message;
+      }
+    } else {
+      if (!r.failed) {
+        try {
+          const std::vector<uint8_t> o = recv_finish(docs[i], r.s, r.m, r.before);
+          out_states[i] = dup(o);
+          out_state_lens[i] = o.size();
+        } catch (const SErr& e) {
+          r.failed = true;
+          r.err = e;
+        }
+      }
+      if (r.failed) {
+        code = (r.err.code ? r.err.code : (uint32_t)AM_E_LOCAL) | (r.err.type_error ? 0x80000000u : 0u) | (r.applied ? 0x40000000u : 0u);
+        msg = r.err.msg;
+        if (patches[i]) { am_free(patches[i]); patches[i] = nullptr; patch_lens[i] = 0; }
+        if (info && info[i].heads) { am_free(info[i].heads); info[i] = am_call_info{0, 0, 0, nullptr}; }
+      }
+    }
+    codes[i] = code;
+    if (errmsgs) {
+      errmsgs[i] = nullptr;
+      if (code) {
+        errmsgs[i] = (char*)malloc(msg.size() + 1);
+        if (errmsgs[i]) memcpy(errmsgs[i], msg.c_str(), msg.size() + 1);
+      }
+    }
+    nfail += code != 0;
+  }
+  return nfail;
 }
 
 // encodeHashes (sync.js:130-139) of a JSON array of hex strings

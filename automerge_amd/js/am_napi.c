@@ -533,7 +533,8 @@ static napi_value js_sync_generate(napi_env env, napi_callback_info info) {
   size_t* osl = (size_t*)calloc(n ? n : 1, sizeof(size_t));
   uint8_t** msg = (uint8_t**)calloc(n ? n : 1, sizeof(uint8_t*));
   size_t* ml = (size_t*)calloc(n ? n : 1, sizeof(size_t));
-  am_error* errs = (am_error*)calloc(n ? n : 1, sizeof(am_error));
+  uint32_t* codes = (uint32_t*)calloc(n ? n : 1, sizeof(uint32_t));
+  char** emsg = (char**)calloc(n ? n : 1, sizeof(char*));
   napi_value res = NULL;
   int ok = 1;
   for (uint32_t i = 0; i < n && ok; i++) {
@@ -544,14 +545,14 @@ static napi_value js_sync_generate(napi_env env, napi_callback_info info) {
     if (ok) docs[i] = b->doc;
   }
   if (ok) {
-    am_sync_generate(n, docs, st, sl, ost, osl, msg, ml, errs);
+    am_sync_generate(n, docs, st, sl, ost, osl, msg, ml, codes, emsg);
     napi_create_array_with_length(env, n, &res);
     for (uint32_t i = 0; i < n; i++) {
       napi_value el;
-      if (errs[i].code) {
+      if (codes[i]) {
         napi_value m;
-        napi_create_string_utf8(env, errs[i].message, NAPI_AUTO_LENGTH, &m);
-        if (errs[i].is_type_error) napi_create_type_error(env, NULL, m, &el);
+        napi_create_string_utf8(env, emsg[i] ? emsg[i] : "", NAPI_AUTO_LENGTH, &m);
+        if (codes[i] & 0x80000000u) napi_create_type_error(env, NULL, m, &el);
         else napi_create_range_error(env, NULL, m, &el);
       } else {
         napi_value nul;
@@ -565,7 +566,9 @@ static napi_value js_sync_generate(napi_env env, napi_callback_info info) {
       am_free(msg[i]);
     }
   }
-  free(docs); free(st); free(sl); free(ost); free(osl); free(msg); free(ml); free(errs);
+  free(docs); free(st); free(sl); free(ost); free(osl); free(msg); free(ml); free(codes);
+  for (uint32_t i = 0; i < n; i++) am_free(emsg[i]);
+  free(emsg);
   return res;
 }
 

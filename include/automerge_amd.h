@@ -224,6 +224,9 @@ uint64_t am_batch_workspace_bytes(am_batch *b);
  * out3[1] = k_doc_fast LDS slice per document (0: none in its envelope), out3[2] = largest k_doc
  * hot working set. Not part of the reference interface (bench/profiling only). */
 int am_batch_kernel_info(am_batch *b, uint64_t *out3);
+/* Workspace plan of one staged document (diagnostics, not part of the reference interface):
+ * R, E, P, hot set, workspace bytes, workspace offset, span_lo, span_hi, runs-from-LDS, input bytes. */
+int am_batch_doc_plan(am_batch *b, uint32_t doc, uint64_t *out10);
 
 /* ---- pipelined batches: the whole job from host memory to host memory ----
  * A stream of batches (each = many documents, one Backend.load + Backend.applyChanges per document,
@@ -300,6 +303,38 @@ int am_doc_change(const am_doc *doc, size_t i, const uint8_t **data, size_t *len
 int am_doc_get_patch(am_doc *doc, uint8_t **out, size_t *len, am_error *err);
 /* i-th enqueued change (this.queue, new.js:1796-1871: changes waiting for missing deps), as given */
 int am_doc_queued(const am_doc *doc, size_t i, const uint8_t **data, size_t *len);
+/* ---- the per-document calls over n handles in ONE GPU batch (the batched backend surface) ----
+ * Same semantics per handle as the single calls above, as if they ran in index order; a handle that
+ * appears twice takes its later calls after the batch, in order. Per call: codes[i] (0 = ok; bit 31
+ * set when the reference throws a TypeError) and, when msgs is non-null, msgs[i] = the error text
+ * (malloc'd, am_free; nullptr when the call succeeded). Output buffers are malloc'd (am_free).
+ * Each returns the number of calls that failed; a failed call leaves its handle unchanged.
+ *   am_doc_load_batch          <- Backend.load           backend.js:104-107 (docs[i] = nullptr on error)
+ *   am_doc_apply_changes_batch <- Backend.applyChanges   backend.js:27-32   (patches != nullptr)
+ *                                 Backend.loadChanges    backend.js:115-120 (patches == nullptr)
+ *     handle i gets the changes bufs[off[i] .. off[i+1]); loaded handles whose changes need the
+ *     hash graph (new.js:1826-1832) have it computed together in one batch and run again.
+ *     info (optional): per call, the handle's maxOp / heads / pending right after that call.
+ *   am_doc_get_patch_batch     <- Backend.getPatch       backend.js:125-127
+ *   am_doc_save_batch          <- Backend.save           backend.js:96-98 (one SHA-256 launch)
+ *   am_doc_compute_hash_graph_batch <- computeHashGraph  new.js:1879-1904 */
+/* What a patch is materialized with (maxOp, deps = heads, pendingChanges), taken right after call i:
+ * heads is malloc'd (am_free), 32 x nheads bytes. */
+typedef struct am_call_info {
+  int64_t max_op;
+  uint32_t pending;
+  uint32_t nheads;
+  uint8_t *heads;
+} am_call_info;
+int am_doc_load_batch(am_engine *eng, size_t n, const uint8_t *const *data, const size_t *lens, am_doc **docs,
+                      uint32_t *codes, char **msgs);
+int am_doc_apply_changes_batch(size_t n, am_doc *const *docs, const size_t *off, const uint8_t *const *bufs,
+                               const size_t *lens, uint8_t **patches, size_t *patch_lens, am_call_info *info,
+                               uint32_t *codes, char **msgs);
+int am_doc_get_patch_batch(size_t n, am_doc *const *docs, uint8_t **out, size_t *lens, am_call_info *info, uint32_t *codes,
+                           char **msgs);
+int am_doc_save_batch(size_t n, am_doc *const *docs, uint8_t **out, size_t *lens, uint32_t *codes, char **msgs);
+int am_doc_compute_hash_graph_batch(size_t n, am_doc *const *docs, uint32_t *codes, char **msgs);
 /* ---- hash-graph queries (BackendDoc, new.js:1913-2020); the graph of a loaded document is
  * computed on first use (computeHashGraph, new.js:1879-1904). Change indexes refer to
  * am_doc_change; arrays are malloc'd (am_free). ----
@@ -343,26 +378,39 @@ int am_doc_apply_local_change(am_doc *doc, const char *json, size_t len, uint8_t
  *   array receiveSyncMessage resets it to) | H sharedHeads | H lastSentHeads | [H theirHeads]
  *   | [H theirNeed] | [uleb n, n x (H lastSync, uleb len, bloom bytes)] | H sentHashes
  * where H = uleb count + count x 32-byte hash (sentHashes in insertion order).
- * am_sync_generate       <- generateSyncMessage(backend, state)  sync.js:281-344, for n documents
+ * am_sync_generate       <- generateSyncMessage(backend, state)  sync.js:327-400, for n documents
  *     at once: their Bloom filters are built in one k_bloom_build launch and their change
- *     selections run in one k_sync_select launch. Per document: out state blob, message (NULL
- *     when none is due) and error; returns the number of documents that failed.
- * am_sync_receive        <- receiveSyncMessage(backend, state, msg) sync.js:381-438; *patch is the
+ *     selections run in one k_sync_select launch; loaded documents get their hash graphs in one
+ *     batch. Per document: out state blob, message (NULL when none is due) and codes[i] / errmsgs[i]
+ *     as the batched per-handle calls; returns the number of documents that failed.
+ * am_sync_receive        <- receiveSyncMessage(backend, state, msg) sync.js:420-473; *patch is the
  *     applyChanges patch log when the message carried changes (else NULL). Returns 0, 1 (error,
  *     document unchanged) or 2 (error after the changes were applied).
- * am_sync_encode_message <- encodeSyncMessage(message)  sync.js:153-170 (message as JSON)
- * am_sync_decode_messages<- decodeSyncMessage(bytes)    sync.js:175-198, n messages: spans of
+ * am_sync_encode_message <- encodeSyncMessage(message)  sync.js:157-171 (message as JSON)
+ * am_sync_decode_messages<- decodeSyncMessage(bytes)    sync.js:177-199, n messages: spans of
  *     message i are spans[span_off[i] .. span_off[i+1]): heads (off, count), need (off, count),
  *     per have: lastSync (off, count) and bloom (off, len), per change (off, len); offsets into
  *     the message, counts[4i..4i+3] = heads, need, have, changes. Returns the number failed.
- * am_sync_encode_state   <- encodeSyncState(state)      sync.js:205-210 (from a state blob)
- * am_sync_decode_state   <- decodeSyncState(bytes)      sync.js:216-224 (to a state blob) */
+ * am_sync_encode_state   <- encodeSyncState(state)      sync.js:206-211 (from a state blob)
+ * am_sync_decode_state   <- decodeSyncState(bytes)      sync.js:217-225 (to a state blob) */
 typedef struct { uint64_t off, len; } am_span;
 int am_bloom_check(const uint8_t *filter, uint64_t len, am_error *err);
 int am_sync_generate(size_t n, am_doc *const *docs, const uint8_t *const *states, const size_t *state_lens,
-                     uint8_t **out_states, size_t *out_state_lens, uint8_t **msgs, size_t *msg_lens, am_error *errs);
+                     uint8_t **out_states, size_t *out_state_lens, uint8_t **msgs, size_t *msg_lens, uint32_t *codes,
+                     char **errmsgs);
 int am_sync_receive(am_doc *doc, const uint8_t *state, size_t state_len, const uint8_t *msg, size_t msg_len,
                     uint8_t **out_state, size_t *out_state_len, uint8_t **patch, size_t *patch_len, am_error *err);
+/* receiveSyncMessage of n (document, state, message) triples in one call: every message's changes
+ * go through ONE am_doc_apply_changes_batch, the hash graphs the heads lookups need are computed in
+ * one batch (am_doc_compute_hash_graph_batch), then each state is updated as am_sync_receive does.
+ * Outputs per triple as am_sync_receive (malloc'd, am_free), info (optional) as
+ * am_doc_apply_changes_batch for the triples that applied changes; codes[i] = 0 or the error code with
+ * bit 31 set for a TypeError and bit 30 set when the changes were applied before the error (the
+ * single call's return 2); errmsgs (optional) as the batched per-handle calls. A document named
+ * twice takes its later triples after the batch, in order. Returns the number that failed. */
+int am_sync_receive_batch(size_t n, am_doc *const *docs, const uint8_t *const *states, const size_t *state_lens,
+                          const uint8_t *const *msgs, const size_t *msg_lens, uint8_t **out_states, size_t *out_state_lens,
+                          uint8_t **patches, size_t *patch_lens, am_call_info *info, uint32_t *codes, char **errmsgs);
 int am_sync_encode_message(const char *json, size_t len, uint8_t **out, size_t *out_len, am_error *err);
 int am_sync_decode_messages(size_t n, const uint8_t *const *msgs, const size_t *lens, am_span **spans,
                             uint64_t *span_off, uint32_t *counts, am_error *errs);

@@ -149,3 +149,71 @@ def _divergent(B, f, sc, handles):
                 return []
             return [(f, sc["name"], i, e["fn"], "known divergence raised", str(x))]
     return [(f, sc["name"], -1, "", "known divergence did not raise", "")]
+
+
+# the batched surface: fn -> (batch function of backend module B, how it takes the args columns)
+BATCHED = {
+    "applyChanges": "applyChangesBatch", "loadChanges": "loadChangesBatch", "load": "loadBatch",
+    "save": "saveBatch", "getPatch": "getPatchBatch", "generateSyncMessage": "generateSyncMessages",
+    "receiveSyncMessage": "receiveSyncMessages",
+}
+
+
+def replay_lockstep(B, files=FILES, stop_at=40):
+    """The logs replayed in lockstep: call k of every scenario of every file at once, the calls of
+    one function in one batched call (BATCHED), the rest one by one. A scenario's calls stay in
+    order, so each sees the same handles and states as in replay(); results are compared the same
+    way. Returns (calls, batched calls, bad)."""
+    scens = [(f, sc) for f in files for sc in load(f)["scenarios"] if (f, sc["name"]) not in KNOWN_DIVERGENT]
+    handles = [{} for _ in scens]
+    live = [True] * len(scens)
+    bad, calls, batched = [], 0, 0
+    k = 0
+    while any(live):
+        groups = {}
+        for j, (f, sc) in enumerate(scens):
+            if not live[j]:
+                continue
+            if k >= len(sc["log"]):
+                live[j] = False
+                continue
+            e = sc["log"][k]
+            args = _args(e["fn"], decode(e["args"], handles[j]))
+            key = e["fn"] if (e["fn"] in BATCHED and len(args) == (1 if e["fn"] in ("save", "getPatch", "load") else
+                                                                    3 if e["fn"] == "receiveSyncMessage" else 2)) else None
+            groups.setdefault(key, []).append((j, e, args))
+        results = {}
+        for key, items in groups.items():
+            if key is None:
+                for j, e, args in items:
+                    try:
+                        results[j] = (getattr(B, e["fn"])(*args), None)
+                    except Exception as x:  # noqa: BLE001 -- the error is the result being compared
+                        results[j] = (None, x)
+                continue
+            cols = list(zip(*[args for _, _, args in items]))
+            out = getattr(B, BATCHED[key])(*[list(c) for c in cols])
+            batched += len(items)
+            for (j, e, _), r in zip(items, out):
+                results[j] = (None, r) if isinstance(r, Exception) else (r, None)
+        for key, items in groups.items():
+            for j, e, _ in items:
+                f, sc = scens[j]
+                calls += 1
+                res, x = results[j]
+                err = None if x is None else {"name": _err_name(x), "message": str(x)}
+                if "error" in e:
+                    if err is None or err["message"] != e["error"]["message"] or err["name"] != e["error"]["name"]:
+                        bad.append((f, sc["name"], k, e["fn"], e["error"], err))
+                    continue
+                if err is not None:
+                    bad.append((f, sc["name"], k, e["fn"], "unexpected", err))
+                    live[j] = False
+                    continue
+                if not match(e["result"], res, handles[j]):
+                    bad.append((f, sc["name"], k, e["fn"], json.dumps(e["result"])[:400], json.dumps(canon(res))[:400]))
+                    live[j] = False
+        if len(bad) >= stop_at:
+            break
+        k += 1
+    return calls, batched, bad

@@ -15,6 +15,8 @@ lib = C.CDLL(_LIB)
 _P = C.c_void_p
 for _name, _res, _args in (
         ("am_workload_c4", C.c_uint64, [C.c_uint64, C.c_uint32, _P, C.c_uint64, _P, _P, C.POINTER(C.c_uint64), C.c_int]),
+        ("am_workload_c5", C.c_uint64, [C.c_uint64, C.c_uint32, C.c_uint32, _P, C.c_uint64, _P, _P, C.POINTER(C.c_uint64),
+                                        C.c_int]),
         ("am_workload_c2", C.c_uint64, [C.c_uint64, C.c_uint32, _P, C.c_uint64, _P, _P, C.POINTER(C.c_uint64), C.c_int]),
         ("am_workload_text", C.c_uint64, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, C.c_uint64, _P, _P,
                                           C.POINTER(C.c_uint64), C.c_int]),
@@ -51,6 +53,21 @@ def c2(first, n, nthreads=None):
     docs = np.empty(n, DOC_DT)
     got = lib.am_workload_c2(first, n, arena.ctypes.data, need, chunks.ctypes.data, docs.ctypes.data, C.byref(ops),
                                nthreads)
+    assert got == need
+    return arena, chunks, docs, int(ops.value)
+
+
+def c5(first, n, per_side=10, nthreads=None):
+    """C5 document pairs [first, first+n): (arena, chunks, docs, ops); pair i = the base chunk, side
+    A's per_side changes, then side B's (chunk order)."""
+    nthreads = nthreads or min(16, os.cpu_count() or 1)
+    ops = C.c_uint64()
+    need = lib.am_workload_c5(first, n, per_side, None, 0, None, None, C.byref(ops), nthreads)
+    arena = np.empty(need, np.uint8)
+    chunks = np.empty((1 + 2 * per_side) * n, CHUNK_DT)
+    docs = np.empty(n, DOC_DT)
+    got = lib.am_workload_c5(first, n, per_side, arena.ctypes.data, need, chunks.ctypes.data, docs.ctypes.data,
+                             C.byref(ops), nthreads)
     assert got == need
     return arena, chunks, docs, int(ops.value)
 

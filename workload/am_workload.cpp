@@ -224,6 +224,45 @@ void gen_c4(uint32_t doc_index, DocOut& out) {
   out.ops = 60;
 }
 
+// C5 (SURVEY.md §8(d), configs[4]): one document pair = the C4 base document plus two concurrent
+// chains of `per_side` changes (actor 1 for side A, actor 2 for side B; each change 4 list inserts
+// + 1 conflicting title set, as C4's), so each side holds per_side changes the other lacks since
+// their last sync (the base). changes = A's chain, then B's chain.
+void gen_c5(uint32_t doc_index, uint32_t per_side, DocOut& out) {
+  uint32_t s = doc_index ^ 0x5c5c5c5cu;
+  std::vector<Actor> actors;
+  uint8_t h0[32];
+  out.base = c4_base_from(s, actors, h0);
+  for (int i = 1; i <= 2; i++) {
+    std::vector<uint8_t> last(h0, h0 + 32);
+    int64_t last_title_ctr = 2;
+    int last_title_actor = 0;
+    std::vector<int64_t> own;
+    for (uint32_t j = 0; j < per_side; j++) {
+      const int64_t start = 3 + 5 * (int64_t)j;
+      std::vector<Op> ops;
+      int ref_actor = -1;
+      int64_t ref_ctr = 0;
+      if (!own.empty() && lcg(s) % 4 != 0) { ref_ctr = own[lcg(s) % own.size()]; ref_actor = i; }
+      for (int k = 0; k < 4; k++) {
+        const char c = (char)(97 + lcg(s) % 26);
+        ops.push_back({0, 1, "", ref_actor, ref_ctr, true, 1, 6, 0, std::string(1, c), {}});
+        own.push_back(start + k);
+        ref_actor = i;
+        ref_ctr = start + k;
+      }
+      std::string title = "s" + std::to_string(i) + "." + std::to_string(j) + "." + std::to_string(lcg(s) % 1000);
+      ops.push_back({-1, 0, "title", -1, 0, false, 1, 6, 0, title, {{last_title_ctr, last_title_actor}}});
+      last_title_ctr = start + 4;
+      last_title_actor = i;
+      uint8_t h[32];
+      out.changes.push_back(encode_change(actors, i, 1 + (int64_t)j, start, {last}, ops, h));
+      last.assign(h, h + 32);
+    }
+  }
+  out.ops = 10ull * per_side;
+}
+
 // C2 (SURVEY.md §8(d), configs[1]): change 1 by actor 0 sets k0..k7 (int), a counter 'count' and a
 // string 'name'; two concurrent changes (actors 1, 2) increment the counter and overwrite k1.
 // JS generator: tests/golden/gen/make_fixtures.js c2Doc (same LCG call order).
@@ -467,6 +506,14 @@ uint64_t am_workload_c4(uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap
 uint64_t am_workload_c2(uint64_t first, uint32_t n, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks, am_doc_desc* docs,
                         uint64_t* ops_out, int nthreads) {
   return generate(gen_c2, 2, first, n, arena, cap, chunks, docs, ops_out, nthreads);
+}
+
+/* C5 document pairs [first, first + n) (gen_c5 above): base chunk + 2 * per_side change chunks
+ * each (side A's chain, then side B's). */
+uint64_t am_workload_c5(uint64_t first, uint32_t n, uint32_t per_side, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks,
+                        am_doc_desc* docs, uint64_t* ops_out, int nthreads) {
+  auto gen = [=](uint32_t d, DocOut& o) { gen_c5(d, per_side, o); };
+  return generate(gen, mix_key(5, per_side, 0, 0), first, n, arena, cap, chunks, docs, ops_out, nthreads);
 }
 
 /* Text editing histories (gen_text above; C1: cross_every 0, C3: cross_every 10): documents

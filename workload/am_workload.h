@@ -18,6 +18,10 @@ uint64_t am_workload_c4(uint64_t first_doc, uint32_t ndocs, uint8_t *arena, uint
  * two concurrent changes incrementing the counter and overwriting k1), 3 chunks per document. */
 uint64_t am_workload_c2(uint64_t first_doc, uint32_t ndocs, uint8_t *arena, uint64_t cap, am_chunk_desc *chunks,
                         am_doc_desc *docs, uint64_t *ops_out, int nthreads);
+/* C5 (configs[4]): document pair i = the C4 base + per_side changes by actor 1 (side A) and
+ * per_side concurrent changes by actor 2 (side B); 1 + 2 * per_side chunks per pair. */
+uint64_t am_workload_c5(uint64_t first_doc, uint32_t ndocs, uint32_t per_side, uint8_t *arena, uint64_t cap,
+                        am_chunk_desc *chunks, am_doc_desc *docs, uint64_t *ops_out, int nthreads);
 /* Text editing histories (C1: cross_every 0, two actors concurrent from the same base; C3:
  * cross_every 10, interleaved): document i = Backend.init() + 1 + nchanges change chunks (change 0
  * = makeText), per_change ops each (1/5 deletes of live elements, otherwise one-character
