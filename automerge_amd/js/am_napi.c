@@ -662,6 +662,215 @@ static napi_value js_sync_state_conv(napi_env env, napi_callback_info info, int 
 static napi_value js_sync_encode_state(napi_env env, napi_callback_info info) { return js_sync_state_conv(env, info, 1); }
 static napi_value js_sync_decode_state(napi_env env, napi_callback_info info) { return js_sync_state_conv(env, info, 0); }
 
+// ---- the batched surface (am_doc_*_batch, am_sync_receive_batch): one GPU batch per call; per
+// item the single call's result, or its error object in its place ----
+static napi_value err_obj(napi_env env, uint32_t code, const char* msg) {
+  napi_value m, e;
+  napi_create_string_utf8(env, msg ? msg : "", NAPI_AUTO_LENGTH, &m);
+  if (code & 0x80000000u) napi_create_type_error(env, NULL, m, &e);
+  else napi_create_range_error(env, NULL, m, &e);
+  if (code & 0x40000000u) {
+    napi_value t;
+    napi_get_boolean(env, true, &t);
+    napi_set_named_property(env, e, "applied", t);
+  }
+  return e;
+}
+// {log, maxOp, heads, pending}: what a patch log is materialized with, as of its call
+static napi_value call_result(napi_env env, uint8_t* log, size_t len, am_call_info* ci) {
+  napi_value o, v;
+  napi_create_object(env, &o);
+  napi_set_named_property(env, o, "log", new_u8(env, log, len));
+  napi_create_double(env, (double)ci->max_op, &v);
+  napi_set_named_property(env, o, "maxOp", v);
+  napi_set_named_property(env, o, "heads", hex_list(env, ci->heads, ci->nheads));
+  napi_create_uint32(env, ci->pending, &v);
+  napi_set_named_property(env, o, "pending", v);
+  am_free(ci->heads);
+  ci->heads = NULL;
+  return o;
+}
+static int handles_of(napi_env env, napi_value arr, uint32_t n, am_doc** docs) {
+  for (uint32_t i = 0; i < n; i++) {
+    napi_value hv;
+    DocBox* b;
+    if (napi_get_element(env, arr, i, &hv) != napi_ok || (b = get_box(env, hv)) == NULL) return 0;
+    docs[i] = b->doc;
+  }
+  return 1;
+}
+#define NA(n) ((n) ? (n) : 1)
+
+// docLoadBatch([Uint8Array]) -> [handle | Error]
+static napi_value js_doc_load_batch(napi_env env, napi_callback_info info) {
+  ARGS(1)
+  uint32_t n = 0;
+  NAPI_OK(napi_get_array_length(env, argv[0], &n));
+  am_engine* e = engine(env);
+  if (!e) return NULL;
+  const uint8_t** data = (const uint8_t**)calloc(NA(n), sizeof(uint8_t*));
+  size_t* lens = (size_t*)calloc(NA(n), sizeof(size_t));
+  am_doc** docs = (am_doc**)calloc(NA(n), sizeof(am_doc*));
+  uint32_t* codes = (uint32_t*)calloc(NA(n), sizeof(uint32_t));
+  char** msgs = (char**)calloc(NA(n), sizeof(char*));
+  napi_value res = NULL;
+  int ok = 1;
+  for (uint32_t i = 0; i < n && ok; i++) {
+    napi_value v;
+    ok = napi_get_element(env, argv[0], i, &v) == napi_ok && arg_bytes(env, v, &data[i], &lens[i]);
+  }
+  if (ok) {
+    am_doc_load_batch(e, n, data, lens, docs, codes, msgs);
+    napi_create_array_with_length(env, n, &res);
+    for (uint32_t i = 0; i < n; i++) napi_set_element(env, res, i, codes[i] ? err_obj(env, codes[i], msgs[i]) : wrap_doc(env, docs[i]));
+  }
+  for (uint32_t i = 0; i < n; i++) am_free(msgs[i]);
+  free(data); free(lens); free(docs); free(codes); free(msgs);
+  return res;
+}
+
+// docApplyBatch([handle], [[Uint8Array]], wantPatch) -> [{log, maxOp, heads, pending} | null | Error]
+static napi_value js_doc_apply_batch(napi_env env, napi_callback_info info) {
+  ARGS(3)
+  uint32_t n = 0;
+  NAPI_OK(napi_get_array_length(env, argv[0], &n));
+  bool want = false;
+  napi_get_value_bool(env, argv[2], &want);
+  am_doc** docs = (am_doc**)calloc(NA(n), sizeof(am_doc*));
+  size_t* off = (size_t*)calloc(n + 1, sizeof(size_t));
+  uint8_t** pats = (uint8_t**)calloc(NA(n), sizeof(uint8_t*));
+  size_t* pl = (size_t*)calloc(NA(n), sizeof(size_t));
+  am_call_info* ci = (am_call_info*)calloc(NA(n), sizeof(am_call_info));
+  uint32_t* codes = (uint32_t*)calloc(NA(n), sizeof(uint32_t));
+  char** msgs = (char**)calloc(NA(n), sizeof(char*));
+  const uint8_t** bufs = NULL;
+  size_t* lens = NULL;
+  size_t nb = 0, cap = 0;
+  napi_value res = NULL;
+  int ok = handles_of(env, argv[0], n, docs);
+  for (uint32_t i = 0; i < n && ok; i++) {
+    napi_value cl;
+    uint32_t k = 0;
+    bool is_arr = false;
+    ok = napi_get_element(env, argv[1], i, &cl) == napi_ok && napi_is_array(env, cl, &is_arr) == napi_ok && is_arr &&
+         napi_get_array_length(env, cl, &k) == napi_ok;
+    if (!ok) { napi_throw_type_error(env, NULL, "Pass an array of changes"); break; }
+    if (nb + k > cap) {
+      cap = 2 * (nb + k) + 16;
+      bufs = (const uint8_t**)realloc(bufs, cap * sizeof(uint8_t*));
+      lens = (size_t*)realloc(lens, cap * sizeof(size_t));
+    }
+    for (uint32_t j = 0; j < k && ok; j++) {
+      napi_value el;
+      ok = napi_get_element(env, cl, j, &el) == napi_ok && get_bytes(env, el, &bufs[nb], &lens[nb]);
+      if (!ok) napi_throw_type_error(env, NULL, "Change is not a byte array");
+      nb++;
+    }
+    off[i + 1] = nb;
+  }
+  if (ok) {
+    am_doc_apply_changes_batch(n, docs, off, bufs ? bufs : (const uint8_t**)pats, lens ? lens : pl, want ? pats : NULL,
+                               want ? pl : NULL, ci, codes, msgs);
+    napi_create_array_with_length(env, n, &res);
+    for (uint32_t i = 0; i < n; i++) {
+      napi_value el;
+      if (codes[i]) {
+        el = err_obj(env, codes[i], msgs[i]);
+      } else if (want) {
+        el = call_result(env, pats[i], pl[i], &ci[i]);
+      } else {
+        napi_get_null(env, &el);
+        am_free(ci[i].heads);
+      }
+      napi_set_element(env, res, i, el);
+      am_free(pats[i]);
+    }
+  }
+  for (uint32_t i = 0; i < n; i++) am_free(msgs[i]);
+  free(docs); free(off); free(pats); free(pl); free(ci); free(codes); free(msgs); free(bufs); free(lens);
+  return res;
+}
+
+// docSaveBatch([handle]) -> [Uint8Array | Error]; docPatchBatch([handle]) -> [{log, ...} | Error]
+static napi_value save_or_patch_batch(napi_env env, napi_callback_info info, int patch) {
+  ARGS(1)
+  uint32_t n = 0;
+  NAPI_OK(napi_get_array_length(env, argv[0], &n));
+  am_doc** docs = (am_doc**)calloc(NA(n), sizeof(am_doc*));
+  uint8_t** out = (uint8_t**)calloc(NA(n), sizeof(uint8_t*));
+  size_t* ol = (size_t*)calloc(NA(n), sizeof(size_t));
+  am_call_info* ci = (am_call_info*)calloc(NA(n), sizeof(am_call_info));
+  uint32_t* codes = (uint32_t*)calloc(NA(n), sizeof(uint32_t));
+  char** msgs = (char**)calloc(NA(n), sizeof(char*));
+  napi_value res = NULL;
+  if (handles_of(env, argv[0], n, docs)) {
+    if (patch) am_doc_get_patch_batch(n, docs, out, ol, ci, codes, msgs);
+    else am_doc_save_batch(n, docs, out, ol, codes, msgs);
+    napi_create_array_with_length(env, n, &res);
+    for (uint32_t i = 0; i < n; i++) {
+      napi_value el = codes[i] ? err_obj(env, codes[i], msgs[i]) : patch ? call_result(env, out[i], ol[i], &ci[i])
+                                                                          : new_u8(env, out[i], ol[i]);
+      napi_set_element(env, res, i, el);
+      am_free(out[i]);
+      am_free(msgs[i]);
+    }
+  }
+  free(docs); free(out); free(ol); free(ci); free(codes); free(msgs);
+  return res;
+}
+static napi_value js_doc_save_batch(napi_env env, napi_callback_info info) { return save_or_patch_batch(env, info, 0); }
+static napi_value js_doc_patch_batch(napi_env env, napi_callback_info info) { return save_or_patch_batch(env, info, 1); }
+
+// syncReceiveBatch([handle], [stateBlob], [message]) -> [[stateBlob, {log, ...} | null] | Error]
+static napi_value js_sync_receive_batch(napi_env env, napi_callback_info info) {
+  ARGS(3)
+  uint32_t n = 0;
+  NAPI_OK(napi_get_array_length(env, argv[0], &n));
+  am_doc** docs = (am_doc**)calloc(NA(n), sizeof(am_doc*));
+  const uint8_t** st = (const uint8_t**)calloc(NA(n), sizeof(uint8_t*));
+  size_t* sl = (size_t*)calloc(NA(n), sizeof(size_t));
+  const uint8_t** m = (const uint8_t**)calloc(NA(n), sizeof(uint8_t*));
+  size_t* ml = (size_t*)calloc(NA(n), sizeof(size_t));
+  uint8_t** ost = (uint8_t**)calloc(NA(n), sizeof(uint8_t*));
+  size_t* osl = (size_t*)calloc(NA(n), sizeof(size_t));
+  uint8_t** pa = (uint8_t**)calloc(NA(n), sizeof(uint8_t*));
+  size_t* pl = (size_t*)calloc(NA(n), sizeof(size_t));
+  am_call_info* ci = (am_call_info*)calloc(NA(n), sizeof(am_call_info));
+  uint32_t* codes = (uint32_t*)calloc(NA(n), sizeof(uint32_t));
+  char** msgs = (char**)calloc(NA(n), sizeof(char*));
+  napi_value res = NULL;
+  int ok = handles_of(env, argv[0], n, docs);
+  for (uint32_t i = 0; i < n && ok; i++) {
+    napi_value a, b;
+    ok = napi_get_element(env, argv[1], i, &a) == napi_ok && arg_bytes(env, a, &st[i], &sl[i]) &&
+         napi_get_element(env, argv[2], i, &b) == napi_ok && arg_bytes(env, b, &m[i], &ml[i]);
+  }
+  if (ok) {
+    am_sync_receive_batch(n, docs, st, sl, m, ml, ost, osl, pa, pl, ci, codes, msgs);
+    napi_create_array_with_length(env, n, &res);
+    for (uint32_t i = 0; i < n; i++) {
+      napi_value el;
+      if (codes[i]) {
+        el = err_obj(env, codes[i], msgs[i]);
+      } else {
+        napi_value nul;
+        napi_get_null(env, &nul);
+        napi_create_array_with_length(env, 2, &el);
+        napi_set_element(env, el, 0, new_u8(env, ost[i], osl[i]));
+        napi_set_element(env, el, 1, pa[i] ? call_result(env, pa[i], pl[i], &ci[i]) : nul);
+      }
+      napi_set_element(env, res, i, el);
+      am_free(ost[i]);
+      am_free(pa[i]);
+      am_free(ci[i].heads);
+      am_free(msgs[i]);
+    }
+  }
+  free(docs); free(st); free(sl); free(m); free(ml); free(ost); free(osl); free(pa); free(pl); free(ci); free(codes);
+  free(msgs);
+  return res;
+}
+
 static napi_value js_version(napi_env env, napi_callback_info info) {
   (void)info;
   napi_value v;
@@ -689,6 +898,11 @@ static napi_value init_module(napi_env env, napi_value exports) {
       {"docMissingDeps", 0, js_doc_missing_deps, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
       {"docApplyLocal", 0, js_doc_apply_local, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
       {"encodeChange", 0, js_encode_change, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docLoadBatch", 0, js_doc_load_batch, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docApplyBatch", 0, js_doc_apply_batch, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docSaveBatch", 0, js_doc_save_batch, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"docPatchBatch", 0, js_doc_patch_batch, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
+      {"syncReceiveBatch", 0, js_sync_receive_batch, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
       {"syncGenerate", 0, js_sync_generate, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
       {"syncReceive", 0, js_sync_receive, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},
       {"syncEncodeMessage", 0, js_sync_encode_message, 0, 0, 0, (napi_property_attributes)(napi_writable | napi_enumerable | napi_configurable), 0},

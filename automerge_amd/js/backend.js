@@ -403,11 +403,115 @@ function receiveSyncMessage(backend, oldSyncState, binaryMessage) {
   return [backend, syncState, patch]
 }
 
+// ---- the batched surface: the same calls over many documents, ONE GPU batch per call
+// (am_doc_*_batch, am_sync_receive_batch). Per item the single call's result, or its error object in
+// its place (nothing is thrown for one bad item). Patches are materialized lazily: the [state, patch]
+// pairs carry the engine's log and build the patch object on first access of pair[1]. ----
+function lazyPatch(pair, at, r) {
+  let cached
+  Object.defineProperty(pair, at, {
+    enumerable: true,
+    get() { return cached || (cached = materializePatch(r.log, r.heads, r.pending, r.maxOp)) }
+  })
+  return pair
+}
+function partition(items, prep) {
+  const idx = [], vals = [], out = new Array(items.length)
+  items.forEach((x, i) => {
+    try { vals.push(prep(x, i)); idx.push(i) } catch (e) { out[i] = e }
+  })
+  return [idx, vals, out]
+}
+
+function loadBatch(datas) {
+  return native.docLoadBatch(datas).map(r => r instanceof Error ? r : {state: r, heads: native.docHeads(r)})
+}
+
+function applyBatch(backends, changeLists, wantPatch) {
+  const [idx, states, out] = partition(backends, b => backendState(b))
+  const res = native.docApplyBatch(states, idx.map(i => changeLists[i]), wantPatch)
+  res.forEach((r, k) => {
+    const i = idx[k]
+    if (r instanceof Error) { out[i] = r; return }
+    backends[i].frozen = true
+    if (!wantPatch) { out[i] = {state: states[k], heads: native.docHeads(states[k])}; return }
+    out[i] = lazyPatch([{state: states[k], heads: r.heads}, null], 1, r)
+  })
+  return out
+}
+const applyChangesBatch = (backends, changeLists) => applyBatch(backends, changeLists, true)
+const loadChangesBatch = (backends, changeLists) => applyBatch(backends, changeLists, false)
+
+function saveBatch(backends) {
+  const [idx, states, out] = partition(backends, b => backendState(b))
+  native.docSaveBatch(states).forEach((r, k) => { out[idx[k]] = r })
+  return out
+}
+
+// [patch | Error]; each patch object is built when its index is first read
+function getPatchBatch(backends) {
+  const [idx, states, out] = partition(backends, b => backendState(b))
+  native.docPatchBatch(states).forEach((r, k) => {
+    if (r instanceof Error) out[idx[k]] = r
+    else lazyPatch(out, idx[k], r)
+  })
+  return out
+}
+
+function generateSyncMessages(backends, syncStates) {
+  const [idx, vals, out] = partition(backends, (b, i) => {
+    if (!b) throw new Error('generateSyncMessage called with no Automerge document')
+    if (!syncStates[i]) throw new Error('generateSyncMessage requires a syncState, which can be created with initSyncState()')
+    return [backendState(b), packState(syncStates[i])]
+  })
+  native.syncGenerate(vals.map(v => v[0]), vals.map(v => v[1])).forEach((r, k) => {
+    const i = idx[k]
+    if (r instanceof Error) { out[i] = r; return }
+    const [blob, message] = r
+    if (message === null || Buffer.compare(Buffer.from(blob), Buffer.from(vals[k][1])) === 0) { out[i] = [syncStates[i], message]; return }
+    const next = unpackState(blob)
+    out[i] = [Object.assign({}, syncStates[i], {lastSentHeads: next.lastSentHeads, sentHashes: next.sentHashes}), message]
+  })
+  return out
+}
+
+function receiveSyncMessages(backends, oldSyncStates, binaryMessages) {
+  const [idx, vals, out] = partition(backends, (b, i) => {
+    if (!b) throw new Error('generateSyncMessage called with no Automerge document')
+    if (!oldSyncStates[i]) throw new Error('generateSyncMessage requires a syncState, which can be created with initSyncState()')
+    const message = decodeSyncMessage(binaryMessages[i])
+    const state = (message.changes.length > 0 || message.heads.length > 0) ? backendState(b) : b.state
+    return [state, packState(oldSyncStates[i]), binaryMessages[i], message]
+  })
+  native.syncReceiveBatch(vals.map(v => v[0]), vals.map(v => v[1]), vals.map(v => v[2])).forEach((r, k) => {
+    const i = idx[k], [state, , , message] = vals[k]
+    let backend = backends[i]
+    if (r instanceof Error) {
+      if (r.applied) backend.frozen = true
+      out[i] = r
+      return
+    }
+    const s = unpackState(r[0])
+    const syncState = {sharedHeads: s.sharedHeads, lastSentHeads: s.lastSentHeads, theirHave: message.have,
+                       theirHeads: message.heads, theirNeed: message.need, sentHashes: s.sentHashes}
+    if (!Array.isArray(s.sentHashes)) syncState.sentHashes = oldSyncStates[i].sentHashes
+    if (message.changes.length > 0) {
+      backend.frozen = true
+      backend = {state, heads: r[1].heads}
+      out[i] = lazyPatch([backend, syncState, null], 2, r[1])
+    } else {
+      out[i] = [backend, syncState, null]
+    }
+  })
+  return out
+}
+
 module.exports = {
   init, clone, free, applyChanges, applyLocalChange, save, load, loadChanges, getPatch,
   getHeads, getAllChanges, getChanges, getChangesAdded, getChangeByHash, getMissingDeps,
   receiveSyncMessage, generateSyncMessage, encodeSyncMessage, decodeSyncMessage, encodeSyncState, decodeSyncState,
   initSyncState,
+  loadBatch, applyChangesBatch, loadChangesBatch, saveBatch, getPatchBatch, generateSyncMessages, receiveSyncMessages,
   encodeChange: change => native.encodeChange(requestJSON(change)),  // columnar.js encodeChange (tests)
   engineVersion: native.version,
   _materializePatch: materializePatch  // host stage of getPatch (exported for tests)

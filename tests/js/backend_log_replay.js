@@ -68,6 +68,62 @@ function match(rec, x, h, p = '') {
 // "unsupported" error
 const KNOWN_DIVERGENT = new Set([])  // none since round 4 (the null action is restated)
 const files = (process.argv[2] || 'sync,sync_random,objmeta,backend,test,text,table,errors').split(',')
+// --lockstep: call k of every scenario at once, the calls of one batched function in one call
+// (BATCHED), the rest one by one; results compared the same way
+const BATCHED = {applyChanges: 'applyChangesBatch', loadChanges: 'loadChangesBatch', load: 'loadBatch', save: 'saveBatch',
+                 getPatch: 'getPatchBatch', generateSyncMessage: 'generateSyncMessages', receiveSyncMessage: 'receiveSyncMessages'}
+const ARITY = {save: 1, getPatch: 1, load: 1, receiveSyncMessage: 3}
+if (process.argv[3] === '--lockstep') {
+  const scens = []
+  for (const f of files) for (const sc of JSON.parse(fs.readFileSync(path.join(GOLDEN, `backend_log_${f}.json`))).scenarios) scens.push([f, sc, new Map()])
+  const live = scens.map(() => true), bad = []
+  let calls = 0, batched = 0
+  for (let k = 0; live.some(x => x) && bad.length < 40; k++) {
+    const groups = new Map()
+    scens.forEach(([f, sc, h], j) => {
+      if (!live[j]) return
+      if (k >= sc.log.length) { live[j] = false; return }
+      const e = sc.log[k], args = decode(e.args, h)
+      while (args.length && args[args.length - 1] === undefined) args.pop()
+      const key = (e.fn in BATCHED && args.length === (ARITY[e.fn] || 2)) ? e.fn : null
+      if (!groups.has(key)) groups.set(key, [])
+      groups.get(key).push([j, e, args])
+    })
+    const results = new Map()
+    for (const [key, items] of groups) {
+      if (key === null) {
+        for (const [j, e, args] of items) {
+          try { results.set(j, [B[e.fn](...args), null]) } catch (x) { results.set(j, [undefined, x]) }
+        }
+        continue
+      }
+      const cols = items[0][2].map((_, c) => items.map(it => it[2][c]))
+      const out = B[BATCHED[key]](...cols)
+      batched += items.length
+      items.forEach(([j], q) => results.set(j, out[q] instanceof Error ? [undefined, out[q]] : [out[q], null]))
+    }
+    for (const items of groups.values()) {
+      for (const [j, e] of items) {
+        const [f, sc, h] = scens[j]
+        calls++
+        const [res, x] = results.get(j)
+        const err = x ? {name: x.constructor.name, message: x.message} : null
+        if (e.error) {
+          if (!err || err.message !== e.error.message || err.name !== e.error.name) bad.push({file: f, scenario: sc.name, k, fn: e.fn, want: e.error, got: err || 'no error'})
+          continue
+        }
+        if (err) { bad.push({file: f, scenario: sc.name, k, fn: e.fn, unexpected: err}); live[j] = false; continue }
+        if (!match(e.result, res, h)) {
+          bad.push({file: f, scenario: sc.name, k, fn: e.fn, where, want: JSON.stringify(e.result).slice(0, 400),
+                    got: JSON.stringify(canon(res)).slice(0, 400)})
+          live[j] = false
+        }
+      }
+    }
+  }
+  console.log(JSON.stringify({files, lockstep: true, calls, batched, nbad: bad.length, bad: bad.slice(0, 20)}))
+  process.exit(0)
+}
 const bad = [], perFn = {}
 let calls = 0, scenarios = 0
 for (const f of files) {

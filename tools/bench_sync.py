@@ -65,7 +65,7 @@ def e2e(args):
     clen = (C.c_size_t * len(flat))(*[len(c) for c in flat])
     off = np.arange(n + 1, dtype=np.uint64) * K
     t0 = time.perf_counter()
-    bad = N.lib.am_doc_apply_changes_batch(n, handles.ctypes.data, off.ctypes.data, carr, clen, None, None,
+    bad = N.lib.am_doc_apply_changes_batch(n, handles.ctypes.data, off.ctypes.data, carr, clen, None, None, None,
                                            codes.ctypes.data, None)
     setup_apply_s = time.perf_counter() - t0
     assert bad == 0, int(bad)
@@ -119,7 +119,7 @@ def e2e(args):
         t0 = time.perf_counter()
         bad = N.lib.am_sync_receive_batch(m, rh.ctypes.data, rs.ctypes.data, rsl.ctypes.data, mm.ctypes.data,
                                           mml.ctypes.data, ost2.ctypes.data, ostl2.ctypes.data, pat.ctypes.data,
-                                          pl.ctypes.data, rc.ctypes.data, None)
+                                          pl.ctypes.data, None, rc.ctypes.data, None)
         t_recv += time.perf_counter() - t0
         assert bad == 0, (int(bad), int(rc[rc != 0][0]) if bad else 0)
         for p in list(st[recv]) + list(mm) + list(pat[pat != 0]):
