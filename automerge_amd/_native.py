@@ -154,6 +154,7 @@ _sigs = {
     "am_doc_get_patch_batch": (C.c_int, [C.c_size_t, P, P, P, P, P, P]),
     "am_doc_save_batch": (C.c_int, [C.c_size_t, P, P, P, P, P]),
     "am_doc_compute_hash_graph_batch": (C.c_int, [C.c_size_t, P, P, P]),
+    "am_doc_graph_ready": (C.c_int, [P]),
     "am_host_alloc": (P, [C.c_size_t]),
     "am_host_free": (None, [P]),
     "am_pipe_create": (P, [P, C.POINTER(PipeCaps), C.POINTER(Error)]),

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <functional>
 #include <cstdarg>
 #include <cstdio>
@@ -21,6 +22,7 @@
 
 #include "am_graph.h"
 #include "am_launch.h"
+#include "am_par.h"
 #include "am_patch.h"
 
 namespace {
@@ -276,7 +278,7 @@ std::vector<uint8_t> make_chunk(const uint8_t checksum[4], uint8_t type, const s
 struct CollectBufs {
   DevBuf<uint64_t> olen, ooff, plen, poff, tmp, totals;
   DevBuf<am_doc_summary> summ;
-  DevBuf<uint8_t> out, pat;
+  DevBuf<uint8_t> out, pat, hashes;
 };
 struct am_engine {
   int device = 0;
@@ -284,6 +286,7 @@ struct am_engine {
   hipEvent_t ev[5] = {};
   am_batch* scratch = nullptr;  // batch reused by the per-document API
   void* hist = nullptr;         // device buffers of the history batches (am_hist.hip)
+  void* sync = nullptr;         // device buffers of the Bloom / selection calls (am_sync.hip)
   CollectBufs* coll = nullptr;  // the batched per-handle calls
 };
 
@@ -331,6 +334,7 @@ extern "C" const char* am_version(void) { return "automerge_amd 0.1 (gfx950)"; }
 hipStream_t am_engine_stream(am_engine* e) { return e->stream; }
 int am_engine_device(am_engine* e) { return e->device; }
 void*& am_engine_hist(am_engine* e) { return e->hist; }
+void*& am_engine_sync(am_engine* e) { return e->sync; }
 
 extern "C" am_engine* am_engine_create(int device, am_error* err) {
   int n = 0;
@@ -363,6 +367,7 @@ extern "C" void am_engine_destroy(am_engine* eng) {
   set_device(eng);
   am_batch_destroy(eng->scratch);
   am_hist_cache_free(eng->hist);
+  am_sync_cache_free(eng->sync);
   delete eng->coll;
   for (auto& ev : eng->ev) (void)hipEventDestroy(ev);
   (void)hipStreamDestroy(eng->stream);
@@ -1254,98 +1259,158 @@ struct ManyOut {
   Err err;
   bool ok = false;
 };
+// AM_SYNC_PROFILE=1: stage wall times of the batched per-handle calls on stderr
+struct HostClock {
+  bool on = std::getenv("AM_SYNC_PROFILE") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  std::string line;
+  void mark(const char* what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    char b[64];
+    std::snprintf(b, sizeof b, " %s=%.1fms", what, std::chrono::duration<double, std::milli>(now - t).count());
+    line += b;
+    t = now;
+  }
+  void print(const char* call, size_t n) {
+    if (on) std::fprintf(stderr, "[am_batch] %s n=%zu%s\n", call, n, line.c_str());
+  }
+};
+
 bool run_many(am_engine* e, const std::vector<ManyJob>& jobs, std::vector<ManyOut>& outs, Err& err) {
+  HostClock clk;
   const size_t n = jobs.size();
   outs.assign(n, ManyOut());
   if (!n) return true;
-  std::vector<uint8_t> arena;
-  std::vector<am_chunk_desc> cds;
+  // layout: per document its base and changes adjacent, then every objectMeta blob; offsets first,
+  // then the copies on the host workers
+  std::vector<uint64_t> aoff(n + 1), moff(n + 1);
+  std::vector<uint32_t> c0(n + 1), kb(n + 1);
   std::vector<am_doc_desc> dds(n);
-  std::vector<am_known_hash> known;
-  std::vector<uint32_t> c0(n), cn(n);
+  c0[0] = 0;
+  aoff[0] = 0;
+  kb[0] = 0;
   for (size_t i = 0; i < n; i++) {
+    const ManyJob& j = jobs[i];
+    uint64_t bytes = (j.base ? j.base->size() : 0);
+    uint32_t nc = (j.base && !j.base->empty()) ? 1u : 0u;
+    if (j.chg)
+      for (auto& c : *j.chg) bytes += c.size();
+    nc += j.chg ? (uint32_t)j.chg->size() : 0u;
+    aoff[i + 1] = aoff[i] + bytes;
+    c0[i + 1] = c0[i] + nc;
+    kb[i + 1] = kb[i] + (j.known ? (uint32_t)j.known->size() : 0u);
+  }
+  moff[0] = aoff[n];
+  uint32_t nmeta = 0;
+  for (size_t i = 0; i < n; i++) {
+    const bool m = jobs[i].meta && jobs[i].patch_mode == 2 && !jobs[i].meta->empty();
+    moff[i + 1] = moff[i] + (m ? jobs[i].meta->size() : 0);
+    nmeta += m;
+  }
+  const uint32_t nchunks = c0[n] + nmeta;
+  std::vector<uint8_t> arena(moff[n]);
+  std::vector<am_chunk_desc> cds(nchunks);
+  std::vector<am_known_hash> known(kb[n]);
+  std::vector<uint32_t> mchunk(n, 0);
+  for (uint32_t i = 0, k = c0[n]; i < n; i++)
+    if (moff[i + 1] > moff[i]) mchunk[i] = k++;
+  am_par_for(n, [&](size_t i) {
     const ManyJob& j = jobs[i];
     am_doc_desc dd{};
     dd.base_chunk = -1;
-    c0[i] = (uint32_t)cds.size();
+    uint64_t o = aoff[i];
+    uint32_t c = c0[i];
     if (j.base && !j.base->empty()) {
-      dd.base_chunk = (int64_t)cds.size();
-      cds.push_back({arena.size(), (uint32_t)j.base->size(), j.base_verified ? 1u : 0u});
-      arena.insert(arena.end(), j.base->begin(), j.base->end());
+      dd.base_chunk = (int64_t)c;
+      cds[c++] = {o, (uint32_t)j.base->size(), j.base_verified ? 1u : 0u};
+      std::memcpy(arena.data() + o, j.base->data(), j.base->size());
+      o += j.base->size();
     }
-    dd.chg_begin = (uint32_t)cds.size();
+    dd.chg_begin = c;
     dd.chg_count = j.chg ? (uint32_t)j.chg->size() : 0u;
     if (j.chg)
-      for (auto& c : *j.chg) {
-        cds.push_back({arena.size(), (uint32_t)c.size(), 0});
-        arena.insert(arena.end(), c.begin(), c.end());
+      for (auto& ch : *j.chg) {
+        cds[c++] = {o, (uint32_t)ch.size(), 0};
+        if (!ch.empty()) std::memcpy(arena.data() + o, ch.data(), ch.size());
+        o += ch.size();
       }
-    cn[i] = (uint32_t)cds.size() - c0[i];
-    dd.known_begin = (uint32_t)known.size();
-    dd.known_count = j.known ? (uint32_t)j.known->size() : 0u;
-    if (j.known) known.insert(known.end(), j.known->begin(), j.known->end());
+    dd.known_begin = kb[i];
+    dd.known_count = kb[i + 1] - kb[i];
+    if (dd.known_count) std::memcpy(known.data() + kb[i], j.known->data(), sizeof(am_known_hash) * dd.known_count);
     dd.flags = (j.have_graph ? 1u : 0u) | (j.patch_mode == 1 ? AM_DOC_WANT_PATCH : 0u) | (j.patch_mode == 2 ? AM_DOC_WANT_DIFF : 0u);
     dd.meta_chunk = 0;
-    dds[i] = dd;
-  }
-  for (size_t i = 0; i < n; i++)  // objectMeta blobs after every document's chunks
-    if (jobs[i].meta && jobs[i].patch_mode == 2) {
-      dds[i].flags |= AM_DOC_META;
-      if (!jobs[i].meta->empty()) {
-        dds[i].meta_chunk = (uint32_t)cds.size() + 1;
-        cds.push_back({arena.size(), (uint32_t)jobs[i].meta->size(), AM_CHUNK_RAW});
-        arena.insert(arena.end(), jobs[i].meta->begin(), jobs[i].meta->end());
+    if (j.meta && j.patch_mode == 2) {  // objectMeta blobs after every document's chunks
+      dd.flags |= AM_DOC_META;
+      if (moff[i + 1] > moff[i]) {
+        dd.meta_chunk = mchunk[i] + 1;
+        cds[mchunk[i]] = {moff[i], (uint32_t)j.meta->size(), AM_CHUNK_RAW};
+        std::memcpy(arena.data() + moff[i], j.meta->data(), j.meta->size());
       }
     }
+    dds[i] = dd;
+  });
+  clk.mark("pack");
   am_batch* b = scratch_batch(e);
   am_error ce;
-  if (am_batch_stage(b, arena.data(), arena.size(), cds.data(), (uint32_t)cds.size(), dds.data(), (uint32_t)n, known.data(),
+  if (am_batch_stage(b, arena.data(), arena.size(), cds.data(), nchunks, dds.data(), (uint32_t)n, known.data(),
                      (uint32_t)known.size(), &ce) ||
       am_batch_run(b) || am_batch_sync(b, &ce)) {
     err = {AM_U_CAPACITY, false, std::string("automerge_amd: GPU pipeline failed: ") + ce.message};
     return false;
   }
+  clk.mark("gpu");
   std::vector<am_doc_result> rr(n);
-  std::vector<uint8_t> hs(32 * cds.size());
-  std::vector<int32_t> cst(cds.size());
-  std::vector<uint32_t> st(cds.size());
+  std::vector<uint8_t> hs(32ull * nchunks);
+  std::vector<int32_t> cst(nchunks);
   std::vector<am_doc_summary> summ;
   std::vector<uint8_t> out, pat;
-  if (am_batch_results(b, rr.data()) || (!cds.empty() && am_batch_chunk_results(b, hs.data(), cst.data(), st.data())) ||
-      !batch_collect(b, summ, out, pat)) {
+  if (!e->coll) e->coll = new CollectBufs();
+  bool ok = am_batch_results(b, rr.data()) == 0 && e->coll->hashes.ensure(32ull * nchunks + 16);
+  if (ok && nchunks) {
+    am_launch_chunk_hashes(b->info.p, nchunks, e->coll->hashes.p, e->stream);
+    ok = hipMemcpyAsync(hs.data(), e->coll->hashes.p, hs.size(), hipMemcpyDeviceToHost, e->stream) == hipSuccess &&
+         hipMemcpyAsync(cst.data(), b->chg_state.p, 4ull * nchunks, hipMemcpyDeviceToHost, e->stream) == hipSuccess &&
+         hipStreamSynchronize(e->stream) == hipSuccess;
+  }
+  if (!ok || !batch_collect(b, summ, out, pat)) {
     err = {AM_U_CAPACITY, false, "automerge_amd: result copy failed"};
     return false;
   }
-  for (size_t i = 0; i < n; i++) {
+  clk.mark("home");
+  am_par_for(n, [&](size_t i) {
     ManyOut& o = outs[i];
     OneResult& res = o.res;
     res.r = rr[i];
-    res.chg_state.assign(cst.begin() + c0[i], cst.begin() + c0[i] + cn[i]);
-    res.hashes.resize(cn[i]);
-    for (uint32_t k = 0; k < cn[i]; k++) std::memcpy(res.hashes[k].data(), hs.data() + 32ull * (c0[i] + k), 32);
+    const uint32_t cb = c0[i], cn = c0[i + 1] - c0[i];
+    res.chg_state.assign(cst.begin() + cb, cst.begin() + cb + cn);
+    res.hashes.resize(cn);
+    for (uint32_t k = 0; k < cn; k++) std::memcpy(res.hashes[k].data(), hs.data() + 32ull * (cb + k), 32);
     if (rr[i].status) {
       std::string actor;
       if (rr[i].arg_actor_len && rr[i].arg_actor_off + rr[i].arg_actor_len <= arena.size())
         actor = hexs(arena.data() + rr[i].arg_actor_off, rr[i].arg_actor_len);
       o.err = {rr[i].status, false, message_for(rr[i].status, rr[i].arg0, rr[i].arg1, actor)};
-      continue;
+      return;
     }
     const am_doc_summary& sm = summ[i];
     if (sm.status || sm.out_len != rr[i].out_len) {
       o.err = {AM_U_CAPACITY, false, "automerge_amd: output compaction failed"};
-      continue;
+      return;
     }
     res.out.assign(out.begin() + sm.out_off, out.begin() + sm.out_off + sm.out_len);
     if (!chunk_heads(res.out, res.heads)) {
       o.err = {AM_U_VALUE, false, "automerge_amd: corrupt merged document"};
-      continue;
+      return;
     }
     if (jobs[i].patch_mode) {
       res.patch.assign(pat.begin() + sm.patch_off, pat.begin() + sm.patch_off + sm.patch_len);
       split_meta(res);
     }
     o.ok = true;
-  }
+  });
+  clk.mark("unpack");
+  clk.print("run_many", n);
   return true;
 }
 
@@ -1612,7 +1677,7 @@ static int apply_finish(am_doc* d, std::vector<std::vector<uint8_t>>& orig, bool
     else if (st == CHG_QUEUED) { newq.push_back(orig[i]); newqh.push_back(res.hashes[base + i]); }
   }
   for (size_t k = 0; k < applied.size(); k++) {
-    d->changes.push_back(orig[applied[k]]);
+    d->changes.push_back(std::move(orig[applied[k]]));
     d->hashes.push_back(res.hashes[base + applied[k]]);
   }
   d->queue = std::move(newq);
@@ -1849,7 +1914,7 @@ static int publish(const std::vector<Err>& E, uint32_t* codes, char** msgs) {
 // computeHashGraph (new.js:1879-1904) of the given loaded handles, k_history batches of 4096
 static void hash_graphs(const std::vector<am_doc*>& ds, std::vector<Err>& E) {
   E.assign(ds.size(), Err{});
-  const size_t G = 4096;  // am_history carries an am_error per document: bounded host memory
+  const size_t G = 16384;  // am_history carries an am_error per document: bounded host memory (128 MiB)
   for (size_t g0 = 0; g0 < ds.size(); g0 += G) {
     const size_t g1 = std::min(ds.size(), g0 + G);
     std::vector<const uint8_t*> ptr;
@@ -1881,7 +1946,11 @@ static void hash_graphs(const std::vector<am_doc*>& ds, std::vector<Err>& E) {
   }
 }
 
-// computeHashGraph of n handles (all of one engine): one k_history batch per 4096
+static bool ensure_graph(am_doc* d, am_error* err);
+
+// computeHashGraph of n handles (all of one engine): one k_history batch per 4096; then every
+// handle's graph index is brought up to date on the host worker threads, so that the graph queries
+// that follow (getChanges, getMissingDeps, getChangeByHash) only read it.
 extern "C" int am_doc_compute_hash_graph_batch(size_t n, am_doc* const* docs, uint32_t* codes, char** msgs) {
   std::vector<Err> E(n);
   std::vector<am_doc*> need;
@@ -1900,6 +1969,11 @@ extern "C" int am_doc_compute_hash_graph_batch(size_t n, am_doc* const* docs, ui
   std::vector<Err> ge;
   hash_graphs(need, ge);
   for (size_t k = 0; k < at.size(); k++) E[at[k]] = ge[k];
+  std::vector<am_doc*> idx;  // distinct handles whose graph exists
+  std::unordered_set<am_doc*> seen2;
+  for (size_t i = 0; i < n; i++)
+    if (docs[i]->have_hash_graph && seen2.insert(docs[i]).second) idx.push_back(docs[i]);
+  am_par_for(idx.size(), [&](size_t k) { (void)ensure_graph(idx[k], nullptr); });
   return publish(E, codes, msgs);
 }
 
@@ -1984,20 +2058,26 @@ extern "C" int am_doc_apply_changes_batch(size_t n, am_doc* const* docs, const s
       known[k].index = (int64_t)k;
     }
   };
+  HostClock clk;
   for (size_t i = 0; i < n; i++) {
     if (patches) { patches[i] = nullptr; patch_lens[i] = 0; }
     if (info) info[i] = am_call_info{0, 0, 0, nullptr};
     am_doc* d = docs[i];
     const bool first = seen.insert(d).second;
     if (d->eng != eng || !first || (patches && d->meta_lost)) { single.push_back(i); continue; }
-    Call c;
-    c.i = i;
-    for (size_t k = off[i]; k < off[i + 1]; k++) c.orig.emplace_back(bufs[k], bufs[k] + lens[k]);
+    calls.emplace_back();
+    calls.back().i = i;
+  }
+  am_par_for(calls.size(), [&](size_t k) {  // the calls' inputs, on the host workers (distinct handles)
+    Call& c = calls[k];
+    am_doc* d = docs[c.i];
+    c.orig.reserve(off[c.i + 1] - off[c.i] + d->queue.size());
+    for (size_t q = off[c.i]; q < off[c.i + 1]; q++) c.orig.emplace_back(bufs[q], bufs[q] + lens[q]);
     for (auto& q : d->queue) c.orig.push_back(q);
     c.track = !d->meta_lost;
     known_of(d, c.known);
-    calls.push_back(std::move(c));
-  }
+  });
+  clk.mark("inputs");
   for (int round = 0; round < 2 && !calls.empty(); round++) {
     std::vector<ManyJob> jobs(calls.size());
     for (size_t k = 0; k < calls.size(); k++) {
@@ -2017,7 +2097,9 @@ extern "C" int am_doc_apply_changes_batch(size_t n, am_doc* const* docs, const s
       calls.clear();
       break;
     }
+    clk.mark("run");
     std::vector<Call> graph;
+    std::vector<uint8_t> commit(calls.size(), 0);
     for (size_t k = 0; k < calls.size(); k++) {
       Call& c = calls[k];
       am_doc* d = docs[c.i];
@@ -2033,18 +2115,28 @@ extern "C" int am_doc_apply_changes_batch(size_t n, am_doc* const* docs, const s
         std::memcpy(&ph, o.res.patch.data(), sizeof ph);
         if (ph.status == AM_U_CAPACITY) { single.push_back(c.i); continue; }  // 8x pools: the single path
       }
+      commit[k] = 1;
+    }
+    // the commits (new.js:1838-1860), each touching only its own handle, on the host workers
+    am_par_for(calls.size(), [&](size_t k) {
+      if (!commit[k]) return;
+      Call& c = calls[k];
+      am_doc* d = docs[c.i];
       std::vector<uint8_t> log;
       am_error tmp;
-      if (apply_finish(d, c.orig, c.track, o.res, patches ? &log : nullptr, &tmp)) {
+      if (apply_finish(d, c.orig, c.track, outs[k].res, patches ? &log : nullptr, &tmp)) {
         E[c.i] = from_c(tmp);
-        continue;
+        return;
       }
       if (patches) {
         patches[c.i] = dup_bytes(log);
         patch_lens[c.i] = log.size();
       }
       call_info(d, info ? info + c.i : nullptr);
-    }
+    });
+    clk.mark("commit");
+    am_par_for(outs.size(), [&](size_t k) { outs[k] = ManyOut(); });
+    if (graph.empty()) am_par_for(calls.size(), [&](size_t k) { calls[k] = Call(); });
     calls.clear();
     if (!graph.empty()) {
       std::vector<am_doc*> gd;
@@ -2075,6 +2167,8 @@ extern "C" int am_doc_apply_changes_batch(size_t n, am_doc* const* docs, const s
     }
     call_info(docs[i], info ? info + i : nullptr);
   }
+  clk.mark("single");
+  clk.print("apply_changes_batch", n);
   return publish(E, codes, msgs);
 }
 
@@ -2244,6 +2338,8 @@ extern "C" int am_doc_get_changes_added(am_doc* d1, am_doc* d2, uint64_t** idx, 
   d2->graph.added_since(known, heads_of(d2), out);
   return out_indexes(out, idx, n, err);
 }
+
+extern "C" int am_doc_graph_ready(const am_doc* d) { return d->have_hash_graph && d->graph.size() == d->changes.size(); }
 
 extern "C" int64_t am_doc_change_index(am_doc* d, const uint8_t* hash32) {
   if (!ensure_graph(d, nullptr)) return -2;

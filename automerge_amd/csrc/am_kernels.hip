@@ -1046,6 +1046,17 @@ void am_launch_out_hash(const BatchDev& b, hipStream_t s) {
   if (!b.ndocs) return;
   hipLaunchKernelGGL(k_out_hash_ws, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, b.results, b.ndocs, b.ws, b.bounds);
 }
+// the 32-byte hashes of every chunk of a batch, densely (the batched per-handle calls copy home
+// these instead of the whole ChunkInfo table)
+__global__ void __launch_bounds__(256) k_chunk_hashes(const ChunkInfo* __restrict__ info, uint32_t n, uint32_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 8ull * n) return;
+  out[i] = reinterpret_cast<const uint32_t*>(info[i >> 3].hash)[i & 7];
+}
+void am_launch_chunk_hashes(const ChunkInfo* info, uint32_t n, uint8_t* out32, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_chunk_hashes, dim3((unsigned)((8ull * n + 255) / 256)), dim3(256), 0, s, info, n,
+                            reinterpret_cast<uint32_t*>(out32));
+}
 void am_launch_sha256(const uint8_t* arena, const am_chunk_desc* msgs, uint32_t n, uint8_t* out, hipStream_t s) {
   if (!n) return;
   hipLaunchKernelGGL(k_sha256, dim3((n + 255) / 256), dim3(256), 0, s, arena, msgs, n, out);

@@ -36,6 +36,7 @@ struct BatchDev {
 };
 
 void am_launch_chunks(const BatchDev& b, hipStream_t s);
+void am_launch_chunk_hashes(const ChunkInfo* info, uint32_t n, uint8_t* out32, hipStream_t s);
 void am_launch_bounds(const BatchDev& b, hipStream_t s);   // k_bounds + scan of ws bytes
 void am_launch_doc(const BatchDev& b, hipStream_t s);
 void am_launch_out_hash(const BatchDev& b, hipStream_t s);
@@ -84,6 +85,8 @@ void am_launch_history_compact(const HistResult* res, const HistDesc* hd, uint32
 // the engine's history buffers (am_hist.hip), freed with the engine
 void*& am_engine_hist(am_engine* e);
 void am_hist_cache_free(void* cache);
+void*& am_engine_sync(am_engine* e);
+void am_sync_cache_free(void* cache);
 // host stages of am_capi.hip shared with am_hist.hip: Backend.load's staging of a document chunk
 // (DEFLATEd columns inflated, checksum verified), the reference error text of an AM_* code
 bool am_stage_doc_chunk(am_engine* e, const std::vector<uint8_t>& in, std::vector<uint8_t>& out, bool& verified, am_error* err);

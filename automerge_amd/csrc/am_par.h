@@ -1,0 +1,37 @@
+// am_par.h -- host worker threads for the per-document host stages of the batched calls (the sync
+// protocol's graph queries and message building, the graph indexing): f(i) for i in [0, n) on
+// AM_HOST_THREADS threads (default: the machine's, at most 16), in chunks of 64 items.
+#pragma once
+#include <stdlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <thread>
+#include <vector>
+
+inline unsigned am_host_threads() {
+  const char* e = getenv("AM_HOST_THREADS");
+  unsigned n = e ? (unsigned)atoi(e) : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  return n ? n : 1;
+}
+
+template <class F>
+void am_par_for(size_t n, F f) {
+  const unsigned nt = am_host_threads();
+  if (nt <= 1 || n < 128) {
+    for (size_t i = 0; i < n; i++) f(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (;;) {
+      const size_t i0 = next.fetch_add(64);
+      if (i0 >= n) return;
+      for (size_t i = i0; i < std::min(n, i0 + 64); i++) f(i);
+    }
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
+  work();
+  for (auto& x : th) x.join();
+}

@@ -239,12 +239,41 @@ extern "C" uint8_t amx_sync_select_one(const uint64_t* coff, const uint8_t* hash
 // ------------------------------------------------------------------------------------------
 namespace {
 
-template <typename T>
-struct DBuf {
-  T* p = nullptr;
-  bool alloc(size_t n) { return hipMalloc(&p, (n ? n : 1) * sizeof(T)) == hipSuccess; }
-  ~DBuf() { if (p) (void)hipFree(p); }
+// Device buffers of the engine's sync calls, kept between calls and grown on demand (a sync round
+// calls these once per batch; a hipMalloc/hipFree pair per call would dominate small batches).
+struct GBuf {
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t bytes) {
+    if (bytes <= cap && p) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = bytes + bytes / 4 + 256;
+    if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return false; }
+    cap = want;
+    return true;
+  }
+  ~GBuf() { if (p) (void)hipFree(p); }
 };
+struct SyncCache {
+  GBuf b[9];
+};
+template <typename T>
+struct DBuf {  // view of one cached buffer of the engine
+  T* p = nullptr;
+  GBuf* g = nullptr;
+  bool alloc(size_t n) {
+    if (!g->ensure((n ? n : 1) * sizeof(T))) return false;
+    p = reinterpret_cast<T*>(g->p);
+    return true;
+  }
+};
+SyncCache& sync_cache(am_engine* e) {
+  void*& slot = am_engine_sync(e);
+  if (!slot) slot = new SyncCache();
+  return *static_cast<SyncCache*>(slot);
+}
 
 void fail(am_error* err, uint32_t code, const char* msg) {
   if (!err) return;
@@ -275,6 +304,8 @@ bool gpu_ok(am_error* err, hipError_t e, const char* what) {
 #define GPU(expr) do { if (!gpu_ok(err, (expr), #expr)) return 1; } while (0)
 
 }  // namespace
+
+void am_sync_cache_free(void* cache) { delete static_cast<SyncCache*>(cache); }
 
 extern "C" uint64_t am_bloom_encoded_size(uint64_t nhashes) { return bloom_size(nhashes); }
 // new BloomFilter(bytes) header check on the host (sync.js:47-58): 0 when well formed, else the
@@ -321,8 +352,9 @@ extern "C" int am_bloom_build(am_engine* eng, const uint8_t* hashes32, const uin
   if (!nfilt || !total) return 0;
   GPU(hipSetDevice(am_engine_device(eng)));
   hipStream_t s = am_engine_stream(eng);
-  DBuf<uint8_t> dh, dout;
-  DBuf<uint64_t> dhoff, dfoff;
+  SyncCache& K = sync_cache(eng);
+  DBuf<uint8_t> dh{nullptr, &K.b[0]}, dout{nullptr, &K.b[1]};
+  DBuf<uint64_t> dhoff{nullptr, &K.b[2]}, dfoff{nullptr, &K.b[3]};
   if (!dh.alloc(32 * nh) || !dout.alloc(total) || !dhoff.alloc(nfilt + 1) || !dfoff.alloc(nfilt + 1)) {
     fail(err, AM_U_CAPACITY, "automerge_amd: device allocation failed");
     return 1;
@@ -345,9 +377,10 @@ extern "C" int am_bloom_probe(am_engine* eng, const uint8_t* filters, const uint
   GPU(hipSetDevice(am_engine_device(eng)));
   hipStream_t s = am_engine_stream(eng);
   const uint64_t fbytes = foff[nfilt];
-  DBuf<uint8_t> df, dp, dc;
-  DBuf<uint64_t> dfo;
-  DBuf<uint32_t> dpf;
+  SyncCache& K = sync_cache(eng);
+  DBuf<uint8_t> df{nullptr, &K.b[0]}, dp{nullptr, &K.b[1]}, dc{nullptr, &K.b[2]};
+  DBuf<uint64_t> dfo{nullptr, &K.b[3]};
+  DBuf<uint32_t> dpf{nullptr, &K.b[4]};
   if (!df.alloc(fbytes) || !dp.alloc(32 * nprobe) || !dc.alloc(nprobe) || !dfo.alloc(nfilt + 1) || !dpf.alloc(nprobe)) {
     fail(err, AM_U_CAPACITY, "automerge_amd: device allocation failed");
     return 1;
@@ -373,9 +406,10 @@ extern "C" int am_sync_select(am_engine* eng, uint32_t npairs, const uint64_t* c
   GPU(hipSetDevice(am_engine_device(eng)));
   hipStream_t s = am_engine_stream(eng);
   const uint64_t nc = coff[npairs], nd = doff[nc], nf = pfoff[npairs], fbytes = foff[nf];
-  DBuf<uint8_t> dh, dflt, dsend, dst;
-  DBuf<uint64_t> dcoff, ddoff, dpfoff, dfoff;
-  DBuf<int32_t> ddidx;
+  SyncCache& K = sync_cache(eng);
+  DBuf<uint8_t> dh{nullptr, &K.b[0]}, dflt{nullptr, &K.b[1]}, dsend{nullptr, &K.b[2]}, dst{nullptr, &K.b[3]};
+  DBuf<uint64_t> dcoff{nullptr, &K.b[4]}, ddoff{nullptr, &K.b[5]}, dpfoff{nullptr, &K.b[6]}, dfoff{nullptr, &K.b[7]};
+  DBuf<int32_t> ddidx{nullptr, &K.b[8]};
   if (!dh.alloc(32 * nc) || !dflt.alloc(fbytes) || !dsend.alloc(nc) || !dst.alloc(npairs) || !dcoff.alloc(npairs + 1) ||
       !ddoff.alloc(nc + 1) || !dpfoff.alloc(npairs + 1) || !dfoff.alloc(nf + 1) || !ddidx.alloc(nd)) {
     fail(err, AM_U_CAPACITY, "automerge_amd: device allocation failed");

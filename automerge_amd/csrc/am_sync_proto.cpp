@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <map>
 #include <string>
 #include <unordered_map>
@@ -27,6 +28,7 @@
 #include "../../include/automerge_amd.h"
 #include "am_graph.h"
 #include "am_json.h"
+#include "am_par.h"
 
 namespace {
 
@@ -431,6 +433,24 @@ void gen_finish(Gen& g) {
   s.last_sent_heads = g.our_heads;
 }
 
+// AM_SYNC_PROFILE=1: per-stage wall times of the batched sync calls on stderr
+struct StageClock {
+  bool on = getenv("AM_SYNC_PROFILE") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  std::string line;
+  void mark(const char* what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    char b[64];
+    snprintf(b, sizeof b, " %s=%.1fms", what, std::chrono::duration<double, std::milli>(now - t).count());
+    line += b;
+    t = now;
+  }
+  void print(const char* call, size_t n) {
+    if (on) fprintf(stderr, "[am_sync] %s n=%zu%s\n", call, n, line.c_str());
+  }
+};
+
 uint8_t* dup(const std::vector<uint8_t>& v) {
   uint8_t* p = (uint8_t*)malloc(v.size() ? v.size() : 1);
   if (p && !v.empty()) memcpy(p, v.data(), v.size());
@@ -448,17 +468,21 @@ Hashes sorted_unique(Hashes v) {
 extern "C" int am_sync_generate(size_t n, am_doc* const* docs, const uint8_t* const* states, const size_t* state_lens,
                                 uint8_t** out_states, size_t* out_state_lens, uint8_t** msgs, size_t* msg_lens,
                                 uint32_t* codes, char** errmsgs) {
+  StageClock clk;
   std::vector<Gen> gs(n);
   {  // the hash graphs of loaded documents (computeHashGraph, new.js:1879-1904) in one batch
     std::vector<am_doc*> gd(docs, docs + n);
     std::vector<uint32_t> gc(n);
     if (n) am_doc_compute_hash_graph_batch(n, gd.data(), gc.data(), nullptr);  // errors resurface below
   }
+  clk.mark("graphs");
   auto fail = [&](Gen& g, const SErr& e) {
     g.failed = true;
     g.err = e;
   };
-  for (size_t i = 0; i < n; i++) {
+  // the graph queries only read the (indexed) graphs: host workers over the documents; a document
+  // whose graph is not ready (its history failed to decode) raises that error on this thread
+  auto prepare = [&](size_t i) {
     gs[i].doc = docs[i];
     try {
       gs[i].st = read_state(states[i], state_lens[i]);
@@ -468,7 +492,13 @@ extern "C" int am_sync_generate(size_t n, am_doc* const* docs, const uint8_t* co
     } catch (const std::bad_alloc&) {
       fail(gs[i], SErr{false, "automerge_amd: out of host memory", AM_U_CAPACITY});
     }
-  }
+  };
+  std::vector<uint8_t> ready(n);
+  for (size_t i = 0; i < n; i++) ready[i] = am_doc_graph_ready(docs[i]) != 0;
+  am_par_for(n, [&](size_t i) { if (ready[i]) prepare(i); });
+  for (size_t i = 0; i < n; i++)
+    if (!ready[i]) prepare(i);
+  clk.mark("prepare");
   // the GPU stages, one launch per engine for all its documents
   std::vector<am_engine*> engines;
   for (auto& g : gs)
@@ -533,8 +563,8 @@ extern "C" int am_sync_generate(size_t n, am_doc* const* docs, const uint8_t* co
       for (size_t k = 0; k < sel.size(); k++) sel[k]->send.assign(send.begin() + coff[k], send.begin() + coff[k + 1]);
     }
   }
-  int nfail = 0;
-  for (size_t i = 0; i < n; i++) {
+  clk.mark("gpu");
+  auto finish = [&](size_t i) {
     Gen& g = gs[i];
     out_states[i] = nullptr;
     out_state_lens[i] = 0;
@@ -552,8 +582,18 @@ extern "C" int am_sync_generate(size_t n, am_doc* const* docs, const uint8_t* co
         }
       } catch (const SErr& e) {
         fail(g, e);
+      } catch (const std::bad_alloc&) {
+        fail(g, SErr{false, "automerge_amd: out of host memory", AM_U_CAPACITY});
       }
     }
+  };
+  am_par_for(n, [&](size_t i) { if (ready[i]) finish(i); });
+  for (size_t i = 0; i < n; i++)
+    if (!ready[i]) finish(i);
+  clk.mark("finish");
+  int nfail = 0;
+  for (size_t i = 0; i < n; i++) {
+    Gen& g = gs[i];
     codes[i] = 0;
     if (errmsgs) errmsgs[i] = nullptr;
     if (g.failed) {
@@ -565,6 +605,11 @@ extern "C" int am_sync_generate(size_t n, am_doc* const* docs, const uint8_t* co
       nfail++;
     }
   }
+  clk.mark("out");
+  am_par_for(n, [&](size_t i) { gs[i] = Gen(); });  // the per-document buffers, freed on the workers
+  std::vector<Gen>().swap(gs);
+  clk.mark("free");
+  clk.print("generate", n);
   return nfail;
 }
 
@@ -651,6 +696,7 @@ extern "C" int am_sync_receive_batch(size_t n, am_doc* const* docs, const uint8_
     bool failed = false, applied = false, single = false;
     SErr err;
   };
+  StageClock clk;
   std::vector<R> rs(n);
   std::unordered_set<am_doc*> seen;
   for (size_t i = 0; i < n; i++) {
@@ -659,8 +705,11 @@ extern "C" int am_sync_receive_batch(size_t n, am_doc* const* docs, const uint8_
     patches[i] = nullptr;
     patch_lens[i] = 0;
     if (info) info[i] = am_call_info{0, 0, 0, nullptr};
+    if (!seen.insert(docs[i]).second) rs[i].single = true;  // after the batch, in order
+  }
+  am_par_for(n, [&](size_t i) {
     R& r = rs[i];
-    if (!seen.insert(docs[i]).second) { r.single = true; continue; }  // after the batch, in order
+    if (r.single) return;
     try {
       r.s = read_state(states[i], state_lens[i]);
       r.m = decode_msg(msgs[i], msg_lens[i]);
@@ -668,8 +717,12 @@ extern "C" int am_sync_receive_batch(size_t n, am_doc* const* docs, const uint8_
     } catch (const SErr& e) {
       r.failed = true;
       r.err = e;
+    } catch (const std::bad_alloc&) {
+      r.failed = true;
+      r.err = SErr{false, "automerge_amd: out of host memory", AM_U_CAPACITY};
     }
-  }
+  });
+  clk.mark("decode");
   // every message's changes: one batched applyChanges
   std::vector<size_t> at, off{0};
   std::vector<am_doc*> ad;
@@ -706,6 +759,7 @@ extern "C" int am_sync_receive_batch(size_t n, am_doc* const* docs, const uint8_
       if (mm[k]) am_free(mm[k]);
     }
   }
+  clk.mark("apply");
   // the hash graphs the heads lookups need (loaded documents), in one batch
   std::vector<am_doc*> gd;
   for (size_t i = 0; i < n; i++)
@@ -714,6 +768,26 @@ extern "C" int am_sync_receive_batch(size_t n, am_doc* const* docs, const uint8_
     std::vector<uint32_t> gc(gd.size());
     am_doc_compute_hash_graph_batch(gd.size(), gd.data(), gc.data(), nullptr);  // errors resurface below
   }
+  clk.mark("graphs");
+  // the state updates (graph reads only) on the host workers, for documents whose graph is ready
+  std::vector<uint8_t> done(n, 0);
+  am_par_for(n, [&](size_t i) {
+    R& r = rs[i];
+    if (r.single || r.failed || (!r.m.heads.empty() && !am_doc_graph_ready(docs[i]))) return;
+    try {
+      const std::vector<uint8_t> o = recv_finish(docs[i], r.s, r.m, r.before);
+      out_states[i] = dup(o);
+      out_state_lens[i] = o.size();
+    } catch (const SErr& e) {
+      r.failed = true;
+      r.err = e;
+    } catch (const std::bad_alloc&) {
+      r.failed = true;
+      r.err = SErr{false, "automerge_amd: out of host memory", AM_U_CAPACITY};
+    }
+    done[i] = 1;
+  });
+  clk.mark("finish");
   int nfail = 0;
   for (size_t i = 0; i < n; i++) {
     R& r = rs[i];
@@ -735,7 +809,7 @@ extern "C" int am_sync_receive_batch(size_t n, am_doc* const* docs, const uint8_
         msg = e.message;
       }
     } else {
-      if (!r.failed) {
+      if (!r.failed && !done[i]) {
         try {
           const std::vector<uint8_t> o = recv_finish(docs[i], r.s, r.m, r.before);
           out_states[i] = dup(o);
@@ -762,6 +836,11 @@ extern "C" int am_sync_receive_batch(size_t n, am_doc* const* docs, const uint8_
     }
     nfail += code != 0;
   }
+  clk.mark("out");
+  am_par_for(n, [&](size_t i) { rs[i] = R(); });
+  std::vector<R>().swap(rs);
+  clk.mark("free");
+  clk.print("receive", n);
   return nfail;
 }
 

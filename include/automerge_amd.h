@@ -335,6 +335,9 @@ int am_doc_get_patch_batch(size_t n, am_doc *const *docs, uint8_t **out, size_t 
                            char **msgs);
 int am_doc_save_batch(size_t n, am_doc *const *docs, uint8_t **out, size_t *lens, uint32_t *codes, char **msgs);
 int am_doc_compute_hash_graph_batch(size_t n, am_doc *const *docs, uint32_t *codes, char **msgs);
+/* 1 when the document's hash graph is computed and indexed: its graph queries then only read it
+ * (safe from several host threads at once). */
+int am_doc_graph_ready(const am_doc *doc);
 /* ---- hash-graph queries (BackendDoc, new.js:1913-2020); the graph of a loaded document is
  * computed on first use (computeHashGraph, new.js:1879-1904). Change indexes refer to
  * am_doc_change; arrays are malloc'd (am_free). ----
