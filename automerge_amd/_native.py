@@ -163,6 +163,9 @@ _sigs = {
                                  C.POINTER(C.c_uint64), C.POINTER(Error)]),
     "am_pipe_drain": (C.c_int, [P, P, C.c_uint32, C.POINTER(Error)]),
     "am_pipe_times": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_uint32)]),
+    "am_pipe_run_resident": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, C.c_uint32, C.c_int, P, P, C.c_uint64, P,
+                                       C.c_uint64, P, C.POINTER(Error)]),
+    "am_pipe_resident_sync": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(Error)]),
 }
 for _name, (_res, _args) in _sigs.items():
     _f = getattr(lib, _name)

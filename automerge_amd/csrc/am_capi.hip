@@ -767,6 +767,8 @@ struct am_pipe {
   std::vector<uint64_t> totals;                // per finalized batch since the last drain: out, patch bytes
   float ms_comp = 0.f, ms_doc = 0.f;           // kernel times of the drained batches
   uint32_t nms = 0;
+  std::vector<hipEvent_t> rev;                 // resident batches: 4 events each (chain start, doc kernels, end)
+  uint32_t nres = 0;                           // resident batches since the last am_pipe_resident_sync
 };
 
 static void pipe_free(am_pipe* p) {
@@ -781,6 +783,7 @@ static void pipe_free(am_pipe* p) {
   }
   for (hipStream_t s : {p->s_in, p->s_c, p->s_out})
     if (s) (void)hipStreamDestroy(s);
+  for (hipEvent_t e : p->rev) (void)hipEventDestroy(e);
   delete p;
 }
 
@@ -995,6 +998,72 @@ extern "C" int am_pipe_submit(am_pipe* p, const uint8_t* arena, uint64_t arena_l
     if (prev->busy && !pipe_finalize(p, prev)) return fail("automerge_amd: HIP error while finishing a batch");
   }
   p->next++;
+  if (err) err->code = 0;
+  return 0;
+}
+
+// One batch whose inputs are already resident in device memory: the whole chain of am_pipe_submit
+// (k_chunks .. k_pipe_compact) on the pipeline's compute stream, with the merged documents, patch
+// logs and summaries compacted into the caller's device buffers and the two arena totals written to
+// d_totals; nothing crosses the host link and the host does not wait (hipStreamSynchronize /
+// am_pipe_drain). Batches run back to back on one stream and share slot 0's workspace.
+extern "C" int am_pipe_run_resident(am_pipe* p, const uint8_t* d_arena, uint64_t arena_len, const am_chunk_desc* d_chunks,
+                                    uint32_t nchunks, const am_doc_desc* d_docs, uint32_t ndocs, int any_diff,
+                                    am_doc_summary* d_summary, uint8_t* d_out, uint64_t out_cap, uint8_t* d_patches,
+                                    uint64_t patch_cap, uint64_t* d_totals, am_error* err) {
+  auto fail = [&](const char* m) { to_c(Err{AM_U_CAPACITY, false, m}, err); return 1; };
+  if (!set_device(p->eng)) return fail("automerge_amd: no device");
+  const am_pipe_caps& c = p->caps;
+  if (arena_len > c.arena_bytes || nchunks > c.chunks || ndocs > c.docs)
+    return fail("automerge_amd: batch exceeds the pipeline capacities");
+  PipeSlot* sl = p->slots[0];
+  if (sl->busy && !pipe_retire(p, sl, true)) return fail("automerge_amd: HIP error while retiring a batch");
+  am_batch& b = sl->b;
+  b.nchunks = nchunks;
+  b.ndocs = ndocs;
+  b.any_diff = any_diff != 0;
+  BatchDev d = b.dev();
+  d.arena = d_arena;
+  d.chunks = d_chunks;
+  d.docs = d_docs;
+  d.ws_cap = c.ws_bytes;
+  while (p->rev.size() < 4ull * (p->nres + 1)) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return fail("automerge_amd: cannot create a HIP event");
+    p->rev.push_back(e);
+  }
+  hipEvent_t* ev = p->rev.data() + 4ull * p->nres++;
+  hipStream_t s = p->s_c;
+  (void)hipEventRecord(ev[0], s);
+  am_launch_chunks(d, s);
+  am_launch_bounds(d, s);
+  (void)hipEventRecord(ev[1], s);
+  am_launch_doc(d, s);
+  (void)hipEventRecord(ev[2], s);
+  am_launch_out_hash(d, s);
+  am_launch_pipe_compact(d, sl->olen.p, sl->ooff.p, sl->plen.p, sl->poff.p, sl->tmp.p, d_totals, d_out, out_cap, d_patches,
+                         patch_cap, d_summary, s);
+  if (hipEventRecord(ev[3], s) != hipSuccess || hipGetLastError() != hipSuccess) return fail("automerge_amd: kernel launch failed");
+  if (err) err->code = 0;
+  return 0;
+}
+
+// Waits for the resident batches run since the last call; ms2 = their whole chains and their
+// document kernels (k_doc_fast + k_doc), summed over the batches (HIP events on the compute stream).
+extern "C" int am_pipe_resident_sync(am_pipe* p, float* ms2, am_error* err) {
+  if (!set_device(p->eng) || hipStreamSynchronize(p->s_c) != hipSuccess) {
+    to_c(Err{AM_U_CAPACITY, false, "automerge_amd: HIP error in a resident batch"}, err);
+    return 1;
+  }
+  ms2[0] = ms2[1] = 0.f;
+  for (uint32_t k = 0; k < p->nres; k++) {
+    float a = 0.f, d = 0.f;
+    (void)hipEventElapsedTime(&a, p->rev[4 * k], p->rev[4 * k + 3]);
+    (void)hipEventElapsedTime(&d, p->rev[4 * k + 1], p->rev[4 * k + 2]);
+    ms2[0] += a;
+    ms2[1] += d;
+  }
+  p->nres = 0;
   if (err) err->code = 0;
   return 0;
 }

@@ -104,3 +104,20 @@ class Pipeline:
         n = C.c_uint32()
         N.lib.am_pipe_times(self._p, ms, C.byref(n))
         return float(ms[0]), float(ms[1]), int(n.value)
+
+    def run_resident(self, d_arena, arena_len, d_chunks, nchunks, d_docs, ndocs, any_diff, d_summary, d_out, out_cap,
+                     d_patches, patch_cap, d_totals):
+        """One batch whose inputs are resident in device memory (device pointers as ints: the arena
+        with 64 readable bytes past arena_len); outputs compacted into device buffers. Async."""
+        err = N.Error()
+        if N.lib.am_pipe_run_resident(self._p, d_arena, arena_len, d_chunks, nchunks, d_docs, ndocs, int(bool(any_diff)),
+                                      d_summary, d_out, out_cap, d_patches, patch_cap, d_totals, C.byref(err)):
+            N.raise_for(err)
+
+    def resident_sync(self):
+        """Waits for the resident batches; (ms of their chains, ms of their document kernels), summed."""
+        ms = (C.c_float * 2)()
+        err = N.Error()
+        if N.lib.am_pipe_resident_sync(self._p, ms, C.byref(err)):
+            N.raise_for(err)
+        return float(ms[0]), float(ms[1])

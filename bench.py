@@ -158,7 +158,9 @@ def main():
     ap.add_argument("--docs", type=int, default=1 << 20, help="documents of the whole job (sharded over the ranks)")
     ap.add_argument("--batch", type=int, default=0, help="documents per pipeline batch (0: auto)")
     ap.add_argument("--slots", type=int, default=3, help="batches in flight")
-    ap.add_argument("--mode", choices=["pipe", "resident"], default="pipe")
+    ap.add_argument("--mode", choices=["resident", "pipe"], default="resident",
+                    help="resident: inputs in HBM when the timed region starts (the `value`); pipe: from host memory")
+    ap.add_argument("--no-pcie", action="store_true", help="resident mode: skip the PCIe-inclusive pipe run")
     ap.add_argument("--workload", choices=["c4", "c2"], default="c4")
     ap.add_argument("--no-patch", action="store_true", help="merge without the applyChanges patch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -207,126 +209,157 @@ def main():
             dist.barrier()
 
     extra = {}
-    if args.mode == "resident":
-        # inputs resident in HBM: the kernel-only rate (no H2D / D2H in the timed region)
-        b = Batch(device=local)
-        b.stage(arena, chunks, docs)
-        for _ in range(args.warmup):
-            b.run()
-        b.sync()
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            b.run()
-            b.sync()
-        torch.cuda.synchronize()
-        barrier()
-        elapsed = time.perf_counter() - t0
-        st = b.stage_times()
-        res = b.results()
-        statuses = res["status"]
-        out_bytes = int(res["out_len"].sum())
-        patch_bytes = 0
-        t_doc = st[2]
-        in_b = int(arena.nbytes)
-        alg_launch = in_b + out_bytes
-        extra["stage_ms"] = dict(zip(["k_chunks", "k_bounds+scan", "k_doc", "k_out_hash"], st))
-        extra["fast_docs"] = int(b.fast_flags().sum())
-        digest = b.digest(0) if args.workload == "c2" else None
-        workspace = int(b.workspace_bytes())
+    from automerge_amd import pipe
+    # 65536 documents per batch: big enough to fill the 256 CUs many times over (k_doc_fast: one
+    # wave per document), small enough that one workspace serves every batch in turn
+    batch = args.batch or max(16384, min(65536, -(-D // 4)))
+    parts = split_batches(arena, chunks, docs, batch)
+    # capacities from a representative batch (the largest one), staged the ordinary way
+    probe = Batch(device=local)
+    probe.stage(*max(parts, key=lambda p: len(p[0])))
+    ws_need = int(probe.workspace_bytes())
+    kinfo = probe.kernel_info()
+    del probe
+    arena_cap = max(len(p[0]) for p in parts)
+    ncap = max(len(p[2]) for p in parts)
+    ccap = max(len(p[1]) for p in parts)
+    out_cap = ncap * 1024 + (1 << 20)
+    patch_cap = ncap * 1024 + (1 << 20) if not args.no_patch else (1 << 20)
+    pl = pipe.Pipeline(arena_cap, ccap, ncap, ws_need + ws_need // 8 + (1 << 20), out_cap, patch_cap,
+                       kinfo["k_doc_fast_lds_per_doc"], slots=args.slots, device=local)
+    nb = len(parts)
+    in_b = int(arena.nbytes)
+    starts = np.cumsum([0] + [len(p[2]) for p in parts])
 
-        def check(i):
-            return b.doc_output(i, res[i]), (b.doc_patch(i) if not args.no_patch else None)
-    else:
-        from automerge_amd import pipe
-        # 65536 documents per batch: the pipeline is bound by H2D and by the kernel chain alike, and
-        # smaller batches shorten its fill and drain (131072: 52-57 ms per step, 65536: 48 ms, 32768:
-        # 49 ms, 16384: 57 ms; tools/gpu_batch_ab.sh)
-        batch = args.batch or max(16384, min(65536, -(-D // 4)))
-        parts = split_batches(arena, chunks, docs, batch)
-        # capacities from a representative batch (the largest one), staged the ordinary way
-        probe = Batch(device=local)
-        probe.stage(*max(parts, key=lambda p: len(p[0])))
-        ws_need = int(probe.workspace_bytes())
-        kinfo = probe.kernel_info()
-        del probe
-        arena_cap = max(len(p[0]) for p in parts)
-        ncap = max(len(p[2]) for p in parts)
-        ccap = max(len(p[1]) for p in parts)
-        out_cap = ncap * 1024 + (1 << 20)
-        patch_cap = ncap * 1024 + (1 << 20) if not args.no_patch else (1 << 20)
-        pl = pipe.Pipeline(arena_cap, ccap, ncap, ws_need + ws_need // 8 + (1 << 20), out_cap, patch_cap,
-                           kinfo["k_doc_fast_lds_per_doc"], slots=args.slots, device=local)
-        # pinned host memory: inputs, and one set of outputs per batch
+    def run_pipe(steps, warmup):
+        """The job from host memory back to host memory (am_pipe_submit / drain): PCIe-inclusive."""
         pin_in = [(pipe.pinned_copy(a), pipe.pinned_copy(c), pipe.pinned_copy(d)) for a, c, d in parts]
         pin_out = []
         for a, c, d in parts:
-            s = pipe.Pinned(len(d) * pipe.SUMMARY_DT.itemsize)
-            pin_out.append((s, s.view(pipe.SUMMARY_DT, len(d)), pipe.Pinned(out_cap), pipe.Pinned(patch_cap)))
+            sb = pipe.Pinned(len(d) * pipe.SUMMARY_DT.itemsize)
+            pin_out.append((sb, sb.view(pipe.SUMMARY_DT, len(d)), pipe.Pinned(out_cap), pipe.Pinned(patch_cap)))
 
         def step():
             for (pa, pc, pd), (_, summ, po, pp) in zip(pin_in, pin_out):
                 pl.submit(pa.arr, pc.arr, pd.arr, summ, po.u8, pp.u8)
-            return pl.drain(len(parts))
+            return pl.drain(nb)
 
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             step()
         pl.times()
-        # the host link on its own (pinned copies of the rank's input bytes, each way)
-        hb = torch.empty(min(int(arena.nbytes), 1 << 30), dtype=torch.uint8).pin_memory()
-        db = torch.empty_like(hb, device="cuda")
-        db.copy_(hb, non_blocking=True)
-        torch.cuda.synchronize()
-        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-        e0.record()
-        db.copy_(hb, non_blocking=True)
-        e1.record()
-        hb.copy_(db, non_blocking=True)
-        e2.record()
-        torch.cuda.synchronize()
-        extra["pcie_GBps"] = {"h2d": hb.numel() / (e0.elapsed_time(e1) * 1e-3) / 1e9,
-                              "d2h": hb.numel() / (e1.elapsed_time(e2) * 1e-3) / 1e9}
-        del hb, db
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(steps):
             totals = step()
         torch.cuda.synchronize()
         barrier()
+        el = time.perf_counter() - t0
+        ms_c, ms_d, nt = pl.times()
+        return el, totals, pin_out, ms_c, ms_d / max(nt, 1)
+
+    if args.mode == "resident":
+        # inputs resident in HBM (copied before the timed region); each step runs every batch of the
+        # shard through the whole chain (am_pipe_run_resident), outputs compacted in HBM
+        dev = []
+        for a, c, d in parts:
+            ta = torch.zeros(len(a) + 64, dtype=torch.uint8, device="cuda")
+            ta[:len(a)].copy_(torch.from_numpy(np.ascontiguousarray(a)))
+            tc = torch.from_numpy(np.ascontiguousarray(c).view(np.uint8)).cuda()
+            td = torch.from_numpy(np.ascontiguousarray(d).view(np.uint8)).cuda()
+            ts = torch.zeros(len(d) * pipe.SUMMARY_DT.itemsize, dtype=torch.uint8, device="cuda")
+            to = torch.empty(out_cap, dtype=torch.uint8, device="cuda")
+            tp = torch.empty(patch_cap, dtype=torch.uint8, device="cuda")
+            tt = torch.zeros(2, dtype=torch.int64, device="cuda")
+            dev.append((len(a), len(c), len(d), ta, tc, td, ts, to, tp, tt))
+        torch.cuda.synchronize()
+
+        def step():
+            for na, nc, nd, ta, tc, td, ts, to, tp, tt in dev:
+                pl.run_resident(ta.data_ptr(), na, tc.data_ptr(), nc, td.data_ptr(), nd, not args.no_patch,
+                                ts.data_ptr(), to.data_ptr(), out_cap, tp.data_ptr(), patch_cap, tt.data_ptr())
+            return pl.resident_sync()
+
+        for _ in range(args.warmup):
+            step()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ms_comp = ms_doc = 0.0
+        for _ in range(args.steps):
+            a_, d_ = step()
+            ms_comp += a_
+            ms_doc += d_
+        torch.cuda.synchronize()
+        barrier()
         elapsed = time.perf_counter() - t0
-        ms_comp, ms_doc, nt = pl.times()
-        summ_all = np.concatenate([o[1] for o in pin_out])
-        statuses = summ_all["status"]
-        out_bytes = sum(t[0] for t in totals[:len(parts)])
-        patch_bytes = sum(t[1] for t in totals[:len(parts)])
-        in_b = int(arena.nbytes)
-        nb = len(parts)
-        t_doc = ms_doc / max(nt, 1)  # average document-kernel time per batch (one launch each)
-        alg_launch = (in_b + out_bytes + patch_bytes) / nb
-        extra["kernel_resident_ops_per_s"] = ops_rank * args.steps / (ms_comp * 1e-3) if ms_comp else None
+        # results home (outside the timed region): summaries, merged documents, patch logs
+        summ_b = [x[6].cpu().numpy().view(pipe.SUMMARY_DT) for x in dev]
+        tot_b = [x[9].cpu().numpy() for x in dev]
+        outs_b = [x[7][:int(t[0])].cpu().numpy() for x, t in zip(dev, tot_b)]
+        pats_b = [x[8][:int(t[1])].cpu().numpy() for x, t in zip(dev, tot_b)]
+        out_bytes = int(sum(int(t[0]) for t in tot_b))
+        patch_bytes = int(sum(int(t[1]) for t in tot_b))
+        summ_all = np.concatenate(summ_b)
+        t_doc = ms_doc / (args.steps * nb)
         extra["kernel_ms_per_step"] = ms_comp / args.steps
         extra["batches"] = nb
         extra["batch_docs"] = batch
-        extra["pcie_bytes_per_step_rank0"] = {"h2d": in_b + int(chunks.nbytes) + int(docs.nbytes),
-                                              "d2h": out_bytes + patch_bytes + D * pipe.SUMMARY_DT.itemsize}
-        workspace = int(ws_need)
-        # per-shard digest: container checksum, length and status of every merged document
-        chk = []
-        for _, s, po, _ in pin_out:
-            off = s["out_off"].astype(np.int64)
-            b4 = [po.u8[off + j].astype(np.uint64) for j in range(4, 8)]
-            chk.append(np.where(s["status"] == 0, b4[0] | (b4[1] << 8) | (b4[2] << 16) | (b4[3] << 24), 0))
-        digest = shard.doc_digest_np(ids, statuses, summ_all["out_len"], np.concatenate(chk).astype(np.uint64))
-        starts = np.cumsum([0] + [len(p[2]) for p in parts])
+        del dev
+        if not args.no_pcie:
+            # the same job from host memory (H2D + chain + D2H, pipelined): PCIe-inclusive, never `value`
+            el_p, _, _, _, _ = run_pipe(max(2, args.steps // 2), 1)
+            sp = max(2, args.steps // 2)
+            hb = torch.empty(min(in_b, 1 << 30), dtype=torch.uint8).pin_memory()
+            db = torch.empty_like(hb, device="cuda")
+            db.copy_(hb, non_blocking=True)
+            torch.cuda.synchronize()
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record()
+            db.copy_(hb, non_blocking=True)
+            e1.record()
+            hb.copy_(db, non_blocking=True)
+            e2.record()
+            torch.cuda.synchronize()
+            extra["pcie_inclusive"] = {
+                "what": "the same job from pinned host memory back to host memory through am_pipe_submit (H2D of "
+                        "arena + descriptors, chain, D2H of documents, patches, summaries; pipelined)",
+                "ops_per_s_rank0": ops_rank / (el_p / sp), "ms_per_step": el_p * 1000.0 / sp, "steps": sp,
+                "pcie_GBps": {"h2d": hb.numel() / (e0.elapsed_time(e1) * 1e-3) / 1e9,
+                              "d2h": hb.numel() / (e1.elapsed_time(e2) * 1e-3) / 1e9},
+                "bytes_per_step_rank0": {"h2d": in_b + int(chunks.nbytes) + int(docs.nbytes),
+                                         "d2h": out_bytes + patch_bytes + D * pipe.SUMMARY_DT.itemsize}}
+            del hb, db
+    else:
+        elapsed, totals, pin_out, ms_comp, t_doc = run_pipe(args.steps, args.warmup)
+        summ_b = [o[1] for o in pin_out]
+        outs_b = [o[2].u8 for o in pin_out]
+        pats_b = [o[3].u8 for o in pin_out]
+        out_bytes = sum(t[0] for t in totals[:nb])
+        patch_bytes = sum(t[1] for t in totals[:nb])
+        summ_all = np.concatenate(summ_b)
+        extra["kernel_ms_per_step"] = ms_comp / args.steps
+        extra["batches"] = nb
+        extra["batch_docs"] = batch
+    statuses = summ_all["status"]
+    alg_launch = (in_b + out_bytes + patch_bytes) / nb
+    workspace = int(ws_need)
+    # per-shard digest: container checksum, length and status of every merged document
+    chk = []
+    for s_, po in zip(summ_b, outs_b):
+        off = s_["out_off"].astype(np.int64)
+        ok_ = s_["status"] == 0
+        offs = np.where(ok_, off, 0)
+        b4 = [po[offs + j].astype(np.uint64) if len(po) else np.zeros(len(offs), np.uint64) for j in range(4, 8)]
+        chk.append(np.where(ok_, b4[0] | (b4[1] << 8) | (b4[2] << 16) | (b4[3] << 24), 0))
+    digest = shard.doc_digest_np(ids, statuses, summ_all["out_len"], np.concatenate(chk).astype(np.uint64))
 
-        def check(i):
-            k = int(np.searchsorted(starts, i, side="right") - 1)
-            s = pin_out[k][1][i - starts[k]]
-            o = bytes(pin_out[k][2].u8[int(s["out_off"]):int(s["out_off"]) + int(s["out_len"])])
-            p = bytes(pin_out[k][3].u8[int(s["patch_off"]):int(s["patch_off"]) + int(s["patch_len"])])
-            return o, (p if not args.no_patch else None)
+    def check(i):
+        k = int(np.searchsorted(starts, i, side="right") - 1)
+        s_ = summ_b[k][i - starts[k]]
+        o = bytes(outs_b[k][int(s_["out_off"]):int(s_["out_off"]) + int(s_["out_len"])])
+        p_ = bytes(pats_b[k][int(s_["patch_off"]):int(s_["patch_off"]) + int(s_["patch_len"])])
+        return o, (p_ if not args.no_patch else None)
 
     nerr = int((statuses != 0).sum())
     tot, _ = shard.exchange(dist, [D, ops_rank, nerr, out_bytes, digest or 0], xdev)
@@ -357,14 +390,13 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
     value = tot[1] / (elapsed / args.steps)
     achieved = alg_launch / (t_doc * 1e-3) / 1e9 if t_doc else None
-    tr = (measured_traffic(extra.get("batch_docs")) if args.mode == "pipe" and args.workload == "c4" and not args.no_patch
-          else None)
+    tr = measured_traffic(extra.get("batch_docs")) if args.workload == "c4" and not args.no_patch else None
     if t_doc:
         # decode GB/s: algorithmic decode bytes of one launch (encoded input read + SoA
         # written, per document from an oracle-decoded sample) / the document kernel's time; the
         # kernel does the merge, encode and patch in the same time, so this is a lower bound
         din, dsoa = decode_alg_bytes(arena, chunks, docs)
-        per_launch = (D / (nb if args.mode == "pipe" else 1)) * (din + dsoa)
+        per_launch = (D / nb) * (din + dsoa)
         extra["decode_GBps"] = per_launch / (t_doc * 1e-3) / 1e9
         extra["decode_frac_of_hbm_peak"] = extra["decode_GBps"] / HBM_PEAK_GBPS
         extra["decode_bytes_per_doc"] = {"input": din, "soa": dsoa}
@@ -378,7 +410,8 @@ def main():
                                   "how": "oracle load + applyChanges + save of all %d documents (tools/pin_c4_digest.py)" % tot[0]}
     wl = {"c4": "C4 1M-document job: load base doc + applyChanges of 12 concurrent changes (4 actors x 3), 60 ops/doc",
           "c2": "C2: applyChanges of 3 changes (10 map/counter/string sets + 2 concurrent inc/overwrite), 14 ops/doc"}
-    what = "H2D + merge + applyChanges patch + D2H (pipelined)" if args.mode == "pipe" else "kernels, inputs resident in HBM"
+    what = ("H2D + merge + applyChanges patch + D2H (pipelined)" if args.mode == "pipe" else
+            "inputs resident in HBM: merge + applyChanges patch + compaction in HBM, all 16 batch chains per step")
     if args.no_patch:
         what = what.replace(" + applyChanges patch", "")
     line = {

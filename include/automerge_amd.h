@@ -271,6 +271,18 @@ int am_pipe_submit(am_pipe *p, const uint8_t *arena, uint64_t arena_len, const a
 /* Waits until every submitted batch is home. totals (optional, 2 per batch in submission order
  * since the last drain, up to cap batches): output / patch arena bytes. */
 int am_pipe_drain(am_pipe *p, uint64_t *totals, uint32_t cap, am_error *err);
+/* The same chain for a batch already resident in device memory (the bench's HBM-resident job):
+ * d_arena (arena_len + 64 readable bytes), d_chunks, d_docs and the outputs are device pointers;
+ * any_diff: some document asks for the applyChanges patch. Merged documents, patch logs and
+ * summaries are compacted into d_out / d_patches / d_summary (layout of am_pipe_submit) and their
+ * two arena totals into d_totals; nothing crosses the host link and the call does not wait.
+ * am_pipe_resident_sync waits for the stream; ms2 = the chains / document kernels of the resident
+ * batches since its last call, summed (HIP events). */
+int am_pipe_run_resident(am_pipe *p, const uint8_t *d_arena, uint64_t arena_len, const am_chunk_desc *d_chunks,
+                         uint32_t nchunks, const am_doc_desc *d_docs, uint32_t ndocs, int any_diff, am_doc_summary *d_summary,
+                         uint8_t *d_out, uint64_t out_cap, uint8_t *d_patches, uint64_t patch_cap, uint64_t *d_totals,
+                         am_error *err);
+int am_pipe_resident_sync(am_pipe *p, float *ms2, am_error *err);
 /* Device time (ms) of the batches retired since the last call (reset on read): [0] their whole
  * compute chains summed, [1] their document kernels (k_doc_fast + k_doc) summed; n = batches. */
 int am_pipe_times(am_pipe *p, float *ms2, uint32_t *n);
