@@ -301,6 +301,7 @@ struct am_batch {
   DevBuf<DocBounds> bounds;
   DevBuf<uint64_t> ws_bytes, ws_off, scan_tmp, ws_total, max_hot;
   DevBuf<uint8_t> fast_done;
+  DevBuf<uint32_t> rest;  // k_rest's list of what k_doc_fast left
   uint32_t fast_lds = 0;
   bool fast_only = false;
   bool any_diff = false;
@@ -320,7 +321,7 @@ struct am_batch {
     BatchDev b;
     b.arena = arena.p; b.chunks = chunks.p; b.docs = docs.p; b.known = known.p; b.info = info.p; b.hdr = hdr.p; b.bounds = bounds.p;
     b.ws_bytes = ws_bytes.p; b.ws_off = ws_off.p; b.scan_tmp = scan_tmp.p; b.ws_total = ws_total.p; b.max_hot = max_hot.p; b.lds_bytes = lds_bytes; b.max_hot_host = max_hot_v; b.ws = ws.p;
-    b.fast_lds = fast_lds; b.fast_done = fast_done.p; b.fast_only = fast_only; b.any_diff = any_diff;
+    b.fast_lds = fast_lds; b.fast_done = fast_done.p; b.fast_only = fast_only; b.any_diff = any_diff; b.rest = rest.p;
     b.ws_cap = ws.cap; b.results = results.p; b.chg_state = chg_state.p; b.nchunks = nchunks; b.ndocs = ndocs;
     return b;
   }
@@ -457,7 +458,7 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   if (!b->arena.ensure(arena_len + 64) || !b->chunks.ensure(nchunks) || !b->docs.ensure(ndocs) || !b->known.ensure(nknown) ||
       !b->info.ensure(nchunks) || !b->hdr.ensure(nchunks) || !b->bounds.ensure(ndocs) || !b->ws_bytes.ensure(ndocs) || !b->ws_off.ensure(ndocs) ||
       !b->scan_tmp.ensure(am_scan_tmp_elems(ndocs)) || !b->ws_total.ensure(1) || !b->max_hot.ensure(2) ||
-      !b->fast_done.ensure(ndocs) || !b->results.ensure(ndocs) ||
+      !b->fast_done.ensure(ndocs) || !b->rest.ensure(ndocs + 1) || !b->results.ensure(ndocs) ||
       !b->chg_state.ensure(nchunks))
     return false;
   if (arena_len) HIPCHECK(hipMemcpyAsync(b->arena.p, arena, arena_len, hipMemcpyHostToDevice, s));
@@ -817,7 +818,8 @@ extern "C" am_pipe* am_pipe_create(am_engine* eng, const am_pipe_caps* caps, am_
         b.arena.ensure(c.arena_bytes + 64) && b.chunks.ensure(c.chunks) && b.docs.ensure(c.docs) && b.known.ensure(1) &&
         b.info.ensure(c.chunks) && b.hdr.ensure(c.chunks) && b.bounds.ensure(c.docs) && b.ws_bytes.ensure(c.docs) &&
         b.ws_off.ensure(c.docs) && b.scan_tmp.ensure(am_scan_tmp_elems(c.docs)) && b.ws_total.ensure(1) &&
-        b.max_hot.ensure(2) && b.fast_done.ensure(c.docs) && b.results.ensure(c.docs) && b.chg_state.ensure(c.chunks) &&
+        b.max_hot.ensure(2) && b.fast_done.ensure(c.docs) && b.rest.ensure(c.docs + 1) && b.results.ensure(c.docs) &&
+        b.chg_state.ensure(c.chunks) &&
         b.ws.ensure(c.ws_bytes + 16) && sl->olen.ensure(c.docs) && sl->ooff.ensure(c.docs) && sl->plen.ensure(c.docs) &&
         sl->poff.ensure(c.docs) && sl->tmp.ensure(am_scan_tmp_elems(c.docs)) && sl->totals.ensure(2) &&
         sl->dout.ensure(c.out_bytes + 16) && sl->dpatch.ensure(c.patch_bytes + 16) && sl->summ.ensure(c.docs);

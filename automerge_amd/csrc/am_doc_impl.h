@@ -1180,14 +1180,15 @@ __device__ static bool radix_docorder(DocShared& s, SortRec* sr, uint32_t n, uin
   return true;
 }
 
-__global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
-                                               const am_doc_desc* __restrict__ docs, const am_known_hash* __restrict__ known,
-                                               const ChunkInfo* __restrict__ info, const DocBounds* __restrict__ bounds,
-                                               const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base,
-                                               uint64_t ws_cap, uint32_t lds_bytes, am_doc_result* __restrict__ results,
-                                               int32_t* __restrict__ chg_state, const uint8_t* __restrict__ fast_done) {
+// One document by the whole workgroup (the body of k_doc below).
+__device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
+                                          const am_doc_desc* __restrict__ docs, const am_known_hash* __restrict__ known,
+                                          const ChunkInfo* __restrict__ info, const DocBounds* __restrict__ bounds,
+                                          const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base,
+                                          uint64_t ws_cap, uint32_t lds_bytes, am_doc_result* __restrict__ results,
+                                          int32_t* __restrict__ chg_state, const uint8_t* __restrict__ fast_done) {
   __shared__ DocShared s;
-  const uint32_t doc = blockIdx.x, t = threadIdx.x, T = blockDim.x;
+  const uint32_t t = threadIdx.x, T = blockDim.x;
   if (fast_done && fast_done[doc]) return;  // merged by k_doc_fast (am_doc_fast.h)
   const am_doc_desc dd = docs[doc];
   uint8_t* const wsg = ws_base + ws_off[doc];  // global (derived from the kernel argument)
@@ -2037,6 +2038,32 @@ done:
     r.ws_off = ws_off[doc];
     r.ws_bytes = s.L.total;
     results[doc] = r;
+  }
+}
+
+// k_doc: workgroup per document (grid = documents), or -- LDS mode after k_doc_fast, with `rest` --
+// a grid of a few thousand workgroups looping over the list of the documents k_doc_fast left
+// (rest[0] = how many, rest[1..]), so a batch the fast kernel merged whole costs microseconds here.
+__global__ void __launch_bounds__(kDocT) K_DOC_WAVES_ATTR k_doc(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
+                                               const am_doc_desc* __restrict__ docs, const am_known_hash* __restrict__ known,
+                                               const ChunkInfo* __restrict__ info, const DocBounds* __restrict__ bounds,
+                                               const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base,
+                                               uint64_t ws_cap, uint32_t lds_bytes, am_doc_result* __restrict__ results,
+                                               int32_t* __restrict__ chg_state, const uint8_t* __restrict__ fast_done,
+                                               const uint32_t* __restrict__ rest) {
+  if constexpr (kHotLds) {
+    // one call site (the body is large): without `rest` the loop runs once, for blockIdx.x
+    const uint32_t n = rest ? rest[0] : blockIdx.x + 1, step = rest ? gridDim.x : 1u;
+    for (uint32_t i = blockIdx.x; i < n; i += step) {
+      __syncthreads();  // the previous document's shared state is no longer read
+      k_doc_one(rest ? rest[1 + i] : i, arena, chunks, docs, known, info, bounds, ws_off, ws_base, ws_cap, lds_bytes, results,
+                chg_state, fast_done);
+    }
+  } else {
+    // the global mode keeps one workgroup per document (a loop costs it its register budget)
+    (void)rest;
+    k_doc_one(blockIdx.x, arena, chunks, docs, known, info, bounds, ws_off, ws_base, ws_cap, lds_bytes, results, chg_state,
+              fast_done);
   }
 }
 

@@ -903,16 +903,27 @@ size_t am_scan_tmp_elems(uint32_t n) { return (n + SCAN_T - 1) / SCAN_T + 1; }
 // max_hot[0]: largest k_doc hot working set; max_hot[1]: largest k_doc_fast LDS slice (0: none)
 __global__ void __launch_bounds__(256) k_max_hot(const DocBounds* __restrict__ bounds, const am_doc_desc* __restrict__ docs,
                                                  uint32_t ndocs, uint64_t* __restrict__ max_hot) {
-  uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= ndocs) return;
-  const DocBounds b = bounds[d];
-  WsLayout L = ws_layout(b);
-  // a scattered document needs the global-mode launch: report a hot set above any LDS budget
-  const uint64_t h = doc_scattered(b) ? (1ull << 40) : L.hot_total;
-  atomicMax(reinterpret_cast<unsigned long long*>(max_hot), (unsigned long long)h);
-  const am_doc_desc dd = docs[d];
-  if (fast_eligible(b, dd))
-    atomicMax(reinterpret_cast<unsigned long long*>(max_hot + 1), (unsigned long long)fast_layout(b, dd.known_count).total);
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t h = 0, f = 0;
+  if (d < ndocs) {
+    const DocBounds b = bounds[d];
+    const WsLayout L = ws_layout(b);
+    // a scattered document needs the global-mode launch: report a hot set above any LDS budget
+    h = doc_scattered(b) ? (1ull << 40) : L.hot_total;
+    const am_doc_desc dd = docs[d];
+    if (fast_eligible(b, dd)) f = fast_layout(b, dd.known_count).total;
+  }
+  // one atomic per wave (not per document: 65536 on one address serialize)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t h2 = __shfl_xor(h, o, 64), f2 = __shfl_xor(f, o, 64);
+    h = h2 > h ? h2 : h;
+    f = f2 > f ? f2 : f;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (h) atomicMax(reinterpret_cast<unsigned long long*>(max_hot), (unsigned long long)h);
+    if (f) atomicMax(reinterpret_cast<unsigned long long*>(max_hot + 1), (unsigned long long)f);
+  }
 }
 
 void am_launch_chunks(const BatchDev& b, hipStream_t s) {
@@ -976,6 +987,18 @@ void am_launch_bounds(const BatchDev& b, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, b.scan_tmp, nblk, b.ws_total);
   hipLaunchKernelGGL(k_scan_add, dim3(nblk), dim3(SCAN_T), 0, s, b.ws_off, b.scan_tmp, b.ndocs);
 }
+// the documents k_doc_fast left, as a list for k_doc's loop (rest[0] = count, zeroed beforehand)
+__global__ void __launch_bounds__(256) k_rest(const uint8_t* __restrict__ fast_done, uint32_t ndocs, uint32_t* __restrict__ rest) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x, l = threadIdx.x & 63;
+  const bool need = d < ndocs && !fast_done[d];
+  const uint64_t m = __ballot(need);
+  uint32_t base = 0;
+  if (l == 0 && m) base = atomicAdd(rest, (uint32_t)__popcll(m));
+  base = __shfl(base, 0, 64);
+  if (need) rest[1 + base + (uint32_t)__popcll(m & ((1ull << l) - 1))] = d;
+}
+#define K_DOC_LOOP_WG 2048  // workgroups of k_doc's loop over the documents k_doc_fast left
+
 void am_launch_doc(const BatchDev& b, hipStream_t s) {
   if (!b.ndocs) return;
   // documents whose hot working set fits the LDS allocation run from LDS; the rest (if any)
@@ -991,11 +1014,20 @@ void am_launch_doc(const BatchDev& b, hipStream_t s) {
     fd = b.fast_done;
   }
   if (!b.fast_only) {
-    hipLaunchKernelGGL(lds_mode::k_doc, dim3(b.ndocs), dim3(DOC_T), b.lds_bytes, s, b.arena, b.chunks, b.docs, b.known,
-                       b.info, b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd);
+    // after k_doc_fast: k_doc loops over the list of what it left (a batch merged whole by the fast
+    // kernel then costs a few microseconds here instead of one workgroup launch per document)
+    const uint32_t* rest = fd && b.rest ? b.rest : nullptr;
+    uint32_t grid = b.ndocs;
+    if (rest) {
+      (void)hipMemsetAsync(b.rest, 0, sizeof(uint32_t), s);
+      hipLaunchKernelGGL(k_rest, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, fd, b.ndocs, b.rest);
+      grid = b.ndocs < K_DOC_LOOP_WG ? b.ndocs : K_DOC_LOOP_WG;
+    }
+    hipLaunchKernelGGL(lds_mode::k_doc, dim3(grid), dim3(DOC_T), b.lds_bytes, s, b.arena, b.chunks, b.docs, b.known,
+                       b.info, b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd, rest);
     if (b.max_hot_host > b.lds_bytes)
       hipLaunchKernelGGL(glb_mode::k_doc, dim3(b.ndocs), dim3(DOC_T_GLB), 0, s, b.arena, b.chunks, b.docs, b.known, b.info,
-                         b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd);
+                         b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd, nullptr);
   }
 }
 __global__ void __launch_bounds__(256) k_out_hash_ws(am_doc_result* __restrict__ res, uint32_t ndocs, uint8_t* __restrict__ ws,

@@ -26,6 +26,7 @@ struct BatchDev {
   uint64_t max_hot_host;   // host copy of *max_hot
   uint32_t fast_lds;       // k_doc_fast LDS slice per document (0: no document in its envelope / disabled)
   uint8_t* fast_done;      // per doc: 1 = merged by k_doc_fast
+  uint32_t* rest;          // [0] = count, [1..]: the documents k_doc_fast left (k_rest)
   bool fast_only;          // every document is in the fast envelope: skip the k_doc launches
   bool any_diff;           // some document asks for its applyChanges patch (k_doc_fast<true>)
   uint8_t* ws;
