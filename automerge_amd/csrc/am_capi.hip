@@ -468,7 +468,7 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   b->nchunks = nchunks;
   b->ndocs = ndocs;
   b->any_diff = false;
-  for (uint32_t d = 0; d < ndocs && !b->any_diff; d++) b->any_diff = (docs[d].flags & AM_DOC_WANT_DIFF) != 0;
+  for (uint32_t d = 0; d < ndocs && !b->any_diff; d++) b->any_diff = (docs[d].flags & (AM_DOC_WANT_DIFF | AM_DOC_WANT_PATCH)) != 0;
   if (!inflate_stage(b, arena, arena_len, chunks, nchunks, docs, ndocs)) return false;
   // sizing pass: chunk counts -> per-document workspace bounds -> total
   BatchDev d = b->dev();
@@ -958,7 +958,7 @@ extern "C" int am_pipe_submit(am_pipe* p, const uint8_t* arena, uint64_t arena_l
   b.nchunks = nchunks;
   b.ndocs = ndocs;
   b.any_diff = false;
-  for (uint32_t d = 0; d < ndocs && !b.any_diff; d++) b.any_diff = (docs[d].flags & AM_DOC_WANT_DIFF) != 0;
+  for (uint32_t d = 0; d < ndocs && !b.any_diff; d++) b.any_diff = (docs[d].flags & (AM_DOC_WANT_DIFF | AM_DOC_WANT_PATCH)) != 0;
   // inputs
   if (arena_len && hipMemcpyAsync(b.arena.p, arena, arena_len, hipMemcpyHostToDevice, p->s_in) != hipSuccess) return fail("automerge_amd: H2D failed");
   if (nchunks && hipMemcpyAsync(b.chunks.p, chunks, sizeof(am_chunk_desc) * nchunks, hipMemcpyHostToDevice, p->s_in) != hipSuccess)

@@ -118,7 +118,7 @@ __host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t n
   // (a larger image fails the encoder's capacity check: the document then goes to k_doc)
   const uint32_t out = 64 + 40 * b.A + 42 * b.H + 25 * 12 + span;
   if (out > cells) cells = out;
-  if (b.P == 2 && cells < FD_DIFF_SCRATCH) cells = FD_DIFF_SCRATCH;  // fast_diff's tables
+  if (b.P && cells < FD_DIFF_SCRATCH) cells = FD_DIFF_SCRATCH;  // fast_diff's / fast_getpatch's tables
   F.cells = take(cells);
   F.cells_cap = cells;
   F.total = o;
@@ -126,7 +126,8 @@ __host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t n
 }
 
 __host__ __device__ inline bool fast_eligible(const DocBounds& b, const am_doc_desc& dd) {
-  if (dd.flags & (AM_DOC_WANT_PATCH | AM_DOC_FIX_UTF8 | AM_DOC_PATCH_ROOM | AM_DOC_META)) return false;  // getPatch: k_doc (P7); applyChanges patches: fast_diff
+  // getPatch logs: fast_getpatch; applyChanges patches: fast_diff (both fall back to k_doc)
+  if (dd.flags & (AM_DOC_FIX_UTF8 | AM_DOC_PATCH_ROOM | AM_DOC_META)) return false;
   if (b.B == 0 || doc_scattered(b) || b.UC) return false;
   if (dd.base_chunk < 0 && dd.chg_count == 0) return false;
   if (b.span_hi - b.span_lo > FD_SPAN_MAX) return false;
@@ -1022,6 +1023,295 @@ __device__ __forceinline__ bool fast_diff(const uint8_t* IN, uint8_t* PS, uint32
   return true;
 }
 
+// Backend.getPatch (documentPatch, new.js:1604-1635, 2052-2060; patch_scan in am_patch.h) of the
+// merged document, written by the whole wave in wire form for the common shape: every op of the root
+// is a keyed `set`, `inc` or make op, every op of a child object is the insert (`set`) of its own list
+// element, and every child object is made by a root op. For that shape documentPatch's single pass
+// reduces to closed forms over the output positions (document order):
+//   * a key's props are its ops without succ (values, child objects) plus each counter `set` whose
+//     succs are all increments of the key, shown at its last increment with their sum
+//     (counterStates, new.js:937-965); the key record comes with the key's first prop;
+//   * a list's edits are its visible elements as inserts at their visible index, joined by
+//     appendEdit's multi-insert rule (new.js:747-782) into runs of consecutive counters of one actor
+//     with one datatype and JS type;
+//   * a child object is in the patch iff its make op has no succ (objectMeta reachability).
+// Anything else (deletes inside lists, nested objects, map children with ops, errors) returns false
+// and k_doc writes the log (P7). Scratch: FD_DIFF_SCRATCH bytes at PS.
+__device__ __forceinline__ bool fast_getpatch(const uint8_t* IN, uint8_t* PS, uint32_t ps_cap, uint8_t* out, uint64_t out_cap,
+                                              uint8_t* M, uint32_t NOUT, uint32_t NSUCC, uint32_t NA, uint32_t NC, uint32_t nbc,
+                                              uint32_t N, const int32_t* OUTC, const uint8_t* OUTA, const uint32_t* RO,
+                                              const ChgHdrC* chh) {
+  const FdRec P = fd_rec(M);
+  const uint32_t l = lane();
+  const bool outl = l < NOUT;
+  bool pbad = ps_cap < FD_DIFF_SCRATCH || NOUT > 64 || NSUCC > 64;
+  if (__any(pbad)) return false;
+  // the row at output position l and its values
+  const uint32_t r = outl ? P.krow[l] : 0u, sc = outl ? P.sck[l] : 0u, so = outl ? P.sok[l] : 0u;
+  const int32_t k_key = outl ? (int32_t)P.key[r] : FD_NULL, k_objc = outl ? P.objc[r] : FD_NULL;
+  const int32_t k_idc = outl ? P.idc[r] : 0, k_vlen = outl ? P.vlen[r] : FD_NULL;
+  const uint32_t k_voff = outl ? P.voff[r] : 0u;
+  const int32_t k_obja = outl ? (int32_t)P.obja[r] : -1, k_ida = outl ? (int32_t)P.ida[r] : 0;
+  const uint32_t k_kr = outl ? P.krank[r] : 0u;
+  const int32_t k_act = outl ? (int32_t)P.act[r] : 0;
+  const uint32_t fl = outl ? P.flags[r] : 0u;
+  const bool k_ins = (fl & 2) != 0, k_keyed = (fl & 4) != 0;
+  const bool root = outl && k_objc == FD_NULL;
+  const bool child = outl && !root;
+  const bool is_make = k_act == 0 || k_act == 2 || k_act == 4 || k_act == 6;
+  // maxOp of documentPatch: ids and succ ids of every op
+  int32_t mx = outl ? k_idc : 0;
+  if (l < NSUCC && OUTC[l] > mx) mx = OUTC[l];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int32_t y = __shfl_xor(mx, o, 64);
+    mx = y > mx ? y : mx;
+  }
+  // object sections: first position of each object; a child object's make op (a root op)
+  const int32_t p_objc = wave::up1(k_objc, (int32_t)0x7fffffff), p_obja = wave::up1(k_obja, (int32_t)-2);
+  const bool first_obj = outl && (l == 0 || p_objc != k_objc || p_obja != k_obja);
+  const uint64_t fom = __ballot(first_obj);
+  const uint64_t le = l == 63 ? ~0ull : ((2ull << l) - 1);  // positions <= l
+  const uint64_t fo_le = fom & le;
+  const uint32_t ostart = fo_le ? 63u - (uint32_t)__clzll(fo_le) : 0u;
+  int32_t mk = -1;
+  for (uint32_t j = 0; j < NOUT; j++) {
+    const int32_t jc = wave::bcast(k_idc, (int)j), ja = wave::bcast(k_ida, (int)j);
+    if (child && jc == k_objc && ja == k_obja) mk = (int32_t)j;
+  }
+  const uint32_t mku = mk < 0 ? 0u : (uint32_t)mk;
+  const int32_t m_act = __shfl(k_act, mku, 64);
+  const uint32_t m_sc = __shfl(sc, mku, 64);
+  const int32_t m_root = __shfl((int32_t)root, mku, 64);
+  // a child object: made by a root list / text op; reachable iff that op has no succ
+  pbad |= child && (mk < 0 || !m_root || (m_act != 2 && m_act != 4));
+  const bool reach = root || (child && m_sc == 0);
+  pbad |= root && (!k_keyed || (k_key & 255) == 0 || !(k_act == 1 || k_act == 5 || is_make));
+  pbad |= child && reach && (!k_ins || k_keyed || k_act != 1);
+  if (__any(pbad)) return false;
+
+  // ---- counters: lane per succ entry; entry q belongs to the op at output position OWNE[q] ----
+  uint8_t* const OWNE = PS;                                       // succ entry -> owner position
+  uint8_t* const CAT = PS + 64;                                   // position -> 1 + counter completed here
+  uint32_t* const COV = reinterpret_cast<uint32_t*>(PS + 128);    // position -> counter sets naming it
+  CAT[l] = 0;
+  COV[l] = 0;
+  if (outl)
+    for (uint32_t j = 0; j < sc; j++) OWNE[so + j] = (uint8_t)l;
+  wsync();
+  const bool counter = root && k_act == 1 && sc > 0 && k_vlen != FD_NULL && (k_vlen & 15) == 8;
+  int64_t cnt_sum = 0;
+  if (__any(counter) || __any(root && k_act == 5)) {
+    const bool isent = l < NSUCC;
+    const uint32_t own = isent ? OWNE[l] : 0u;
+    const int32_t ec = isent ? OUTC[l] : 0, ea = isent ? (int32_t)OUTA[l] : -1;
+    int32_t tgt = -1;  // the position of the op with the entry's opId
+    for (uint32_t j = 0; j < NOUT; j++) {
+      const int32_t jc = wave::bcast(k_idc, (int)j), ja = wave::bcast(k_ida, (int)j);
+      if (isent && jc == ec && ja == ea) tgt = (int32_t)j;
+    }
+    const uint32_t tu = tgt < 0 ? 0u : (uint32_t)tgt;
+    const int32_t o_counter = __shfl((int32_t)counter, own, 64);
+    const uint32_t o_kr = __shfl(k_kr, own, 64);
+    const int32_t t_act = __shfl(k_act, tu, 64), t_vlen = __shfl(k_vlen, tu, 64), t_root = __shfl((int32_t)root, tu, 64);
+    const uint32_t t_kr = __shfl(k_kr, tu, 64), t_voff = __shfl(k_voff, tu, 64);
+    const bool inc_of_key = isent && tgt >= 0 && t_act == 5 && t_root && t_kr == o_kr;
+    if (isent && o_counter && inc_of_key) atomicAdd(&COV[tu], 1u);
+    int64_t iv = 0;
+    bool ok = isent && o_counter && inc_of_key;
+    if (ok) {
+      uint32_t vt, dt;
+      int64_t v1;
+      const uint32_t t15 = t_vlen == FD_NULL ? 0u : ((uint32_t)t_vlen & 15);
+      ok = (t15 == 3 || t15 == 4 || t15 == 8 || t15 == 9) && fd_value(IN, t_vlen, t_voff, vt, dt, iv, v1);
+      pbad |= isent && o_counter && inc_of_key && !ok;  // a non-integer increment: k_doc writes it
+    }
+    // per counter set: the sum of its increments, whether every succ is one, the last of them
+    uint64_t owners = __ballot(counter);
+    while (owners) {
+      const uint32_t pw = (uint32_t)__builtin_ctzll(owners);
+      owners &= owners - 1;
+      const bool mine = isent && own == pw;
+      int64_t sv = mine && ok ? iv : 0;
+      uint32_t sb = mine && !ok ? 1u : 0u;
+      int32_t last = mine ? tgt : -1;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        sv += __shfl_xor(sv, o, 64);
+        sb += __shfl_xor(sb, o, 64);
+        const int32_t y = __shfl_xor(last, o, 64);
+        last = y > last ? y : last;
+      }
+      if (l == pw) cnt_sum = sv;
+      if (l == 0 && sb == 0 && last >= 0) CAT[last] = (uint8_t)(pw + 1);
+    }
+  }
+  wsync();
+  // every increment is named by exactly one counter set of its key (else: increment operation for
+  // unknown counter -- k_doc reports it)
+  pbad |= root && k_act == 5 && COV[l] != 1;
+  if (__any(pbad)) return false;
+
+  // ---- props of the root (PR_KEY / PR_PROP) and edits of the lists, by output position ----
+  const uint32_t cat = outl ? CAT[l] : 0u;
+  const uint32_t cown = cat ? cat - 1 : 0u;
+  const int64_t c_sum = __shfl(cnt_sum, cown, 64);
+  const int32_t c_idc = __shfl(k_idc, cown, 64), c_ida = __shfl(k_ida, cown, 64);
+  const int32_t c_vlen = __shfl(k_vlen, cown, 64);
+  const uint32_t c_voff = __shfl(k_voff, cown, 64);
+  bool have = false;
+  uint32_t vt = 0, vdt = 0;
+  int64_t v0 = 0, v1 = 0;
+  int32_t pk_c = k_idc, pk_a = k_ida;
+  if (root) {
+    if (k_act == 5) {
+      if (cat) {  // the counter completed by this increment (new.js:962-963)
+        have = true;
+        pbad |= !fd_value(IN, c_vlen, c_voff, vt, vdt, v0, v1);
+        v0 += c_sum;
+        pk_c = c_idc;
+        pk_a = c_ida;
+      }
+    } else if (sc == 0) {
+      have = true;
+      if (k_act == 1) pbad |= !fd_value(IN, k_vlen, k_voff, vt, vdt, v0, v1);
+      else { vt = PV_CHILD; vdt = pv_obj_type(k_act); v0 = k_idc; v1 = k_ida; }
+    }
+  }
+  // key groups of the root: the key record precedes the group's first prop
+  const uint32_t p_kr = wave::up1(k_kr, ~0u);
+  const bool p_root = wave::up1((uint32_t)root, 0u) != 0;
+  const bool gfirst = root && (l == 0 || !p_root || p_kr != k_kr);
+  const uint64_t gm = __ballot(gfirst) & le;
+  const uint32_t gs = gm ? 63u - (uint32_t)__clzll(gm) : 0u;
+  const uint64_t hm = __ballot(have);
+  const uint64_t before_l = le & ~(l == 63 ? 0ull : (1ull << l)) & ~((1ull << gs) - 1);  // positions [gs, l)
+  const bool emit_key = have && (hm & before_l) == 0;
+  // list elements: visible ones are inserts at their visible index
+  const bool vis = child && reach && sc == 0;
+  uint32_t ivt = 0, idt = 0, dtc = 0;
+  int64_t iv0 = 0, iv1 = 0;
+  if (vis) {
+    pbad |= !fd_value(IN, k_vlen, k_voff, ivt, idt, iv0, iv1);
+    dtc = pv_dtcode(ivt, idt);
+    pbad |= dtc == 100;  // datatype 0 (falsy): appendEdit's chain rule differs; k_doc writes it
+  }
+  const uint64_t vm = __ballot(vis);
+  const uint64_t ob = le & ~(l == 63 ? 0ull : (1ull << l)) & ~((1ull << ostart) - 1);  // positions [ostart, l)
+  const int64_t idx = __popcll(vm & ob);
+  const uint64_t pvm = vm & ob;
+  const uint32_t prv = pvm ? 63u - (uint32_t)__clzll(pvm) : 0u;
+  const int32_t q_idc = __shfl(k_idc, prv, 64), q_ida = __shfl(k_ida, prv, 64);
+  const uint32_t q_dtc = __shfl(dtc, prv, 64), q_ty = __shfl((uint32_t)pv_typeof(ivt), prv, 64);
+  const bool chain = vis && pvm && q_ida == k_ida && q_idc + 1 == k_idc && q_dtc == dtc && q_ty == (uint32_t)pv_typeof(ivt);
+  const bool start = vis && !chain;
+  const uint64_t smask = __ballot(start);
+  const uint64_t above = l == 63 ? 0ull : (smask >> (l + 1)) << (l + 1);
+  const uint32_t nxt = above ? ctz64(above) : 64u;
+  const uint64_t span = (nxt >= 64 ? ~0ull : ((1ull << nxt) - 1)) & ~((1ull << l) - 1);
+  const uint32_t run = start ? (uint32_t)__popcll(vm & span) : 0u;
+  const uint32_t mdt = pv_dt_truthy(dtc) ? dtc : 0u;
+  if (__any(pbad)) return false;
+
+  // ---- record sizes: actors, clock, then the positions in document order ----
+  const uint32_t a_off = l < NA ? RO[2 * M[FM_DP2REF + l]] : 0u, a_len = l < NA ? RO[2 * M[FM_DP2REF + l] + 1] : 0u;
+  uint32_t tot;
+  const uint32_t b_act = l < NA ? 1u + pk_uleb_len(a_len) + a_len : 0u;
+  const uint32_t o_act = excl_add(b_act, tot);
+  uint32_t base = tot;
+  uint32_t* const LASTC = reinterpret_cast<uint32_t*>(PS + 384);  // doc actor -> its last change row
+  LASTC[l] = 0;
+  wsync();
+  const uint32_t kc = l >= nbc ? l - nbc : 0u;
+  const uint32_t kc_adp = __shfl(l < N ? (uint32_t)P.adp[l] : 0u, kc & 63, 64);
+  const uint32_t c_actor = l < nbc ? (uint32_t)P.bca[l] : kc_adp;
+  const int64_t c_seq = l < nbc ? (int64_t)P.bcs[l] : chh[kc < 64 ? kc : 0].seq;
+  if (l < NC) atomicMax(&LASTC[c_actor], l);
+  wsync();
+  const bool c_emit = l < NC && LASTC[c_actor] == l;
+  const uint32_t b_clk = c_emit ? 1u + pk_uleb_len(c_actor) + pk_uleb_len((uint64_t)c_seq) : 0u;
+  const uint32_t o_clk = base + excl_add(b_clk, tot);
+  base += tot;
+  const bool obj_rec = first_obj && reach;
+  const uint32_t b_obj = obj_rec ? (root ? 4u : 1u + pk_sleb_len(k_objc) + pk_sleb_len(k_obja) + 1u) : 0u;
+  const uint32_t klen = (uint32_t)k_key & 255;
+  uint32_t b_pos = b_obj;
+  if (root && have)
+    b_pos += (emit_key ? 1u + pk_uleb_len(klen) + klen : 0u) + 1u + pk_uleb_len((uint64_t)pk_c) + pk_uleb_len((uint64_t)pk_a) +
+             pk_value_len(vt, vdt, v0, v1);
+  if (vis) {
+    if (start && run >= 2)
+      b_pos += 1 + pk_uleb_len((uint64_t)idx) + pk_uleb_len((uint64_t)k_idc) + pk_uleb_len((uint64_t)k_ida) + pk_uleb_len(mdt) +
+               pk_uleb_len(run);
+    else if (start)
+      b_pos += 1 + pk_uleb_len((uint64_t)idx) + 2 * (pk_uleb_len((uint64_t)k_idc) + pk_uleb_len((uint64_t)k_ida));
+    b_pos += pk_value_len(ivt, idt, iv0, iv1);
+  }
+  const uint32_t o_pos = base + excl_add(b_pos, tot);
+  base += tot;
+  if (__any(sizeof(PatchHdr2) + (uint64_t)base > out_cap)) return false;
+
+  // ---- write ----
+  uint8_t* const o = out + sizeof(PatchHdr2);
+  if (b_act) {
+    uint8_t* p = o + o_act;
+    *p++ = PR_ACTOR;
+    p = pk_uleb(p, a_len);
+    for (uint32_t q = 0; q < a_len; q++) p[q] = IN[a_off + q];
+  }
+  if (b_clk) {
+    uint8_t* p = o + o_clk;
+    *p++ = PR_CLOCK;
+    p = pk_uleb(p, c_actor);
+    pk_uleb(p, (uint64_t)c_seq);
+  }
+  if (b_pos) {
+    uint8_t* p = o + o_pos;
+    if (obj_rec) {  // PR_OBJ (documentPatch leaves its type field 0)
+      *p++ = PR_OBJ;
+      if (root) { *p++ = 0x7f; *p++ = 0x7f; }
+      else { p = pk_sleb(p, k_objc); p = pk_sleb(p, k_obja); }
+      *p++ = 0;
+    }
+    if (root && have) {
+      if (emit_key) {
+        *p++ = PR_KEY;
+        p = pk_uleb(p, klen);
+        const uint32_t ko = (uint32_t)k_key >> 8;
+        for (uint32_t q = 0; q < klen; q++) *p++ = IN[ko + q];
+      }
+      *p++ = PR_PROP;
+      p = pk_uleb(p, (uint64_t)pk_c);
+      p = pk_uleb(p, (uint64_t)pk_a);
+      pk_value(p, vt, vdt, v0, v1, pv_has_bytes(vt) ? IN + v0 : nullptr);
+    }
+    if (vis) {
+      if (start && run >= 2) {
+        *p++ = PR_MULTI;
+        p = pk_uleb(p, (uint64_t)idx);
+        p = pk_uleb(p, (uint64_t)k_idc);
+        p = pk_uleb(p, (uint64_t)k_ida);
+        p = pk_uleb(p, mdt);
+        p = pk_uleb(p, run);
+      } else if (start) {
+        *p++ = PR_INSERT;
+        p = pk_uleb(p, (uint64_t)idx);
+        p = pk_uleb(p, (uint64_t)k_idc);
+        p = pk_uleb(p, (uint64_t)k_ida);
+        p = pk_uleb(p, (uint64_t)k_idc);
+        p = pk_uleb(p, (uint64_t)k_ida);
+      }
+      pk_value(p, ivt, idt, iv0, iv1, pv_has_bytes(ivt) ? IN + iv0 : nullptr);
+    }
+  }
+  if (l == 0) {
+    PatchHdr2 h;
+    h.magic = AM_PATCH_MAGIC; h.status = 0; h.arg0 = 0; h.arg1 = 0; h.max_op = mx; h.nbytes = base; h.meta_bytes = 0;
+    *reinterpret_cast<PatchHdr2*>(out) = h;
+  }
+  return true;
+}
+
 }  // namespace fastdoc
 
 // registers for three waves per SIMD (<= 168 VGPRs): with the LDS slice of a C4 document (~13 KB)
@@ -1883,7 +2173,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   FD_CHECK();
   // the row values fast_diff reads after the encode, parked in misc tables the merge is done with
   // (registers would stay live through the encode and spill)
-  if (kDiff && b.P == 2) {
+  if (kDiff && b.P) {
     const FdRec P = fd_rec(M);
     if (isrow) {
       P.key[l] = (uint32_t)r_key; P.objc[l] = r_objc; P.idc[l] = r_idc; P.vlen[l] = r_vlen;
@@ -2126,10 +2416,13 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     }
   }
   FPH(13);
-  if (!kDiff && b.P == 2) return;  // launched without the patch writer: k_doc replays the patch
+  if (!kDiff && b.P) return;  // launched without the patch writers: k_doc writes the log
   if (kDiff && b.P == 2 && !fast_diff(IN, S + F.cells, F.cells_cap, wsg + L.pwire, L.pwire_cap, M, R, nb, NOUT, NA, NC, nbc, N,
                                      OUTC, OUTA, RO, chh))
     return;  // outside the shapes fast_diff covers: k_doc replays the patch (am_diff.h)
+  if (kDiff && b.P == 1 && !fast_getpatch(IN, S + F.cells, F.cells_cap, wsg + L.pwire, L.pwire_cap, M, NOUT, NSUCC, NA, NC, nbc,
+                                          N, OUTC, OUTA, RO, chh))
+    return;  // outside the shapes fast_getpatch covers: k_doc writes the log (P7, am_patch.h)
   FPH(14);
   if (l < N) chg_state[dd.chg_begin + l] = (int32_t)l;
   if (l == 0) {

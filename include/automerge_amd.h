@@ -273,7 +273,8 @@ int am_pipe_submit(am_pipe *p, const uint8_t *arena, uint64_t arena_len, const a
 int am_pipe_drain(am_pipe *p, uint64_t *totals, uint32_t cap, am_error *err);
 /* The same chain for a batch already resident in device memory (the bench's HBM-resident job):
  * d_arena (arena_len + 64 readable bytes), d_chunks, d_docs and the outputs are device pointers;
- * any_diff: some document asks for the applyChanges patch. Merged documents, patch logs and
+ * any_diff: some document asks for a patch log (AM_DOC_WANT_DIFF or AM_DOC_WANT_PATCH: the launch
+ * then carries k_doc_fast's patch writers). Merged documents, patch logs and
  * summaries are compacted into d_out / d_patches / d_summary (layout of am_pipe_submit) and their
  * two arena totals into d_totals; nothing crosses the host link and the call does not wait.
  * am_pipe_resident_sync waits for the stream; ms2 = the chains / document kernels of the resident

@@ -253,3 +253,51 @@ def test_fast_and_general_patch_writers_agree(docs, objmeta):
     bad = [i for i in range(len(items)) if pf[i] != pg[i] or of[i] != og[i] or rf[i]["status"] != rg[i]["status"]]
     assert not bad, (int(flags.sum()), bad[:10])
     print("fast patch writer took %d of %d documents" % (int(flags.sum()), len(items)))
+
+
+def test_fast_and_general_getpatch_writers_agree(docs, objmeta):
+    """getPatch logs (documentPatch, new.js:1604-1635) from k_doc_fast's wave-parallel writer
+    (fast_getpatch, am_doc_fast.h) against k_doc's serial patch_scan (P7, am_patch.h): every saved
+    golden state and seeded C4 / C2 documents merged and staged with WANT_PATCH, once with the fast
+    kernel and once without it (AM_FAST=0). Logs, merged documents and statuses must be equal, and
+    the fast writer must take every C4 and C2 document."""
+    import os
+    from automerge_amd import patch as P
+    import workload
+    from automerge_amd.batch import WANT_PATCH, Batch
+    items = []
+    for sc in docs + objmeta:
+        for res in sc["results"]:
+            if "save" in res:
+                items.append((bytes.fromhex(res["save"]), []))
+    nw = 600
+    for kind, first in (("c4", 21), ("c2", 9)):
+        arena, chunks, dd, _ = getattr(workload, kind)(first, nw)
+        items += [workload.doc_chunks(arena, chunks, dd, i) for i in range(nw)]
+
+    def run(fast):
+        old = os.environ.get("AM_FAST")
+        os.environ["AM_FAST"] = "1" if fast else "0"
+        try:
+            b = Batch()
+            b.stage_docs(items, flags=WANT_PATCH)
+        finally:
+            if old is None:
+                del os.environ["AM_FAST"]
+            else:
+                os.environ["AM_FAST"] = old
+        b.run()
+        b.sync()
+        r = b.results()
+        pats = [_jsonable(P.materialize(b.doc_patch(i), [], 0)) if r[i]["status"] == 0 else None for i in range(len(items))]
+        outs = [b.doc_output(i, r[i]) if r[i]["status"] == 0 else b"" for i in range(len(items))]
+        return r, pats, outs, b.fast_flags()
+
+    rf, pf, of, flags = run(True)
+    rg, pg, og, gflags = run(False)
+    assert not gflags.any()
+    assert flags[-2 * nw:-nw].all(), "every C4 document must take the fast getPatch writer"
+    assert flags[-nw:].all(), "every C2 document (counters) must take the fast getPatch writer"
+    bad = [i for i in range(len(items)) if pf[i] != pg[i] or of[i] != og[i] or rf[i]["status"] != rg[i]["status"]]
+    assert not bad, (int(flags.sum()), bad[:10])
+    print("fast getPatch writer took %d of %d documents" % (int(flags.sum()), len(items)))
