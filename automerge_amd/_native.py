@@ -98,6 +98,7 @@ _sigs = {
     "am_batch_workspace_bytes": (C.c_uint64, [P]),
     "am_batch_kernel_info": (C.c_int, [P, P]),
     "am_batch_doc_plan": (C.c_int, [P, C.c_uint32, P]),
+    "am_batch_fast_slices": (C.c_int, [P, P]),
     "am_batch_digest": (C.c_int, [P, C.c_uint64, C.POINTER(C.c_uint64)]),
     "am_batch_fast_flags": (C.c_int, [P, P]),
     "am_doc_init": (P, [P]),

@@ -729,6 +729,19 @@ extern "C" int am_batch_doc_plan(am_batch* b, uint32_t doc, uint64_t* out10) {
   return 0;
 }
 
+// k_doc_fast LDS slice of every document of the staged batch (diagnostics): out[doc] =
+// fast_layout(...).total, 0 when the document is outside the fast kernel's envelope
+extern "C" int am_batch_fast_slices(am_batch* b, uint32_t* out) {
+  if (!set_device(b->eng)) return 1;
+  std::vector<DocBounds> db(b->ndocs);
+  std::vector<am_doc_desc> dd(b->ndocs);
+  if (b->ndocs && (hipMemcpy(db.data(), b->bounds.p, sizeof(DocBounds) * b->ndocs, hipMemcpyDeviceToHost) != hipSuccess ||
+                   hipMemcpy(dd.data(), b->docs.p, sizeof(am_doc_desc) * b->ndocs, hipMemcpyDeviceToHost) != hipSuccess))
+    return 1;
+  am_fast_slices_host(db.data(), dd.data(), b->ndocs, out);
+  return 0;
+}
+
 // =============================================================================================
 // pipelined batches (am_pipe_*): H2D of batch k+1 and D2H of batch k-1 overlap the kernels of k
 // =============================================================================================

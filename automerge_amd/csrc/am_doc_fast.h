@@ -1334,7 +1334,9 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
                int32_t* __restrict__ chg_state, uint8_t* __restrict__ fast_done) {
   using namespace fastdoc;
   const uint32_t l = lane();
-  const uint32_t doc = blockIdx.x * FD_DOCS_PER_WG + (threadIdx.x >> 6);
+  // wave-uniform by construction: readfirstlane tells the compiler, so the document's descriptors,
+  // bounds and layout live in scalar registers and scalar loads fetch them
+  const uint32_t doc = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * FD_DOCS_PER_WG + (threadIdx.x >> 6)));
   if (doc >= ndocs) return;
 #ifdef AM_PHASE_CLOCK
   uint64_t ph_last = clock64();
@@ -1793,15 +1795,20 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   };
   // type-uniform rounds: lanes take (source, column) pairs of one decoder type at a time
   {
-    constexpr uint8_t kU[9] = {OC_OBJ_ACTOR, OC_OBJ_CTR, OC_KEY_ACTOR, OC_ID_ACTOR, OC_ACTION, OC_VAL_LEN,
-                               OC_CHLD_ACTOR, OC_GRP_NUM, OC_GRP_ACTOR};
-    constexpr uint8_t kD[4] = {OC_KEY_CTR, OC_ID_CTR, OC_CHLD_CTR, OC_GRP_CTR};
+    // the column lists as nibbles of one constant (a lane's column is a shift, not a table load)
+    constexpr uint64_t kU = (uint64_t)OC_OBJ_ACTOR | (uint64_t)OC_OBJ_CTR << 4 | (uint64_t)OC_KEY_ACTOR << 8 |
+                            (uint64_t)OC_ID_ACTOR << 12 | (uint64_t)OC_ACTION << 16 | (uint64_t)OC_VAL_LEN << 20 |
+                            (uint64_t)OC_CHLD_ACTOR << 24 | (uint64_t)OC_GRP_NUM << 28 | (uint64_t)OC_GRP_ACTOR << 32;
+    constexpr uint32_t kD = (uint32_t)OC_KEY_CTR | (uint32_t)OC_ID_CTR << 4 | (uint32_t)OC_CHLD_CTR << 8 |
+                            (uint32_t)OC_GRP_CTR << 12;
+    static_assert(OC_NCOLS <= 16, "op column ids fit a nibble");
     uint32_t off, len, n;
     int32_t* dst;
     for (uint32_t it = l; it < nsrc * 9; it += 64)
-      if (stream(it / 9, kU[it % 9], off, len, n, dst)) d32_stream<DT_UINT>(IN, off, len, n, dst, bad);
+      if (stream(it / 9, (uint32_t)(kU >> (4 * (it % 9))) & 15u, off, len, n, dst))
+        d32_stream<DT_UINT>(IN, off, len, n, dst, bad);
     for (uint32_t it = l; it < nsrc * 4; it += 64)
-      if (stream(it / 4, kD[it % 4], off, len, n, dst)) d32_stream<DT_DELTA>(IN, off, len, n, dst, bad);
+      if (stream(it >> 2, (kD >> (4 * (it & 3))) & 15u, off, len, n, dst)) d32_stream<DT_DELTA>(IN, off, len, n, dst, bad);
     for (uint32_t it = l; it < nsrc * 2; it += 64) {
       const uint32_t s2 = it >> 1;
       if (it & 1) { if (stream(s2, OC_INSERT, off, len, n, dst)) d32_stream<DT_BOOL>(IN, off, len, n, dst, bad); }

@@ -1227,7 +1227,7 @@ __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restric
   }
   __syncthreads();
   // LDS mode: the hot set fits and the input span is contiguous (chunks of a scattered document
-  // are read from the arena by the global mode; k_max_hot forces that launch)
+  // are read from the arena by the global mode; k_bounds forces that launch)
   if ((s.L.hot_total <= lds_bytes && !doc_scattered(s.b)) != kHotLds) return;  // the other mode's document
   const WsLayout& L = s.L;
   if (s.status) goto done;

@@ -620,61 +620,6 @@ __global__ void __launch_bounds__(256) k_chunks(const uint8_t* __restrict__ aren
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// k_bounds: one thread per document -> workspace bounds
-// ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_bounds(const uint8_t* __restrict__ arena, const am_doc_desc* __restrict__ docs, uint32_t ndocs,
-                                                const am_chunk_desc* __restrict__ chunks, const ChunkInfo* __restrict__ info,
-                                                DocBounds* __restrict__ bounds, uint64_t* __restrict__ ws_bytes) {
-  uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= ndocs) return;
-  am_doc_desc dd = docs[d];
-  DocBounds b;
-  uint64_t R = 0, E = 0, C = 0, D = 0, A = 0, H = 0, S = 0, B = 0, AM = 0, ND = 0, UC = 0, UV = 0;
-  uint64_t lo = ~0ull, hi = 0;
-  if (dd.base_chunk >= 0) {
-    const ChunkInfo& ci = info[dd.base_chunk];
-    R += ci.nops; E += ci.nents; C += ci.nchg; D += ci.ndeps; A += ci.nactors; H += ci.nheads;
-    S += ci.strbytes; B += chunks[dd.base_chunk].len;
-    if (ci.nunk && !ci.status) {
-      const uint64_t ub = unknown_bound(arena + chunks[dd.base_chunk].off + ci.data_off, ci.data_len, true, ci.nunk, ci.nops);
-      UC += ci.nunk;
-      // a malformed unknown column: a row-sized bound, k_doc's decode reports the error itself
-      UV += (ub >> 32) ? (uint64_t)(ci.nunk + 3) * ci.nops : (uint32_t)ub;
-    }
-    lo = chunks[dd.base_chunk].off;
-    hi = lo + chunks[dd.base_chunk].len;
-  }
-  for (uint32_t k = 0; k < dd.chg_count; k++) {
-    const ChunkInfo& ci = info[dd.chg_begin + k];
-    const am_chunk_desc cd = chunks[dd.chg_begin + k];
-    R += ci.nops; E += ci.nents; C += 1; D += ci.ndeps; A += 1; H += 1; S += ci.strbytes;
-    B += cd.len;
-    if (ci.nunk && !ci.status) {
-      const uint64_t ub = unknown_bound(arena + cd.off + ci.data_off, ci.data_len, false, ci.nunk, ci.nops);
-      UC += ci.nunk;
-      UV += (ub >> 32) ? (uint64_t)(ci.nunk + 3) * ci.nops : (uint32_t)ub;
-    }
-    AM += ci.nactors;
-    ND += ci.ndeps;
-    if (cd.off < lo) lo = cd.off;
-    if (cd.off + cd.len > hi) hi = cd.off + cd.len;
-  }
-  if (hi < lo) lo = hi = 0;
-  // chunks of one document are normally adjacent; a scattered document is not staged in LDS
-  if (hi - lo > 2 * B + 64) hi = lo;
-  const uint64_t cap = 0x3fffffffull;
-  if (R > cap || E > cap || C > cap || D > cap || AM > cap || ND > cap || UV > cap) { R = E = C = D = AM = ND = UC = UV = 0; A = H = 0; S = B = 0; lo = hi = 0; }
-  b.R = (uint32_t)R; b.E = (uint32_t)E; b.C = (uint32_t)C; b.D = (uint32_t)D; b.A = (uint32_t)A;
-  b.H = (uint32_t)H; b.N = dd.chg_count; b.K = (uint32_t)(H + dd.known_count); b.AM = (uint32_t)AM;
-  b.ND = (uint32_t)ND; b.S = S; b.B = B; b.span_lo = lo; b.span_hi = hi;
-  b.P = (dd.flags & AM_DOC_WANT_PATCH) ? 1u : (dd.flags & AM_DOC_WANT_DIFF) ? 2u : 0u;
-  b.U = ((dd.flags & AM_DOC_FIX_UTF8) ? 1u : 0u) | ((dd.flags & AM_DOC_PATCH_ROOM) ? 2u : 0u);
-  b.UC = (uint32_t)UC; b.UV = (uint32_t)UV;
-  WsLayout L = ws_layout(b);
-  bounds[d] = b;
-  ws_bytes[d] = L.total;
-}
 
 // ------------------------------------------------------------------------------------------
 // Exclusive scan of u64 (three kernels: per-block, block totals, add)
@@ -840,6 +785,85 @@ constexpr uint32_t kDocT = DOC_T_GLB;
 #include "am_doc_fast.h"
 #include "am_hist_dev.h"
 
+void am_fast_slices_host(const DocBounds* db, const am_doc_desc* dd, uint32_t n, uint32_t* out) {
+  for (uint32_t d = 0; d < n; d++) out[d] = fast_eligible(db[d], dd[d]) ? fast_layout(db[d], dd[d].known_count).total : 0u;
+}
+
+// ------------------------------------------------------------------------------------------
+// k_bounds: one thread per document -> workspace bounds
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_bounds(const uint8_t* __restrict__ arena, const am_doc_desc* __restrict__ docs, uint32_t ndocs,
+                                                const am_chunk_desc* __restrict__ chunks, const ChunkInfo* __restrict__ info,
+                                                DocBounds* __restrict__ bounds, uint64_t* __restrict__ ws_bytes,
+                                                uint64_t* __restrict__ max_hot) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t h = 0, f = 0;  // k_doc hot set; k_doc_fast LDS slice (0: outside its envelope)
+  if (d < ndocs) {
+  am_doc_desc dd = docs[d];
+  DocBounds b;
+  uint64_t R = 0, E = 0, C = 0, D = 0, A = 0, H = 0, S = 0, B = 0, AM = 0, ND = 0, UC = 0, UV = 0;
+  uint64_t lo = ~0ull, hi = 0;
+  if (dd.base_chunk >= 0) {
+    const ChunkInfo& ci = info[dd.base_chunk];
+    R += ci.nops; E += ci.nents; C += ci.nchg; D += ci.ndeps; A += ci.nactors; H += ci.nheads;
+    S += ci.strbytes; B += chunks[dd.base_chunk].len;
+    if (ci.nunk && !ci.status) {
+      const uint64_t ub = unknown_bound(arena + chunks[dd.base_chunk].off + ci.data_off, ci.data_len, true, ci.nunk, ci.nops);
+      UC += ci.nunk;
+      // a malformed unknown column: a row-sized bound, k_doc's decode reports the error itself
+      UV += (ub >> 32) ? (uint64_t)(ci.nunk + 3) * ci.nops : (uint32_t)ub;
+    }
+    lo = chunks[dd.base_chunk].off;
+    hi = lo + chunks[dd.base_chunk].len;
+  }
+  for (uint32_t k = 0; k < dd.chg_count; k++) {
+    const ChunkInfo& ci = info[dd.chg_begin + k];
+    const am_chunk_desc cd = chunks[dd.chg_begin + k];
+    R += ci.nops; E += ci.nents; C += 1; D += ci.ndeps; A += 1; H += 1; S += ci.strbytes;
+    B += cd.len;
+    if (ci.nunk && !ci.status) {
+      const uint64_t ub = unknown_bound(arena + cd.off + ci.data_off, ci.data_len, false, ci.nunk, ci.nops);
+      UC += ci.nunk;
+      UV += (ub >> 32) ? (uint64_t)(ci.nunk + 3) * ci.nops : (uint32_t)ub;
+    }
+    AM += ci.nactors;
+    ND += ci.ndeps;
+    if (cd.off < lo) lo = cd.off;
+    if (cd.off + cd.len > hi) hi = cd.off + cd.len;
+  }
+  if (hi < lo) lo = hi = 0;
+  // chunks of one document are normally adjacent; a scattered document is not staged in LDS
+  if (hi - lo > 2 * B + 64) hi = lo;
+  const uint64_t cap = 0x3fffffffull;
+  if (R > cap || E > cap || C > cap || D > cap || AM > cap || ND > cap || UV > cap) { R = E = C = D = AM = ND = UC = UV = 0; A = H = 0; S = B = 0; lo = hi = 0; }
+  b.R = (uint32_t)R; b.E = (uint32_t)E; b.C = (uint32_t)C; b.D = (uint32_t)D; b.A = (uint32_t)A;
+  b.H = (uint32_t)H; b.N = dd.chg_count; b.K = (uint32_t)(H + dd.known_count); b.AM = (uint32_t)AM;
+  b.ND = (uint32_t)ND; b.S = S; b.B = B; b.span_lo = lo; b.span_hi = hi;
+  b.P = (dd.flags & AM_DOC_WANT_PATCH) ? 1u : (dd.flags & AM_DOC_WANT_DIFF) ? 2u : 0u;
+  b.U = ((dd.flags & AM_DOC_FIX_UTF8) ? 1u : 0u) | ((dd.flags & AM_DOC_PATCH_ROOM) ? 2u : 0u);
+  b.UC = (uint32_t)UC; b.UV = (uint32_t)UV;
+  WsLayout L = ws_layout(b);
+  bounds[d] = b;
+  ws_bytes[d] = L.total;
+  // a scattered document needs the global-mode launch: report a hot set above any LDS budget
+  h = doc_scattered(b) ? (1ull << 40) : L.hot_total;
+  if (fast_eligible(b, dd)) f = fast_layout(b, dd.known_count).total;
+  }
+  // max_hot[0]: largest k_doc hot working set; max_hot[1]: largest k_doc_fast LDS slice -- one
+  // atomic per wave
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t h2 = __shfl_xor(h, o, 64), f2 = __shfl_xor(f, o, 64);
+    h = h2 > h ? h2 : h;
+    f = f2 > f ? f2 : f;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (h) atomicMax(reinterpret_cast<unsigned long long*>(max_hot), (unsigned long long)h);
+    if (f) atomicMax(reinterpret_cast<unsigned long long*>(max_hot + 1), (unsigned long long)f);
+  }
+}
+
+
 // ------------------------------------------------------------------------------------------
 // k_compact: workgroup per document copies its merged chunk into the dense output arena
 // k_out_hash: thread per document computes the container checksum (columnar.js:659-686)
@@ -900,31 +924,6 @@ static_assert(sizeof(ChgHdr) <= AM_SZ_CHGHDR, "ChgHdr");
 
 size_t am_scan_tmp_elems(uint32_t n) { return (n + SCAN_T - 1) / SCAN_T + 1; }
 
-// max_hot[0]: largest k_doc hot working set; max_hot[1]: largest k_doc_fast LDS slice (0: none)
-__global__ void __launch_bounds__(256) k_max_hot(const DocBounds* __restrict__ bounds, const am_doc_desc* __restrict__ docs,
-                                                 uint32_t ndocs, uint64_t* __restrict__ max_hot) {
-  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t h = 0, f = 0;
-  if (d < ndocs) {
-    const DocBounds b = bounds[d];
-    const WsLayout L = ws_layout(b);
-    // a scattered document needs the global-mode launch: report a hot set above any LDS budget
-    h = doc_scattered(b) ? (1ull << 40) : L.hot_total;
-    const am_doc_desc dd = docs[d];
-    if (fast_eligible(b, dd)) f = fast_layout(b, dd.known_count).total;
-  }
-  // one atomic per wave (not per document: 65536 on one address serialize)
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t h2 = __shfl_xor(h, o, 64), f2 = __shfl_xor(f, o, 64);
-    h = h2 > h ? h2 : h;
-    f = f2 > f ? f2 : f;
-  }
-  if ((threadIdx.x & 63) == 0) {
-    if (h) atomicMax(reinterpret_cast<unsigned long long*>(max_hot), (unsigned long long)h);
-    if (f) atomicMax(reinterpret_cast<unsigned long long*>(max_hot + 1), (unsigned long long)f);
-  }
-}
 
 void am_launch_chunks(const BatchDev& b, hipStream_t s) {
   if (!b.nchunks) return;
@@ -980,8 +979,7 @@ void am_launch_bounds(const BatchDev& b, hipStream_t s) {
   if (!b.ndocs) return;
   (void)hipMemsetAsync(b.max_hot, 0, 2 * sizeof(uint64_t), s);
   hipLaunchKernelGGL(k_bounds, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, b.arena, b.docs, b.ndocs, b.chunks, b.info, b.bounds,
-                     b.ws_bytes);
-  hipLaunchKernelGGL(k_max_hot, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, b.bounds, b.docs, b.ndocs, b.max_hot);
+                     b.ws_bytes, b.max_hot);
   uint32_t nblk = (b.ndocs + SCAN_T - 1) / SCAN_T;
   hipLaunchKernelGGL(k_scan_blocks, dim3(nblk), dim3(SCAN_T), 0, s, b.ws_bytes, b.ws_off, b.scan_tmp, b.ndocs);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, b.scan_tmp, nblk, b.ws_total);

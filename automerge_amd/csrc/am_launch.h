@@ -37,6 +37,8 @@ struct BatchDev {
 };
 
 void am_launch_chunks(const BatchDev& b, hipStream_t s);
+// diagnostics: k_doc_fast LDS slice per document (0: outside its envelope)
+void am_fast_slices_host(const DocBounds* db, const am_doc_desc* dd, uint32_t n, uint32_t* out);
 void am_launch_chunk_hashes(const ChunkInfo* info, uint32_t n, uint8_t* out32, hipStream_t s);
 void am_launch_bounds(const BatchDev& b, hipStream_t s);   // k_bounds + scan of ws bytes
 void am_launch_doc(const BatchDev& b, hipStream_t s);

@@ -227,6 +227,8 @@ int am_batch_kernel_info(am_batch *b, uint64_t *out3);
 /* Workspace plan of one staged document (diagnostics, not part of the reference interface):
  * R, E, P, hot set, workspace bytes, workspace offset, span_lo, span_hi, runs-from-LDS, input bytes. */
 int am_batch_doc_plan(am_batch *b, uint32_t doc, uint64_t *out10);
+/* Diagnostics: the k_doc_fast LDS slice of every staged document (0 = outside its envelope). */
+int am_batch_fast_slices(am_batch *b, uint32_t *out);
 
 /* ---- pipelined batches: the whole job from host memory to host memory ----
  * A stream of batches (each = many documents, one Backend.load + Backend.applyChanges per document,
