@@ -151,6 +151,7 @@ _sigs = {
     "am_sync_encode_state": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
     "am_sync_decode_state": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(u8p), C.POINTER(C.c_size_t), C.POINTER(Error)]),
     "am_doc_load_batch": (C.c_int, [P, C.c_size_t, P, P, P, P, P]),
+    "am_stage_documents": (C.c_int, [P, C.c_size_t, P, P, P, P, P, P, P]),
     "am_doc_apply_changes_batch": (C.c_int, [C.c_size_t, P, P, P, P, P, P, P, P, P]),
     "am_doc_get_patch_batch": (C.c_int, [C.c_size_t, P, P, P, P, P, P]),
     "am_doc_save_batch": (C.c_int, [C.c_size_t, P, P, P, P, P]),
@@ -264,6 +265,35 @@ def stage_document(data, device=0):
     b = C.string_at(out, n.value)
     lib.am_free(out)
     return b, bool(v.value)
+
+
+def stage_documents(datas, device=0):
+    """stage_document over many documents in one call (am_stage_documents: one GPU checksum batch,
+    one GPU inflate batch): a list of (bytes, checksum_already_verified); raises the first error."""
+    datas = [bytes(d) for d in datas]
+    n = len(datas)
+    if n == 0:
+        return []
+    bufs = (C.c_char_p * n)(*datas)
+    lens = (C.c_size_t * n)(*[len(d) for d in datas])
+    outs = (u8p * n)()
+    olens = (C.c_size_t * n)()
+    ver = (C.c_uint8 * n)()
+    codes = (C.c_uint32 * n)()
+    msgs = (C.c_void_p * n)()
+    lib.am_stage_documents(engine(device), n, bufs, lens, outs, olens, ver, codes, msgs)
+    errs = batch_errors(n, codes, msgs)
+    res = []
+    for i in range(n):
+        if outs[i]:
+            res.append((C.string_at(outs[i], olens[i]), bool(ver[i])))
+            lib.am_free(outs[i])
+        else:
+            res.append(None)
+    for e in errs:
+        if e is not None:
+            raise e
+    return res
 
 
 def inflate_raw(buffers, device=0):

@@ -26,16 +26,19 @@ WANT_DIFF = 4   # AM_DOC_WANT_DIFF: also write the patch applyChanges returns
 def pack(docs, device=0, flags=0):
     """docs: iterable of (base_bytes | None, [change bytes]) -> (arena, chunks, docdescs).
     Compressed change chunks (type 2) are inflated on the GPU when the batch is staged
-    (am_inflate.hip); base documents with DEFLATEd columns go through am_stage_document.
+    (am_inflate.hip); base documents with DEFLATEd columns go through am_stage_documents (one batch).
     flags: WANT_PATCH or WANT_DIFF for every document."""
     parts, chunks, descs = [], [], []
     off = 0
+    docs = list(docs)
+    # every base document's DEFLATEd columns in one GPU checksum + inflate batch
+    staged = iter(N.stage_documents([b for b, _ in docs if b], device))
     for base, changes in docs:
         d = np.zeros((), DOC_DT)
         d["base_chunk"] = -1
         changes = [bytes(c) for c in changes]
         if base:
-            base, verified = N.stage_document(base, device)
+            base, verified = next(staged)
             d["base_chunk"] = len(chunks)
             chunks.append((off, len(base), 1 if verified else 0))
             parts.append(base)

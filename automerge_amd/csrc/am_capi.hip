@@ -1592,6 +1592,98 @@ bool stage_doc(am_engine* e, const std::vector<uint8_t>& in, std::vector<uint8_t
   return true;
 }
 
+// stage_doc over n documents with one GPU checksum batch and one inflate batch for every
+// DEFLATEd column of every document (inflateColumn, columnar.js:1062-1068): out[i] is the staged
+// chunk (the input itself when it has no compressed column), errs[i].code != 0 on failure.
+void stage_docs(am_engine* e, size_t n, const uint8_t* const* data, const size_t* lens, std::vector<std::vector<uint8_t>>& out,
+                std::vector<uint8_t>& verified, std::vector<Err>& errs) {
+  out.assign(n, {});
+  verified.assign(n, 0);
+  errs.assign(n, Err{});
+  struct Zd {
+    DocParts parts;
+    uint64_t end = 0;
+    bool z = false;
+  };
+  std::vector<Zd> zd(n);
+  am_par_for(n, [&](size_t i) {
+    const uint8_t* in = data[i];
+    const size_t len = lens[i];
+    Container c;
+    Zd& z = zd[i];
+    if (len < 4 || std::memcmp(in, "\x85\x6f\x4a\x83", 4) != 0 || !read_container(in, len, c) || c.type != 0 ||
+        !split_doc(in + c.data_off, c.data_len, z.parts)) {
+      out[i].assign(in, in + len);  // let the GPU report the exact error
+      return;
+    }
+    for (auto* cols : {&z.parts.ccols, &z.parts.ocols})
+      for (auto& col : *cols) z.z |= (col.id & COL_DEFLATE) != 0;
+    if (!z.z) { out[i].assign(in, in + len); z.parts = DocParts{}; return; }
+    z.end = c.end;
+  });
+  std::vector<size_t> zi;
+  for (size_t i = 0; i < n; i++)
+    if (zd[i].z) zi.push_back(i);
+  if (zi.empty()) return;
+  // checksums of the compressed chunks (one k_chunks-style SHA batch)
+  std::vector<std::vector<uint8_t>> whole(zi.size());
+  std::vector<const std::vector<uint8_t>*> wp(zi.size());
+  for (size_t k = 0; k < zi.size(); k++) {
+    whole[k].assign(data[zi[k]] + 8, data[zi[k]] + zd[zi[k]].end);
+    wp[k] = &whole[k];
+  }
+  std::vector<std::array<uint8_t, 32>> hh;
+  if (!gpu_sha256(e, wp, 0, hh)) {
+    for (size_t i : zi) errs[i] = {AM_U_CAPACITY, false, "automerge_amd: GPU hash failed"};
+    return;
+  }
+  std::vector<std::vector<uint8_t>*> zcol;
+  std::vector<uint64_t*> zid;
+  std::vector<const uint8_t*> zb;
+  std::vector<size_t> zl, zdoc;
+  for (size_t k = 0; k < zi.size(); k++) {
+    const size_t i = zi[k];
+    if (std::memcmp(hh[k].data(), data[i] + 4, 4) != 0) {
+      errs[i] = {AM_E_CHECKSUM, false, message_for(AM_E_CHECKSUM, 0, 0, "")};
+      continue;
+    }
+    for (auto* cols : {&zd[i].parts.ccols, &zd[i].parts.ocols})
+      for (auto& col : *cols)
+        if (col.id & COL_DEFLATE) {
+          zcol.push_back(&col.data);
+          zid.push_back(&col.id);
+          zb.push_back(col.data.data());
+          zl.push_back(col.data.size());
+          zdoc.push_back(i);
+        }
+  }
+  const size_t nz = zb.size();
+  std::vector<uint8_t*> zo(nz, nullptr);
+  std::vector<size_t> zn(nz, 0);
+  std::vector<uint8_t> zok(nz, 0);
+  am_error ae;
+  if (nz && am_inflate_raw(e, zb.data(), zl.data(), nz, zo.data(), zn.data(), zok.data(), &ae)) {
+    for (size_t i : zi)
+      if (!errs[i].code) errs[i] = {AM_U_CAPACITY, false, ae.message};
+    return;
+  }
+  for (size_t q = 0; q < nz; q++) {
+    if (zok[q]) {
+      zcol[q]->assign(zo[q], zo[q] + zn[q]);
+      *zid[q] ^= COL_DEFLATE;
+    } else if (!errs[zdoc[q]].code) {
+      errs[zdoc[q]] = {AM_E_SUBARRAY, false, "invalid deflate data"};
+    }
+    std::free(zo[q]);
+  }
+  am_par_for(zi.size(), [&](size_t k) {
+    const size_t i = zi[k];
+    if (errs[i].code) return;
+    out[i] = make_chunk(data[i] + 4, 0, join_doc(zd[i].parts));
+    verified[i] = 1;
+  });
+}
+
 }  // namespace
 
 bool am_stage_doc_chunk(am_engine* e, const std::vector<uint8_t>& in, std::vector<uint8_t>& out, bool& verified, am_error* err) {
@@ -1599,6 +1691,14 @@ bool am_stage_doc_chunk(am_engine* e, const std::vector<uint8_t>& in, std::vecto
   if (stage_doc(e, in, out, verified, er)) return true;
   to_c(er, err);
   return false;
+}
+void am_stage_doc_chunks(am_engine* e, size_t n, const uint8_t* const* data, const size_t* lens,
+                         std::vector<std::vector<uint8_t>>& out, std::vector<uint8_t>& verified,
+                         const std::function<am_error*(size_t)>& err_of) {
+  std::vector<Err> E;
+  stage_docs(e, n, data, lens, out, verified, E);
+  for (size_t i = 0; i < n; i++)
+    if (E[i].code) to_c(E[i], err_of(i));
 }
 std::string am_message_for(uint32_t code, int64_t a0, int64_t a1, const std::string& actor) { return message_for(code, a0, a1, actor); }
 
@@ -2066,16 +2166,17 @@ extern "C" int am_doc_compute_hash_graph_batch(size_t n, am_doc* const* docs, ui
 extern "C" int am_doc_load_batch(am_engine* eng, size_t n, const uint8_t* const* data, const size_t* lens, am_doc** docs,
                                  uint32_t* codes, char** msgs) {
   std::vector<Err> E(n);
-  std::vector<std::vector<uint8_t>> staged(n);
+  std::vector<std::vector<uint8_t>> staged;
+  std::vector<uint8_t> ver;
+  stage_docs(eng, n, data, lens, staged, ver, E);
   std::vector<ManyJob> jobs;
   std::vector<size_t> at;
   for (size_t i = 0; i < n; i++) {
     docs[i] = nullptr;
-    bool v = false;
-    if (!stage_doc(eng, std::vector<uint8_t>(data[i], data[i] + lens[i]), staged[i], v, E[i])) continue;
+    if (E[i].code) continue;
     ManyJob j;
     j.base = &staged[i];
-    j.base_verified = v;
+    j.base_verified = ver[i] != 0;
     jobs.push_back(j);
     at.push_back(i);
   }
@@ -2519,6 +2620,27 @@ extern "C" int am_stage_change(const uint8_t* in, size_t len, uint8_t** out, siz
   return 0;
 }
 
+// Host stage of Backend.load over n documents (am_stage_document batched): one GPU checksum batch
+// and one GPU inflate batch for the DEFLATEd columns of all of them. outs[i] (malloc'd) = the staged
+// chunk, verified[i] = 1 when its checksum was verified here; codes[i] / msgs[i] as in
+// am_doc_load_batch. Returns the number that failed.
+extern "C" int am_stage_documents(am_engine* eng, size_t n, const uint8_t* const* data, const size_t* lens, uint8_t** outs,
+                                  size_t* out_lens, uint8_t* verified, uint32_t* codes, char** msgs) {
+  std::vector<std::vector<uint8_t>> st;
+  std::vector<uint8_t> ver;
+  std::vector<Err> E;
+  stage_docs(eng, n, data, lens, st, ver, E);
+  am_par_for(n, [&](size_t i) {
+    outs[i] = nullptr;
+    out_lens[i] = 0;
+    verified[i] = ver[i];
+    if (E[i].code) return;
+    outs[i] = static_cast<uint8_t*>(std::malloc(st[i].size() ? st[i].size() : 1));
+    std::memcpy(outs[i], st[i].data(), st[i].size());
+    out_lens[i] = st[i].size();
+  });
+  return publish(E, codes, msgs);
+}
 extern "C" int am_stage_document(am_engine* eng, const uint8_t* in, size_t len, uint8_t** out, size_t* outlen,
                                  int* verified, am_error* err) {
   Err e;

@@ -147,6 +147,8 @@ using lds_mode::EK_B;
 using lds_mode::EK_W;
 
 __device__ __forceinline__ uint32_t lane() { return threadIdx.x & 63; }
+// a value every lane of the wave holds equally, moved to a scalar register (readfirstlane)
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 // Orders this wave's LDS accesses (a wave's DS instructions execute in order; this stops the
 // compiler from moving them across a cross-lane hand-off)
 __device__ __forceinline__ void wsync() {
@@ -1350,7 +1352,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   const uint64_t wso = ws_off[doc];
   if (wso + L.total > ws_cap) return;  // capacity error: reported by k_doc
   uint8_t* const wsg = ws_base + wso;
-  uint8_t* const S = am_lds + (threadIdx.x >> 6) * lds_per_doc;
+  uint8_t* const S = am_lds + uni(threadIdx.x >> 6) * lds_per_doc;
   uint8_t* const M = S + F.misc;
   const bool has_base = dd.base_chunk >= 0;
   const uint32_t N = dd.chg_count;
@@ -1403,14 +1405,16 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   }
   wsync();
   FD_CHECK();
-  const uint32_t NB = dh->nactors, HB = dh->nheads, K = dd.known_count;
+  // header fields every lane reads: readfirstlane keeps them (and the loops they bound) scalar
+  const uint32_t NB = uni(dh->nactors), HB = uni(dh->nheads), K = dd.known_count;
+  const uint64_t dhb = ((uint64_t)uni((uint32_t)(dh->base >> 32)) << 32) | uni((uint32_t)dh->base);
   bad |= NB + N != b.A || HB + N != b.H;
   FD_CHECK();
   // base heads' changeIndexByHash indexes (new.js:1729-1739); -1 = unknown
   if (l == 0) {
     int64_t* bh = reinterpret_cast<int64_t*>(M + FM_BHIDX);
     if (dh->has_hidx) {
-      Rd r{IN + (dh->base + dh->hidx_off - a0), (uint64_t)1 << 40, 0};
+      Rd r{IN + (dhb + dh->hidx_off - a0), (uint64_t)1 << 40, 0};
       for (uint32_t h = 0; h < HB; h++) {
         int64_t v = -1;
         rd_u53(r, v);
@@ -1430,7 +1434,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   }
   if (l < HB) {
     uint32_t w[8];
-    load32(IN + (dh->base + dh->heads_off + 32 * l - a0), w);
+    load32(IN + (dhb + dh->heads_off + 32 * l - a0), w);
 #pragma unroll
     for (int k = 0; k < 8; k++) HT[8 * (N + l) + k] = w[k];
   }
@@ -1456,11 +1460,11 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   uint32_t* RW = reinterpret_cast<uint32_t*>(S + F.refs);               // 8 words per ref
   uint32_t* RO = reinterpret_cast<uint32_t*>(S + F.refs + 32 * NR);     // (off - a0, len) per ref
   if (l == 0 && has_base) {
-    Rd r{IN + (dh->base + dh->actors_off - a0), (uint64_t)1 << 40, 0};
+    Rd r{IN + (dhb + dh->actors_off - a0), (uint64_t)1 << 40, 0};
     for (uint32_t i = 0; i < NB; i++) {
       int64_t len = 0;
       bad |= rd_u53(r, len) != AM_OK;
-      RO[2 * i] = (uint32_t)(dh->base + dh->actors_off + r.off - a0);
+      RO[2 * i] = (uint32_t)(dhb + dh->actors_off + r.off - a0);
       RO[2 * i + 1] = (uint32_t)len;
       r.off += (uint64_t)len;
     }
@@ -1568,7 +1572,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   int64_t* DCC = reinterpret_cast<int64_t*>(S + F.cells);  // [9][nbc] (+ deps at [9*nbc])
   if (has_base && l < DC_NCOLS) {
     const uint32_t col = l;
-    const uint64_t off = dh->base + dh->ccol_off[col];
+    const uint64_t off = dhb + dh->ccol_off[col];
     const uint32_t len = dh->ccol_len[col];
     ColDec d;
     const uint8_t type = (col == DC_ACTOR || col == DC_DEPS_NUM || col == DC_EXTRA_LEN) ? DT_UINT
@@ -1620,7 +1624,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     const uint32_t xo = excl_add(l < nbc ? bc_xraw : 0u, xt);
     excl_add(l < nbc ? bc_nd : 0u, dt);
     if (has_base) bad |= xt > dh->ccol_len[DC_EXTRA_RAW] || dt != nbd;
-    bc_xoff = (uint32_t)(dh->base + dh->ccol_off[DC_EXTRA_RAW] + xo - a0);
+    bc_xoff = (uint32_t)(dhb + dh->ccol_off[DC_EXTRA_RAW] + xo - a0);
     // clock: seq must count 1, 2, ... per actor in row order (new.js:1654-1660)
     uint32_t before = 0;
     for (uint32_t j = 0; j < nbc; j++) {
@@ -1784,7 +1788,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     const bool chg_src = !(has_base && s == 0);
     if (chg_src && (col == OC_ID_ACTOR || col == OC_ID_CTR)) return false;  // ids from the header
     const uint32_t c = has_base ? s - 1 : s;
-    const uint64_t cbase = chg_src ? chh[c].base : dh->base;
+    const uint64_t cbase = chg_src ? chh[c].base : dhb;
     off = (uint32_t)(cbase - a0) + (chg_src ? chh[c].col_off[col] : dh->ocol_off[col]);
     len = chg_src ? chh[c].col_len[col] : dh->ocol_len[col];
     const uint32_t j = col < OC_VAL_RAW ? col : col - 1;
@@ -1868,7 +1872,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   const uint32_t vsum0 = __shfl(vsum, r_row0 & 63, 64), psum0 = __shfl(r_psoff, r_row0 & 63, 64);
   uint32_t r_voff = 0;  // valRaw bytes of the row, relative to a0
   if (isrow) {
-    const uint64_t cbase = r_chg ? chh[r_c].base : dh->base;
+    const uint64_t cbase = r_chg ? chh[r_c].base : dhb;
     const uint32_t coff = r_chg ? chh[r_c].col_off[OC_VAL_RAW] : dh->ocol_off[OC_VAL_RAW];
     const uint32_t clen = r_chg ? chh[r_c].col_len[OC_VAL_RAW] : dh->ocol_len[OC_VAL_RAW];
     r_voff = (uint32_t)(cbase + coff - a0) + (vsum - vsum0);
@@ -2349,7 +2353,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   FPH(12);
   // trailer: heads indexes (all known here) and the base document's extra bytes
   const uint32_t cols_end = cur;
-  const uint32_t xlen = has_base ? dh->extra_len : 0u;
+  const uint32_t xlen = has_base ? uni((uint32_t)dh->extra_len) : 0u;
   uint32_t hib = 0;
   {
     const int64_t* HIDX = reinterpret_cast<const int64_t*>(M + FM_HIDX);
@@ -2358,7 +2362,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     if (cols_end + hib + xlen > F.cells_cap) bad = true;
     else {
       if (l < NH) put_uleb(OB + cols_end + ho, (uint64_t)HIDX[l]);
-      for (uint32_t q = l; q < xlen; q += 64) OB[cols_end + hib + q] = IN[dh->base + dh->extra_off - a0 + q];
+      for (uint32_t q = l; q < xlen; q += 64) OB[cols_end + hib + q] = IN[dhb + dh->extra_off - a0 + q];
     }
   }
   FD_CHECK();

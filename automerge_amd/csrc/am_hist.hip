@@ -301,16 +301,29 @@ extern "C" int am_document_changes_batch(am_engine* eng, const uint8_t* const* d
   std::vector<std::pair<const uint8_t*, size_t>> src(n);
   std::vector<uint8_t> verified(n, 0);
   std::vector<uint32_t> live;
-  for (size_t i = 0; i < n; i++) {
-    if (plain_columns(docs[i], lens[i])) {
-      src[i] = {docs[i], lens[i]};
-    } else {
-      std::vector<uint8_t> in(docs[i], docs[i] + lens[i]);
-      bool v = false;
-      if (!am_stage_doc_chunk(eng, in, staged[i], v, &out[i].err)) continue;
-      verified[i] = v;
-      src[i] = {staged[i].data(), staged[i].size()};
+  // documents with DEFLATEd columns: one batched stage (GPU checksums + one inflate batch)
+  std::vector<size_t> zi;
+  std::vector<const uint8_t*> zp;
+  std::vector<size_t> zl;
+  std::vector<uint8_t> zbad(n, 0);
+  for (size_t i = 0; i < n; i++)
+    if (!plain_columns(docs[i], lens[i])) { zi.push_back(i); zp.push_back(docs[i]); zl.push_back(lens[i]); }
+  if (!zi.empty()) {
+    std::vector<std::vector<uint8_t>> zs;
+    std::vector<uint8_t> zv;
+    am_stage_doc_chunks(eng, zi.size(), zp.data(), zl.data(), zs, zv, [&](size_t k) {
+      zbad[zi[k]] = 1;
+      return &out[zi[k]].err;
+    });
+    for (size_t k = 0; k < zi.size(); k++) {
+      staged[zi[k]] = std::move(zs[k]);
+      verified[zi[k]] = zv[k];
     }
+  }
+  for (size_t i = 0; i < n; i++) {
+    if (zbad[i]) continue;
+    if (plain_columns(docs[i], lens[i])) src[i] = {docs[i], lens[i]};
+    else src[i] = {staged[i].data(), staged[i].size()};
     live.push_back((uint32_t)i);
   }
   std::vector<DocRun> runs(n);

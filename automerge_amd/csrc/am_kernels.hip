@@ -1133,7 +1133,8 @@ __global__ void __launch_bounds__(256) k_pipe_compact(const am_doc_result* __res
                                                       const uint64_t* __restrict__ plen, const uint64_t* __restrict__ poff,
                                                       uint8_t* __restrict__ dout, uint64_t out_cap, uint8_t* __restrict__ dpatch,
                                                       uint64_t patch_cap, am_doc_summary* __restrict__ summary) {
-  const uint32_t d = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  // wave-uniform document index (readfirstlane): scalar loads of its result and offsets
+  const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6))), l = threadIdx.x & 63;
   if (d >= ndocs) return;
   const am_doc_result r = res[d];
   const uint64_t on = olen[d], oo = ooff[d], pn = plen[d], po = poff[d];

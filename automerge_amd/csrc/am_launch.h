@@ -7,6 +7,7 @@
 #include "am_hist.h"
 
 #include <string>
+#include <functional>
 #include <vector>
 
 struct BatchDev {
@@ -93,4 +94,9 @@ void am_sync_cache_free(void* cache);
 // host stages of am_capi.hip shared with am_hist.hip: Backend.load's staging of a document chunk
 // (DEFLATEd columns inflated, checksum verified), the reference error text of an AM_* code
 bool am_stage_doc_chunk(am_engine* e, const std::vector<uint8_t>& in, std::vector<uint8_t>& out, bool& verified, am_error* err);
+// am_stage_doc_chunk over n documents: one GPU checksum batch and one inflate batch; err_of(i)
+// receives document i's error (out[i] is then empty)
+void am_stage_doc_chunks(am_engine* e, size_t n, const uint8_t* const* data, const size_t* lens,
+                         std::vector<std::vector<uint8_t>>& out, std::vector<uint8_t>& verified,
+                         const std::function<am_error*(size_t)>& err_of);
 std::string am_message_for(uint32_t code, int64_t a0, int64_t a1, const std::string& actor);

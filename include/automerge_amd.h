@@ -446,6 +446,13 @@ void am_free(void *p);
 int am_stage_change(const uint8_t *in, size_t len, uint8_t **out, size_t *outlen, am_error *err);
 int am_stage_document(am_engine *eng, const uint8_t *in, size_t len, uint8_t **out, size_t *outlen, int *verified,
                       am_error *err);
+/* am_stage_document over n documents in one call (reference: load -> inflateColumn,
+ * backend/columnar.js:1062-1068, for every document): one GPU checksum batch and one GPU inflate
+ * batch for the DEFLATEd columns of all of them. outs[i] (free with am_free) / out_lens[i] = the
+ * staged chunk, verified[i] = 1 when its checksum was verified here, codes[i] / msgs[i] as in
+ * am_doc_load_batch. Returns the number of documents that failed. */
+int am_stage_documents(am_engine *eng, size_t n, const uint8_t *const *data, const size_t *lens, uint8_t **outs,
+                       size_t *out_lens, uint8_t *verified, uint32_t *codes, char **msgs);
 
 /* ---- utilities ---- */
 /* Change hash (SHA-256 of the uncompressed chunk) of each change, computed on the GPU. */

@@ -95,3 +95,40 @@ def test_deflated_change_chunks_inflate_in_the_batch_stage():
         for c in chg:
             assert hashes[k].tobytes().hex() == O.change_meta(c)["hash"]
             k += 1
+
+
+def test_stage_documents_batch_equals_per_document_stage():
+    """am_stage_documents (one GPU checksum batch + one inflate batch for every DEFLATEd column of
+    every document, inflateColumn columnar.js:1062-1068) stages each saved document exactly as
+    am_stage_document does one at a time; a corrupted checksum fails that document only."""
+    import oracle_ffi as O
+    import workload as W
+    from automerge_amd import _native as N
+    arena, chunks, docs, _ = W.text(7, 5, 40, 30, 4)
+    saved = []
+    for i in range(len(docs)):
+        _, chg = W.doc_chunks(arena, chunks, docs, i)
+        d = O.Doc.init()
+        d.apply(chg)
+        saved.append(d.save())
+    saved.append(O.Doc.init().save())
+    one = [N.stage_document(s) for s in saved]
+    assert sum(1 for s, (o, _) in zip(saved, one) if o != s) >= len(docs)  # columns were DEFLATEd
+    assert N.stage_documents(saved) == one
+    bad = bytearray(saved[1])
+    bad[5] ^= 0xFF  # checksum byte
+    with pytest.raises(N.AutomergeError):
+        N.stage_documents([saved[0], bytes(bad), saved[2]])
+    codes = (N.C.c_uint32 * 3)()
+    msgs = (N.C.c_void_p * 3)()
+    outs = (N.u8p * 3)()
+    olens = (N.C.c_size_t * 3)()
+    ver = (N.C.c_uint8 * 3)()
+    datas = [saved[0], bytes(bad), saved[2]]
+    nfail = N.lib.am_stage_documents(N.engine(), 3, (N.C.c_char_p * 3)(*datas), (N.C.c_size_t * 3)(*map(len, datas)),
+                                     outs, olens, ver, codes, msgs)
+    errs = N.batch_errors(3, codes, msgs)
+    assert nfail == 1 and errs[0] is None and errs[2] is None and errs[1] is not None
+    assert N.C.string_at(outs[0], olens[0]) == one[0][0] and N.C.string_at(outs[2], olens[2]) == one[2][0]
+    for i in (0, 2):
+        N.lib.am_free(outs[i])
