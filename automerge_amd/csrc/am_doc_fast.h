@@ -1,5 +1,5 @@
 // am_doc_fast.h -- k_doc_fast: the merge of a small document with its op rows, changes, entries
-// and columns held one per lane (one wave per document, four documents per workgroup).
+// and columns held one per lane (one wave per document, one document per workgroup).
 //
 // This is the common case of Backend.load + Backend.applyChanges (backend/new.js:1550-1597,
 // 1695-1871): every change of the call applies in list order during the first pass of the
@@ -51,7 +51,11 @@
 #define FD_MAX 64
 #define FD_SPAN_MAX 8192
 #define FD_LDS_CAP (24 * 1024)
-#define FD_DOCS_PER_WG 4
+// documents (waves) per workgroup: with one, the LDS slices pack per wave, so the occupancy is
+// floor(160 KB / slice) waves per CU (C4, 11.2 KB: 14) instead of whole 4-document groups (12)
+#ifndef FD_DOCS_PER_WG
+#define FD_DOCS_PER_WG 1
+#endif
 #define FD_NULL ((int32_t)0x80000000)
 #define FD_DIFF_SCRATCH 1216  // fast_diff's tables in the cells region
 
@@ -90,12 +94,12 @@ enum : uint32_t {
   FM_OUTA = FM_DEPD + 128,        // uint8 [64] output succ actor
   FM_DOWN = FM_OUTA + 64,         // uint8 [64] owner change of each dep slot
   FM_HSEL = FM_DOWN + 64,         // uint8 [64] hash-table slot of each sorted head
-  FM_HIDX = FM_HSEL + 64,         // int64 [64] sorted heads' indexes
-  FM_TOTAL = FM_HIDX + 512
+  FM_HIDX = FM_HSEL + 64,         // int32 [64] sorted heads' indexes
+  FM_TOTAL = FM_HIDX + 256
 };
 
 struct FastLayout {
-  uint32_t input, hashes, refs, misc, chg, cells, cells_cap, total;
+  uint32_t input, hashes, refs, misc, chg, cells, cells_cap, total, rw;
 };
 
 // Per-document LDS slice of k_doc_fast (bytes, 16-aligned regions).
@@ -105,15 +109,18 @@ __host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t n
   auto take = [&](uint32_t n) { const uint32_t at = o; o += (n + 15) & ~15u; return at; };
   const uint32_t span = (uint32_t)(b.span_hi - b.span_lo);
   const uint32_t nbh = b.H - b.N, nrefs = (b.A - b.N) + b.AM;
+  const uint32_t nht = b.N + nbh + nknown;
   F.input = take(span + 32);
-  F.hashes = take(32 * (b.N + nbh + nknown));
-  F.refs = take(40 * nrefs);  // 32 B padded id words + (off, len)
+  F.refs = take(8 * nrefs);  // (off, len) per ref
   F.misc = take(FM_TOTAL);
   F.chg = take((uint32_t)sizeof(ChgHdrC) * b.N);
   const uint32_t nbc = b.C - b.N, nbd = b.D - b.ND;
   uint32_t cells = 4 * (13 * b.R + 2 * b.E);
-  const uint32_t dcc = 8 * (9 * nbc + nbd);
-  if (dcc > cells) cells = dcc;
+  // until the op columns are decoded the cells region holds the hash table (changes | base heads |
+  // known), then the refs' 32 B id words (actor table) and later the base change rows over them
+  const uint32_t dcc = 8 * (9 * nbc + nbd), rwb = 32 * nrefs;
+  const uint32_t early = 32 * nht + (dcc > rwb ? dcc : rwb);
+  if (early > cells) cells = early;
   // output image: header (actors, heads, column table) + columns + heads indexes + extra bytes
   // (a larger image fails the encoder's capacity check: the document then goes to k_doc)
   const uint32_t out = 64 + 40 * b.A + 42 * b.H + 25 * 12 + span;
@@ -121,6 +128,8 @@ __host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t n
   if (b.P && cells < FD_DIFF_SCRATCH) cells = FD_DIFF_SCRATCH;  // fast_diff's / fast_getpatch's tables
   F.cells = take(cells);
   F.cells_cap = cells;
+  F.hashes = F.cells;
+  F.rw = F.cells + 32 * nht;
   F.total = o;
   return F;
 }
@@ -1316,8 +1325,9 @@ __device__ __forceinline__ bool fast_getpatch(const uint8_t* IN, uint8_t* PS, ui
 
 }  // namespace fastdoc
 
-// registers for three waves per SIMD (<= 168 VGPRs): with the LDS slice of a C4 document (~13 KB)
-// three 4-document workgroups fit a CU. Probe builds may ask for another count (-DAM_FAST_WAVES=n).
+// register budget for at least three waves per SIMD (<= 168 VGPRs; the kernel needs ~85 since its
+// per-document values are scalar): the LDS slice decides the occupancy. Probe builds may ask for
+// another count (-DAM_FAST_WAVES=n).
 #ifndef AM_FAST_WAVES
 #define AM_FAST_WAVES 3
 #endif
@@ -1332,7 +1342,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     k_doc_fast(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks, const am_doc_desc* __restrict__ docs,
                const am_known_hash* __restrict__ known, const ChunkInfo* __restrict__ info,
                const HdrSlot* __restrict__ hdr, const DocBounds* __restrict__ bounds, const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base,
-               uint64_t ws_cap, uint32_t lds_per_doc, uint32_t ndocs, am_doc_result* __restrict__ results,
+               uint64_t ws_cap, uint32_t lds_per_doc, uint32_t lds_floor, uint32_t ndocs, am_doc_result* __restrict__ results,
                int32_t* __restrict__ chg_state, uint8_t* __restrict__ fast_done) {
   using namespace fastdoc;
   const uint32_t l = lane();
@@ -1347,7 +1357,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   const DocBounds b = bounds[doc];
   if (!fast_eligible(b, dd)) return;
   const FastLayout F = fast_layout(b, dd.known_count);
-  if (F.total > lds_per_doc) return;
+  if (F.total > lds_per_doc || F.total <= lds_floor) return;  // another launch's slice class (or k_doc's)
   const WsLayout L = ws_layout(b);
   const uint64_t wso = ws_off[doc];
   if (wso + L.total > ws_cap) return;  // capacity error: reported by k_doc
@@ -1457,8 +1467,8 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   const uint32_t NR = NB + am_total;
   bad |= NR > FD_MAX;
   FD_CHECK();
-  uint32_t* RW = reinterpret_cast<uint32_t*>(S + F.refs);               // 8 words per ref
-  uint32_t* RO = reinterpret_cast<uint32_t*>(S + F.refs + 32 * NR);     // (off - a0, len) per ref
+  uint32_t* RW = reinterpret_cast<uint32_t*>(S + F.rw);    // 8 words per ref (cells region, until the actor table)
+  uint32_t* RO = reinterpret_cast<uint32_t*>(S + F.refs);  // (off - a0, len) per ref
   if (l == 0 && has_base) {
     Rd r{IN + (dhb + dh->actors_off - a0), (uint64_t)1 << 40, 0};
     for (uint32_t i = 0; i < NB; i++) {
@@ -1569,7 +1579,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
 
   FPH(2);
   // ---- base document change rows (DOCUMENT_COLUMNS, lane per column), then lane per row ----
-  int64_t* DCC = reinterpret_cast<int64_t*>(S + F.cells);  // [9][nbc] (+ deps at [9*nbc])
+  int64_t* DCC = reinterpret_cast<int64_t*>(S + F.rw);  // [9][nbc] (+ deps at [9*nbc]), after the hash table
   if (has_base && l < DC_NCOLS) {
     const uint32_t col = l;
     const uint64_t off = dhb + dh->ccol_off[col];
@@ -1740,7 +1750,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     if (ishead) {
       const int64_t hidx = l < N ? (int64_t)nbc + l : reinterpret_cast<const int64_t*>(M + FM_BHIDX)[l - N];
       bad |= hidx < 0;
-      reinterpret_cast<int64_t*>(M + FM_HIDX)[pos] = hidx;
+      reinterpret_cast<int32_t*>(M + FM_HIDX)[pos] = (int32_t)hidx;  // < nbc + N <= 128
       M[FM_HSEL + pos] = (uint8_t)l;
       uint4* hg = reinterpret_cast<uint4*>(wsg + L.heads + 32 * pos);
       hg[0] = reinterpret_cast<const uint4*>(HT + 8 * l)[0];
@@ -2356,7 +2366,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   const uint32_t xlen = has_base ? uni((uint32_t)dh->extra_len) : 0u;
   uint32_t hib = 0;
   {
-    const int64_t* HIDX = reinterpret_cast<const int64_t*>(M + FM_HIDX);
+    const int32_t* HIDX = reinterpret_cast<const int32_t*>(M + FM_HIDX);
     const uint32_t hb = l < NH ? (uint32_t)uleb_len((uint64_t)HIDX[l]) : 0u;
     const uint32_t ho = excl_add(hb, hib);
     if (cols_end + hib + xlen > F.cells_cap) bad = true;
@@ -2390,8 +2400,12 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
       for (uint32_t q = 0; q < a_len; q++) o[q] = IN[src + q];
     }
     const uint32_t hbytes0 = heads0 + uleb_len(NH);
-    for (uint32_t q = l; q < 32 * NH; q += 64)
-      OB[hbytes0 + q] = reinterpret_cast<const uint8_t*>(HT + 8 * M[FM_HSEL + (q >> 5)])[q & 31];
+    // head bytes from their sources (the hash table in the cells region is gone): a change of this
+    // call (k_chunks' hash) or a base head (the base document's heads)
+    for (uint32_t q = l; q < 32 * NH; q += 64) {
+      const uint32_t t = M[FM_HSEL + (q >> 5)];
+      OB[hbytes0 + q] = t < N ? info[dd.chg_begin + t].hash[q & 31] : IN[dhb + dh->heads_off + 32 * (t - N) + (q & 31) - a0];
+    }
     if (l == 0) {
       uint8_t* o = OB + start;
       for (int k = 0; k < 4; k++) *o++ = kMagic[k];

@@ -14,6 +14,7 @@
 //              columnar.js:983-1004)
 //   k_out_hash_ws thread per document: container checksum of the merged document (columnar.js:659)
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include "am_dev_util.h"
 #include "am_layout.h"
@@ -1002,13 +1003,25 @@ void am_launch_doc(const BatchDev& b, hipStream_t s) {
   // documents whose hot working set fits the LDS allocation run from LDS; the rest (if any)
   // from their global workspace
   // small documents first: k_doc_fast merges every document in its envelope (one wave each,
-  // four per workgroup) and marks it; k_doc then takes the rest and exits at once for the marked
+  // one per workgroup) and marks it; k_doc then takes the rest and exits at once for the marked
   const uint8_t* fd = nullptr;
   if (b.fast_lds && b.fast_done) {
     (void)hipMemsetAsync(b.fast_done, 0, b.ndocs, s);
-    hipLaunchKernelGGL(b.any_diff ? k_doc_fast<true> : k_doc_fast<false>, dim3((b.ndocs + FD_DOCS_PER_WG - 1) / FD_DOCS_PER_WG), dim3(64 * FD_DOCS_PER_WG),
-                       FD_DOCS_PER_WG * b.fast_lds, s, b.arena, b.chunks, b.docs, b.known, b.info, b.hdr, b.bounds, b.ws_off, b.ws,
-                       b.ws_cap, b.fast_lds, b.ndocs, b.results, b.chg_state, b.fast_done);
+    // AM_FAST_SPLIT=<bytes> (probe): documents whose slice fits that many bytes run in a first launch
+    // with the smaller slice (more workgroups per CU), the others in a second with the largest
+    const char* se = std::getenv("AM_FAST_SPLIT");
+    const uint32_t split = se ? (uint32_t)std::strtoul(se, nullptr, 10) & ~15u : 0u;
+    auto launch = [&](uint32_t slice, uint32_t floor) {
+      hipLaunchKernelGGL(b.any_diff ? k_doc_fast<true> : k_doc_fast<false>, dim3((b.ndocs + FD_DOCS_PER_WG - 1) / FD_DOCS_PER_WG),
+                         dim3(64 * FD_DOCS_PER_WG), FD_DOCS_PER_WG * slice, s, b.arena, b.chunks, b.docs, b.known, b.info, b.hdr,
+                         b.bounds, b.ws_off, b.ws, b.ws_cap, slice, floor, b.ndocs, b.results, b.chg_state, b.fast_done);
+    };
+    if (split && split < b.fast_lds) {
+      launch(split, 0);
+      launch(b.fast_lds, split);
+    } else {
+      launch(b.fast_lds, 0);
+    }
     fd = b.fast_done;
   }
   if (!b.fast_only) {

@@ -246,3 +246,47 @@ def test_fast_and_general_kernels_agree(docs):
             bad.append((i, "heads", bool(flags[i])))
     assert not bad, (nfast, bad[:10])
     print("fast kernel merged %d of %d documents" % (nfast, len(items)))
+
+
+def test_fast_kernel_split_launch_matches_single_launch():
+    """AM_FAST_SPLIT (two k_doc_fast launches by LDS slice class: the documents whose slice fits the
+    split first, with the smaller slice, then the rest) merges and patches every document exactly as
+    one launch with the largest slice does, and the fast kernel still takes all of them."""
+    import os
+    import numpy as np
+    import workload
+    from automerge_amd import _native as N
+    from automerge_amd.batch import WANT_DIFF, Batch
+    items = []
+    for kind in ("c4", "c2"):
+        arena, chunks, dd, _ = getattr(workload, kind)(11, 400)
+        items += [workload.doc_chunks(arena, chunks, dd, i) for i in range(400)]
+
+    def run(split):
+        b = Batch()
+        b.stage_docs(items, flags=WANT_DIFF)
+        sl = np.zeros(len(items), np.uint32)
+        assert N.lib.am_batch_fast_slices(b._b, sl.ctypes.data) == 0
+        old = os.environ.get("AM_FAST_SPLIT")
+        if split is not None:
+            os.environ["AM_FAST_SPLIT"] = str(split(sl))
+        try:
+            b.run()
+            b.sync()
+        finally:
+            if old is None:
+                os.environ.pop("AM_FAST_SPLIT", None)
+            else:
+                os.environ["AM_FAST_SPLIT"] = old
+        r = b.results()
+        outs = [b.doc_output(i, r[i]) for i in range(len(items))]
+        pats = [b.doc_patch(i) for i in range(len(items))]
+        return r, outs, pats, b.fast_flags(), sl
+
+    r1, o1, p1, f1, sl = run(None)
+    assert (sl > 0).all() and len(set(sl.tolist())) > 1
+    r2, o2, p2, f2, _ = run(lambda s: int(np.median(s)) + 16)
+    assert (r1["status"] == 0).all() and (r2["status"] == 0).all()
+    assert f1.all() and f2.all()
+    assert o1 == o2
+    assert p1 == p2
