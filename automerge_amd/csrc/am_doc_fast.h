@@ -58,19 +58,16 @@
 #endif
 #define FD_NULL ((int32_t)0x80000000)
 #define FD_DIFF_SCRATCH 1216  // fast_diff's tables in the cells region
+#define FD_REC_BYTES 1024     // FdRec's row words (key, objc, idc, vlen) at the end of the cells region
 
 // misc region (byte offsets). Tables whose phases never overlap share a union slot:
-//   U1: {BHIDX, KIDX} (headers .. heads) | {IDT} (opId sort .. list elements) | {NSORT, BENT} (succ)
 //   U2: {CLOCK, FIRST} (actor table .. queue) | {SRCR, SRCE} (decode .. rows) | {CNTN} (succ)
+// The 64-bit tables live in the cells region while it is free of decoded cells: the base heads' /
+// known hashes' indexes (BHIDX, KIDX) before the decode, the sorted op ids (IDT) and the succ
+// sort (NSORT, BENT) between the row gather and the encode; FdRec's row words at its end.
 enum : uint32_t {
   FM_DH = 0,                      // DocHdrC (128 B)
-  FM_U1 = 128,                    // 1024 B union
-  FM_BHIDX = FM_U1,               //   int64 [64] base head -> changeIndexByHash index
-  FM_KIDX = FM_U1 + 512,          //   int64 [64] known hash -> index
-  FM_IDT = FM_U1,                 //   uint64 [64] sorted op ids (ctr << 12 | rank << 6 | row)
-  FM_NSORT = FM_U1,               //   uint64 [64] sorted new succ entries
-  FM_BENT = FM_U1 + 512,          //   uint64 [64] base entries (ctr << 6 | rank)
-  FM_U2 = FM_U1 + 1024,           // 512 B union
+  FM_U2 = 128,                    // 512 B union
   FM_CLOCK = FM_U2,               //   uint32 [64] base clock per doc actor
   FM_FIRST = FM_U2 + 256,         //   uint32 [64] first change authored by a canonical ref
   FM_SRCR = FM_U2,                //   int32 [64] row -> source marks
@@ -100,6 +97,8 @@ enum : uint32_t {
 
 struct FastLayout {
   uint32_t input, hashes, refs, misc, chg, cells, cells_cap, total, rw;
+  uint32_t bk;      // BHIDX (int64 per base head), then KIDX (int64 per known hash), in the cells region
+  uint32_t ob_cap;  // bytes of the cells region the output image / patch scratch may use (FdRec after)
 };
 
 // Per-document LDS slice of k_doc_fast (bytes, 16-aligned regions).
@@ -119,17 +118,22 @@ __host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t n
   // until the op columns are decoded the cells region holds the hash table (changes | base heads |
   // known), then the refs' 32 B id words (actor table) and later the base change rows over them
   const uint32_t dcc = 8 * (9 * nbc + nbd), rwb = 32 * nrefs;
-  const uint32_t early = 32 * nht + (dcc > rwb ? dcc : rwb);
+  const uint32_t bk = 32 * nht + (dcc > rwb ? dcc : rwb);
+  const uint32_t early = bk + 8 * (nbh + nknown);
   if (early > cells) cells = early;
+  if (cells < 1024) cells = 1024;  // IDT | NSORT, BENT
   // output image: header (actors, heads, column table) + columns + heads indexes + extra bytes
-  // (a larger image fails the encoder's capacity check: the document then goes to k_doc)
+  // (a larger image fails the encoder's capacity check: the document then goes to k_doc). With a
+  // patch requested, FdRec's row words take the last FD_REC_BYTES: the image gets the rest.
   const uint32_t out = 64 + 40 * b.A + 42 * b.H + 25 * 12 + span;
   if (out > cells) cells = out;
-  if (b.P && cells < FD_DIFF_SCRATCH) cells = FD_DIFF_SCRATCH;  // fast_diff's / fast_getpatch's tables
+  if (b.P && cells < FD_DIFF_SCRATCH + FD_REC_BYTES) cells = FD_DIFF_SCRATCH + FD_REC_BYTES;
   F.cells = take(cells);
   F.cells_cap = cells;
+  F.ob_cap = b.P ? cells - FD_REC_BYTES : cells;
   F.hashes = F.cells;
   F.rw = F.cells + 32 * nht;
+  F.bk = F.cells + bk;
   F.total = o;
   return F;
 }
@@ -664,12 +668,13 @@ struct FdRec {
   int8_t* elem; uint8_t *act, *flags;                         // FC / NS / LON
   uint8_t *bca, *adp;                                         // DEPD: base change row -> actor; DOWN: change -> author
 };
-__device__ __forceinline__ FdRec fd_rec(uint8_t* M) {
+// U1: FD_REC_BYTES at the end of the cells region (after the output image / patch scratch)
+__device__ __forceinline__ FdRec fd_rec(uint8_t* M, uint8_t* U1) {
   FdRec P;
-  P.key = reinterpret_cast<uint32_t*>(M + FM_U1);
-  P.objc = reinterpret_cast<int32_t*>(M + FM_U1 + 256);
-  P.idc = reinterpret_cast<int32_t*>(M + FM_U1 + 512);
-  P.vlen = reinterpret_cast<int32_t*>(M + FM_U1 + 768);
+  P.key = reinterpret_cast<uint32_t*>(U1);
+  P.objc = reinterpret_cast<int32_t*>(U1 + 256);
+  P.idc = reinterpret_cast<int32_t*>(U1 + 512);
+  P.vlen = reinterpret_cast<int32_t*>(U1 + 768);
   P.voff = reinterpret_cast<uint16_t*>(M + FM_U2);
   P.krow = M + FM_U2 + 128; P.sck = M + FM_U2 + 192; P.sok = M + FM_U2 + 256;
   P.obja = reinterpret_cast<int8_t*>(M + FM_U2 + 320); P.ida = M + FM_U2 + 384; P.krank = M + FM_U2 + 448;
@@ -706,7 +711,7 @@ __device__ __forceinline__ bool fast_diff(const uint8_t* IN, uint8_t* PS, uint32
                                           uint8_t* M, uint32_t R, uint32_t nb, uint32_t NOUT, uint32_t NA, uint32_t NC,
                                           uint32_t nbc, uint32_t N, const int32_t* OUTC, const uint8_t* OUTA, const uint32_t* RO,
                                           const ChgHdrC* chh) {
-  const FdRec P = fd_rec(M);
+  const FdRec P = fd_rec(M, PS + ps_cap);
   const uint32_t l = lane();
   const bool isrow_ = l < R;
   const int32_t r_key = isrow_ ? (int32_t)P.key[l] : FD_NULL, r_objc = isrow_ ? P.objc[l] : FD_NULL;
@@ -1052,7 +1057,7 @@ __device__ __forceinline__ bool fast_getpatch(const uint8_t* IN, uint8_t* PS, ui
                                               uint8_t* M, uint32_t NOUT, uint32_t NSUCC, uint32_t NA, uint32_t NC, uint32_t nbc,
                                               uint32_t N, const int32_t* OUTC, const uint8_t* OUTA, const uint32_t* RO,
                                               const ChgHdrC* chh) {
-  const FdRec P = fd_rec(M);
+  const FdRec P = fd_rec(M, PS + ps_cap);
   const uint32_t l = lane();
   const bool outl = l < NOUT;
   bool pbad = ps_cap < FD_DIFF_SCRATCH || NOUT > 64 || NSUCC > 64;
@@ -1422,7 +1427,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   FD_CHECK();
   // base heads' changeIndexByHash indexes (new.js:1729-1739); -1 = unknown
   if (l == 0) {
-    int64_t* bh = reinterpret_cast<int64_t*>(M + FM_BHIDX);
+    int64_t* bh = reinterpret_cast<int64_t*>(S + F.bk);
     if (dh->has_hidx) {
       Rd r{IN + (dhb + dh->hidx_off - a0), (uint64_t)1 << 40, 0};
       for (uint32_t h = 0; h < HB; h++) {
@@ -1458,7 +1463,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     }
 #pragma unroll
     for (int k = 0; k < 8; k++) HT[8 * (N + HB + l) + k] = w[k];
-    reinterpret_cast<int64_t*>(M + FM_KIDX)[l] = kh.index;
+    reinterpret_cast<int64_t*>(S + F.bk + 8 * HB)[l] = kh.index;
   }
 
   // ---- actor references: base actors [0, NB), then each change's actor list ----
@@ -1716,8 +1721,8 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
       if (words_eq(HT + 8 * t, w)) hit = (int32_t)t;
     }
     if (hit >= 0) {
-      dep_idx = hit < (int32_t)(N + HB) ? reinterpret_cast<const int64_t*>(M + FM_BHIDX)[hit - N]
-                                        : reinterpret_cast<const int64_t*>(M + FM_KIDX)[hit - N - HB];
+      dep_idx = hit < (int32_t)(N + HB) ? reinterpret_cast<const int64_t*>(S + F.bk)[hit - N]
+                                        : reinterpret_cast<const int64_t*>(S + F.bk + 8 * HB)[hit - N - HB];
       if (dep_idx < 0) bad = true;
     } else {
       for (uint64_t m = dmask & (N < 64 ? (1ull << N) - 1 : ~0ull); m && hit < 0; m &= m - 1) {
@@ -1748,7 +1753,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     }
     NH = __popcll(__ballot(ishead));
     if (ishead) {
-      const int64_t hidx = l < N ? (int64_t)nbc + l : reinterpret_cast<const int64_t*>(M + FM_BHIDX)[l - N];
+      const int64_t hidx = l < N ? (int64_t)nbc + l : reinterpret_cast<const int64_t*>(S + F.bk)[l - N];
       bad |= hidx < 0;
       reinterpret_cast<int32_t*>(M + FM_HIDX)[pos] = (int32_t)hidx;  // < nbc + N <= 128
       M[FM_HSEL + pos] = (uint8_t)l;
@@ -1936,7 +1941,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   FPH(6);
   // ---- opId order: (counter, actor rank) (new.js:1197-1224) ----
   const uint32_t r_rank = isrow ? RANKDP[r_ida] : 0;
-  uint64_t* IDT = reinterpret_cast<uint64_t*>(M + FM_IDT);
+  uint64_t* IDT = reinterpret_cast<uint64_t*>(S + F.cells);  // the decoded cells are in registers now
   uint32_t r_opr;
   {
     const uint64_t key = isrow ? ((uint64_t)(uint32_t)r_idc << 12) | (r_rank << 6) | l : ~0ull;
@@ -2136,8 +2141,8 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   }
 
   // ---- succ lists: base succs merged with the new succs of each row (new.js:1173-1188) ----
-  uint64_t* BENT = reinterpret_cast<uint64_t*>(M + FM_BENT);
-  uint64_t* NSORT = reinterpret_cast<uint64_t*>(M + FM_NSORT);
+  uint64_t* BENT = reinterpret_cast<uint64_t*>(S + F.cells + 512);
+  uint64_t* NSORT = reinterpret_cast<uint64_t*>(S + F.cells);
   uint32_t* CNTN = reinterpret_cast<uint32_t*>(M + FM_CNTN);
   uint8_t* LON = M + FM_LON;
   CNTN[l] = 0;
@@ -2195,7 +2200,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   // the row values fast_diff reads after the encode, parked in misc tables the merge is done with
   // (registers would stay live through the encode and spill)
   if (kDiff && b.P) {
-    const FdRec P = fd_rec(M);
+    const FdRec P = fd_rec(M, S + F.cells + F.ob_cap);
     if (isrow) {
       P.key[l] = (uint32_t)r_key; P.objc[l] = r_objc; P.idc[l] = r_idc; P.vlen[l] = r_vlen;
       P.voff[l] = (uint16_t)r_voff; P.obja[l] = (int8_t)r_obja; P.ida[l] = (uint8_t)r_ida; P.krank[l] = (uint8_t)r_krank;
@@ -2263,8 +2268,8 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     // pass (enc32r), staged at the end of the image region and copied into place below
     constexpr uint32_t kRowCap = 176;  // 16 values x (1 + 5 + 5) bytes
     const bool t31 = __all(!act || v_time == AM_NULL64 || (v_time >= 0 && v_time <= 0x7fffffff));
-    const bool seg = NC <= 16 && F.cells_cap >= cur + 8 * kRowCap + 64;
-    const uint32_t tbase = F.cells_cap - 8 * kRowCap;
+    const bool seg = NC <= 16 && F.ob_cap >= cur + 8 * kRowCap + 64;
+    const uint32_t tbase = F.ob_cap - 8 * kRowCap;
     uint32_t seglen[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // rows: U {actor, depsNum, extraLen}, D {seq, maxOp, time}
     if (seg) {
       const uint32_t g = l >> 4, p = l & 15;
@@ -2281,7 +2286,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
 #pragma unroll
       for (int r = 0; r < 4; r++) { seglen[r] = wave::bcast(lu, 16 * r); seglen[4 + r] = wave::bcast(ld, 16 * r); }
     }
-    const uint32_t cap_end = seg ? tbase : F.cells_cap;
+    const uint32_t cap_end = seg ? tbase : F.ob_cap;
 #pragma unroll 1
     for (int col = 0; col < DC_NCOLS; col++) {
       uint32_t len;
@@ -2352,7 +2357,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
         default: v = (int32_t)succ_c; n = NSUCC; break;
       }
       const bool eqs = col == OC_KEY_STR && key != FD_NULL && pkr == kr;
-      const uint32_t len = enc32k(kEncKind[col], n, v, nul && out, so, sl, eqs, IN, OB + cur, F.cells_cap - cur, bad);
+      const uint32_t len = enc32k(kEncKind[col], n, v, nul && out, so, sl, eqs, IN, OB + cur, F.ob_cap - cur, bad);
       if (len == ~0u) { bad = true; break; }
       if (l == 0) COLLEN[col] = len;
       cur += len;
@@ -2369,7 +2374,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     const int32_t* HIDX = reinterpret_cast<const int32_t*>(M + FM_HIDX);
     const uint32_t hb = l < NH ? (uint32_t)uleb_len((uint64_t)HIDX[l]) : 0u;
     const uint32_t ho = excl_add(hb, hib);
-    if (cols_end + hib + xlen > F.cells_cap) bad = true;
+    if (cols_end + hib + xlen > F.ob_cap) bad = true;
     else {
       if (l < NH) put_uleb(OB + cols_end + ho, (uint64_t)HIDX[l]);
       for (uint32_t q = l; q < xlen; q += 64) OB[cols_end + hib + q] = IN[dhb + dh->extra_off - a0 + q];
@@ -2442,10 +2447,10 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   }
   FPH(13);
   if (!kDiff && b.P) return;  // launched without the patch writers: k_doc writes the log
-  if (kDiff && b.P == 2 && !fast_diff(IN, S + F.cells, F.cells_cap, wsg + L.pwire, L.pwire_cap, M, R, nb, NOUT, NA, NC, nbc, N,
+  if (kDiff && b.P == 2 && !fast_diff(IN, S + F.cells, F.ob_cap, wsg + L.pwire, L.pwire_cap, M, R, nb, NOUT, NA, NC, nbc, N,
                                      OUTC, OUTA, RO, chh))
     return;  // outside the shapes fast_diff covers: k_doc replays the patch (am_diff.h)
-  if (kDiff && b.P == 1 && !fast_getpatch(IN, S + F.cells, F.cells_cap, wsg + L.pwire, L.pwire_cap, M, NOUT, NSUCC, NA, NC, nbc,
+  if (kDiff && b.P == 1 && !fast_getpatch(IN, S + F.cells, F.ob_cap, wsg + L.pwire, L.pwire_cap, M, NOUT, NSUCC, NA, NC, nbc,
                                           N, OUTC, OUTA, RO, chh))
     return;  // outside the shapes fast_getpatch covers: k_doc writes the log (P7, am_patch.h)
   FPH(14);
