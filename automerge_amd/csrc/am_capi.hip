@@ -886,7 +886,9 @@ static bool pipe_finalize(am_pipe* p, PipeSlot* sl) {
   struct { void* dst; const void* src; uint64_t n; } cp[3] = {{sl->h_summ, sl->summ.p, ns}, {sl->h_out, sl->dout.p, no},
                                                              {sl->h_patch, sl->dpatch.p, np}};
   hsa_agent_t gpu, host;
-  bool sdma = sl->home.handle && hsa_owner(sl->summ.p, gpu);
+  // AM_HOME_SDMA=0: copies home through the HIP copy kernel / stream instead of the SDMA engines
+  static const bool sdma_on = [] { const char* e = std::getenv("AM_HOME_SDMA"); return !(e && e[0] == '0'); }();
+  bool sdma = sdma_on && sl->home.handle && hsa_owner(sl->summ.p, gpu);
   for (auto& c : cp) sdma = sdma && (!c.n || hsa_owner(c.dst, host));
   sl->home_sdma = false;
   if (sdma) {
