@@ -112,7 +112,7 @@ __host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t n
   F.input = take(span + 32);
   F.refs = take(8 * nrefs);  // (off, len) per ref
   F.misc = take(FM_TOTAL);
-  F.chg = take((uint32_t)sizeof(ChgHdrC) * b.N);
+  F.chg = 0;  // change headers: read from k_chunks' slots in global memory
   const uint32_t nbc = b.C - b.N, nbd = b.D - b.ND;
   uint32_t cells = 4 * (13 * b.R + 2 * b.E);
   // until the op columns are decoded the cells region holds the hash table (changes | base heads |
@@ -876,7 +876,8 @@ __device__ __forceinline__ bool fast_diff(const uint8_t* IN, uint8_t* PS, uint32
   const uint32_t kc = l >= nbc ? l - nbc : 0u;
   const uint32_t kc_adp = __shfl(a_dp, kc & 63, 64);  // every lane takes part in the shuffle
   const uint32_t c_actor = l < nbc ? bc_actor : kc_adp;
-  const int64_t c_seq = l < nbc ? bc_seq : chh[kc < 64 ? kc : 0].seq;
+  int64_t c_seq = bc_seq;  // change headers are in global memory: only rows that exist read one
+  if (l >= nbc && kc < N) c_seq = chh[kc].seq;
   if (l < NC) atomicMax(&LASTC[c_actor], l);
   wsync();
   const bool c_emit = l < NC && LASTC[c_actor] == l;
@@ -1241,7 +1242,8 @@ __device__ __forceinline__ bool fast_getpatch(const uint8_t* IN, uint8_t* PS, ui
   const uint32_t kc = l >= nbc ? l - nbc : 0u;
   const uint32_t kc_adp = __shfl(l < N ? (uint32_t)P.adp[l] : 0u, kc & 63, 64);
   const uint32_t c_actor = l < nbc ? (uint32_t)P.bca[l] : kc_adp;
-  const int64_t c_seq = l < nbc ? (int64_t)P.bcs[l] : chh[kc < 64 ? kc : 0].seq;
+  int64_t c_seq = l < nbc ? (int64_t)P.bcs[l] : 0;  // change headers are in global memory
+  if (l >= nbc && kc < N) c_seq = chh[kc].seq;
   if (l < NC) atomicMax(&LASTC[c_actor], l);
   wsync();
   const bool c_emit = l < NC && LASTC[c_actor] == l;
@@ -1406,16 +1408,13 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
 
   // ---- headers: the base document (lane 0) and one change per lane ----
   DocHdrC* dh = reinterpret_cast<DocHdrC*>(M + FM_DH);
-  ChgHdrC* chh = reinterpret_cast<ChgHdrC*>(S + F.chg);
-  // parsed by k_chunks (compact slots): 8 x 16 B per header, base document first
+  // the change headers parsed by k_chunks (compact slots) are read where they lie (global memory,
+  // read a few times per change): their LDS copy would cost 128 B of every slice per change
+  const ChgHdrC* const chh = reinterpret_cast<const ChgHdrC*>(hdr + dd.chg_begin);
+  // the base document's header (8 x 16 B) into LDS
   {
-    const uint32_t hb = has_base ? 1u : 0u;
     const uint4* src_b = reinterpret_cast<const uint4*>(hdr + (has_base ? dd.base_chunk : 0));
-    const uint4* src_c = reinterpret_cast<const uint4*>(hdr + dd.chg_begin);
-    for (uint32_t v = l; v < 8 * (hb + N); v += 64) {
-      if (v < 8 * hb) reinterpret_cast<uint4*>(dh)[v] = src_b[v];
-      else reinterpret_cast<uint4*>(chh)[v - 8 * hb] = src_c[v - 8 * hb];
-    }
+    if (has_base && l < 8) reinterpret_cast<uint4*>(dh)[l] = src_b[l];
     if (!has_base && l == 0) { dh->nactors = 0; dh->nheads = 0; dh->has_hidx = 0; dh->extra_len = 0; dh->base = 0; }
   }
   wsync();
@@ -1803,9 +1802,13 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     const bool chg_src = !(has_base && s == 0);
     if (chg_src && (col == OC_ID_ACTOR || col == OC_ID_CTR)) return false;  // ids from the header
     const uint32_t c = has_base ? s - 1 : s;
-    const uint64_t cbase = chg_src ? chh[c].base : dhb;
-    off = (uint32_t)(cbase - a0) + (chg_src ? chh[c].col_off[col] : dh->ocol_off[col]);
-    len = chg_src ? chh[c].col_len[col] : dh->ocol_len[col];
+    if (chg_src) {
+      off = (uint32_t)(chh[c].base - a0) + chh[c].col_off[col];
+      len = chh[c].col_len[col];
+    } else {
+      off = (uint32_t)(dhb - a0) + dh->ocol_off[col];
+      len = dh->ocol_len[col];
+    }
     const uint32_t j = col < OC_VAL_RAW ? col : col - 1;
     const uint32_t r0 = ROW0[s], e0 = ENT0[s];
     n = j < 13 ? ROW0[s + 1] - r0 : ENT0[s + 1] - e0;
@@ -1846,7 +1849,8 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   const uint32_t r_q = isrow ? l - ROW0[r_src] : 0;
   // actor index of a change row maps through its change's actor list
   const uint32_t cnact = __shfl(c_nact, r_c & 63, 64), cab = __shfl(ambase, r_c & 63, 64);
-  const int64_t cstart = r_chg ? chh[r_c].start_op : 0;
+  int64_t cstart = 0;
+  if (r_chg) cstart = chh[r_c].start_op;
   const int32_t c_adp = (int32_t)__shfl(a_dp, r_c & 63, 64);
   auto mapact = [&](int32_t v) -> int32_t {
     if (v == FD_NULL) return -1;
@@ -1887,9 +1891,16 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   const uint32_t vsum0 = __shfl(vsum, r_row0 & 63, 64), psum0 = __shfl(r_psoff, r_row0 & 63, 64);
   uint32_t r_voff = 0;  // valRaw bytes of the row, relative to a0
   if (isrow) {
-    const uint64_t cbase = r_chg ? chh[r_c].base : dhb;
-    const uint32_t coff = r_chg ? chh[r_c].col_off[OC_VAL_RAW] : dh->ocol_off[OC_VAL_RAW];
-    const uint32_t clen = r_chg ? chh[r_c].col_len[OC_VAL_RAW] : dh->ocol_len[OC_VAL_RAW];
+    uint64_t cbase = dhb;
+    uint32_t coff, clen;
+    if (r_chg) {
+      cbase = chh[r_c].base;
+      coff = chh[r_c].col_off[OC_VAL_RAW];
+      clen = chh[r_c].col_len[OC_VAL_RAW];
+    } else {
+      coff = dh->ocol_off[OC_VAL_RAW];
+      clen = dh->ocol_len[OC_VAL_RAW];
+    }
     r_voff = (uint32_t)(cbase + coff - a0) + (vsum - vsum0);
     if (l + 1 == ROW0[r_src + 1] || l + 1 == R) {  // last row of its source
       bad |= (vsum - vsum0) + r_vb > clen;
