@@ -74,9 +74,9 @@ enum : uint32_t {
   FM_SRCE = FM_U2 + 256,          //   int32 [64] entry -> source marks
   FM_CNTN = FM_U2,                //   uint32 [64] new succs per target row
   FM_OUTC = FM_U2 + 512,          // int32 [64] output succ ctr
-  FM_ROW0 = FM_OUTC + 256,        // uint32 [65] first row of each source
-  FM_ENT0 = FM_ROW0 + 272,        // uint32 [65] first entry of each source
-  FM_COLLEN = FM_ENT0 + 272,      // uint32 [32] encoded column lengths
+  FM_ROW0 = FM_OUTC + 256,        // uint8 [65] first row of each source (<= 64 rows)
+  FM_ENT0 = FM_ROW0 + 80,         // uint8 [65] first entry of each source (<= 64 entries)
+  FM_COLLEN = FM_ENT0 + 80,       // uint32 [32] encoded column lengths
   FM_OWN = FM_COLLEN + 128,       // uint8 [64] owner row of each entry
   FM_CANON = FM_OWN + 64,         // uint8 [64] canonical ref of each ref
   FM_RANKC = FM_CANON + 64,       // uint8 [64] rank of each canonical ref
@@ -87,8 +87,8 @@ enum : uint32_t {
   FM_FC = FM_OPR + 64,            // int8 [64] first child (RGA)
   FM_NS = FM_FC + 64,             // int8 [64] next sibling (RGA)
   FM_LON = FM_NS + 64,            // uint8 [64] first sorted new succ of each target row
-  FM_DEPD = FM_LON + 64,          // uint8 [128] hash candidate is depended on
-  FM_OUTA = FM_DEPD + 128,        // uint8 [64] output succ actor
+  FM_DEPD = FM_LON + 64,          // uint8 [64] head candidate (change | base head, N + HB <= 64) is depended on
+  FM_OUTA = FM_DEPD + 64,         // uint8 [64] output succ actor
   FM_DOWN = FM_OUTA + 64,         // uint8 [64] owner change of each dep slot
   FM_HSEL = FM_DOWN + 64,         // uint8 [64] hash-table slot of each sorted head
   FM_HIDX = FM_HSEL + 64,         // int32 [64] sorted heads' indexes
@@ -1692,7 +1692,6 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   bad |= nd_total != b.ND;
   uint8_t* DEPD = M + FM_DEPD;
   DEPD[l] = 0;
-  DEPD[64 + l] = 0;
   if (l < N)
     for (uint32_t k = 0; k < c_ndeps; k++) M[FM_DOWN + dbase + k] = (uint8_t)l;
   wsync();
@@ -1782,11 +1781,11 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   uint32_t rtot, etot;
   const uint32_t s_row0 = excl_add(s_nr, rtot), s_ent0 = excl_add(s_ne, etot);
   bad |= rtot != R || etot != E || (l < nsrc && s_nr == 0 && s_ne != 0);
-  uint32_t* ROW0 = reinterpret_cast<uint32_t*>(M + FM_ROW0);
-  uint32_t* ENT0 = reinterpret_cast<uint32_t*>(M + FM_ENT0);
-  ROW0[l] = s_row0;
-  ENT0[l] = s_ent0;
-  if (l == 0) { ROW0[64] = rtot; ENT0[64] = etot; }
+  uint8_t* ROW0 = M + FM_ROW0;  // values <= 64 in a document that stays here (else `bad` ends it below)
+  uint8_t* ENT0 = M + FM_ENT0;
+  ROW0[l] = (uint8_t)s_row0;
+  ENT0[l] = (uint8_t)s_ent0;
+  if (l == 0) { ROW0[64] = (uint8_t)rtot; ENT0[64] = (uint8_t)etot; }
   int32_t* SRCR = reinterpret_cast<int32_t*>(M + FM_SRCR);
   int32_t* SRCE = reinterpret_cast<int32_t*>(M + FM_SRCE);
   SRCR[l] = -1;
