@@ -1152,17 +1152,21 @@ __global__ void __launch_bounds__(256) k_pipe_compact(const am_doc_result* __res
   const am_doc_result r = res[d];
   const uint64_t on = olen[d], oo = ooff[d], pn = plen[d], po = poff[d];
   const bool ofit = oo + on <= out_cap, pfit = po + pn <= patch_cap;
-  if (on && ofit) {
-    const uint4* src = reinterpret_cast<const uint4*>(ws + r.out_off);
-    uint4* dst = reinterpret_cast<uint4*>(dout + oo);
-    for (uint64_t q = l; q < on / 16; q += 64) dst[q] = src[q];
-  }
-  if (pn && pfit) {
-    const WsLayout L = ws_layout(bounds[d]);
-    const uint4* src = reinterpret_cast<const uint4*>(ws + r.ws_off + L.pwire);
-    uint4* dst = reinterpret_cast<uint4*>(dpatch + po);
-    for (uint64_t q = l; q < pn / 16; q += 64) dst[q] = src[q];
-  }
+  const uint64_t nov = (on && ofit) ? on / 16 : 0, npv = (pn && pfit) ? pn / 16 : 0;
+  const uint8_t* const pw = pn ? ws + r.ws_off + ws_layout(bounds[d]).pwire : ws;  // the document's patch log
+  const uint4* osrc = reinterpret_cast<const uint4*>(ws + r.out_off);
+  const uint4* psrc = reinterpret_cast<const uint4*>(pw);
+  uint4* odst = reinterpret_cast<uint4*>(dout + oo);
+  uint4* pdst = reinterpret_cast<uint4*>(dpatch + po);
+  // the first 1 KB of the document and of its log loaded together, then stored (most documents
+  // end there); the rest in 1 KB steps
+  uint4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
+  if (l < nov) a = osrc[l];
+  if (l < npv) c = psrc[l];
+  if (l < nov) odst[l] = a;
+  if (l < npv) pdst[l] = c;
+  for (uint64_t q = l + 64; q < nov; q += 64) odst[q] = osrc[q];
+  for (uint64_t q = l + 64; q < npv; q += 64) pdst[q] = psrc[q];
   if (l == 0) {
     am_doc_summary sm;
     sm.status = (!ofit || !pfit) && !r.status ? (uint32_t)AM_U_CAPACITY : r.status;
@@ -1170,8 +1174,7 @@ __global__ void __launch_bounds__(256) k_pipe_compact(const am_doc_result* __res
     sm.out_len = sm.status ? 0u : (uint32_t)r.out_len;
     uint32_t pl = 0;
     if (!sm.status && pn) {
-      const WsLayout L = ws_layout(bounds[d]);
-      const PatchHdr2* h = reinterpret_cast<const PatchHdr2*>(ws + r.ws_off + L.pwire);
+      const PatchHdr2* h = reinterpret_cast<const PatchHdr2*>(pw);
       pl = (uint32_t)(sizeof(PatchHdr2) + h->nbytes + h->meta_bytes);
     }
     sm.patch_len = pl;
