@@ -101,6 +101,7 @@ _sigs = {
     "am_batch_fast_slices": (C.c_int, [P, P]),
     "am_batch_digest": (C.c_int, [P, C.c_uint64, C.POINTER(C.c_uint64)]),
     "am_batch_fast_flags": (C.c_int, [P, P]),
+    "am_engine_stats": (C.c_int, [P, P]),
     "am_doc_init": (P, [P]),
     "am_doc_load": (P, [P, C.c_char_p, C.c_size_t, C.POINTER(Error)]),
     "am_doc_clone": (P, [P]),
@@ -163,6 +164,9 @@ _sigs = {
     "am_pipe_destroy": (None, [P]),
     "am_pipe_submit": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, C.c_uint32, P, P, C.c_uint64, P, C.c_uint64,
                                  C.POINTER(C.c_uint64), C.POINTER(Error)]),
+    "am_pipe_submit_packed": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, C.c_uint32, P, P, C.c_uint64, P,
+                                        C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(Error)]),
+    "am_pipe_engines": (C.c_int, [P, C.POINTER(C.c_uint32)]),
     "am_pipe_drain": (C.c_int, [P, P, C.c_uint32, C.POINTER(Error)]),
     "am_pipe_times": (C.c_int, [P, C.POINTER(C.c_float), C.POINTER(C.c_uint32)]),
     "am_pipe_run_resident": (C.c_int, [P, P, C.c_uint64, P, C.c_uint32, P, C.c_uint32, C.c_int, P, P, C.c_uint64, P,
@@ -228,6 +232,13 @@ def engine(device=0):
             raise_for(err)
         _engines[device] = e
     return _engines[device]
+
+
+def engine_stats(device=0):
+    """(documents of the per-handle calls, of them merged by k_doc_fast) since the last call."""
+    out = (C.c_uint64 * 2)()
+    lib.am_engine_stats(engine(device), out)
+    return int(out[0]), int(out[1])
 
 
 def buf_array(bufs):

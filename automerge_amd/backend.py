@@ -199,7 +199,31 @@ def loadBatch(datas, device=0):
     return out
 
 
+def _rounds(backends, run):
+    """Sequential semantics for a backend named more than once: `run(items)` takes the first
+    occurrence of each backend; a later occurrence runs in a following round, where a handle its
+    earlier call froze raises the outdated-document error (util.js:1-10) in its own slot, as the
+    second of two sequential calls would, and a handle whose earlier call failed (unchanged, not
+    frozen) is applied then. Returns the results in item order."""
+    out = [None] * len(backends)
+    pending = list(range(len(backends)))
+    while pending:
+        seen, now, later = set(), [], []
+        for i in pending:
+            (later if id(backends[i]) in seen else now).append(i)
+            seen.add(id(backends[i]))
+        for i, r in zip(now, run(now)):
+            out[i] = r
+        pending = later
+    return out
+
+
 def _apply_batch(backends, changes_lists, want_patch):
+    return _rounds(backends, lambda items: _apply_once([backends[i] for i in items], [changes_lists[i] for i in items],
+                                                       want_patch))
+
+
+def _apply_once(backends, changes_lists, want_patch):
     from . import patch as P
     idx, states, out = _prepare(len(backends), lambda i: _backend_state(backends[i]))
     n = len(idx)
@@ -678,7 +702,13 @@ def receiveSyncMessage(backend, old_sync_state, message):
 def receiveSyncMessages(backends, old_sync_states, messages):
     """receiveSyncMessage for many documents in one call (am_sync_receive_batch): every message's
     changes go through ONE batched applyChanges. Returns [(backend, syncState, patch or None) or
-    AutomergeError], each as receiveSyncMessage returns it."""
+    AutomergeError], each as receiveSyncMessage returns it (a backend named twice: as two
+    sequential calls, _rounds)."""
+    return _rounds(backends, lambda items: _receive_once([backends[i] for i in items], [old_sync_states[i] for i in items],
+                                                         [messages[i] for i in items]))
+
+
+def _receive_once(backends, old_sync_states, messages):
     from . import patch as P
     n = len(backends)
     decoded = [None] * n

@@ -288,6 +288,8 @@ struct am_engine {
   void* hist = nullptr;         // device buffers of the history batches (am_hist.hip)
   void* sync = nullptr;         // device buffers of the Bloom / selection calls (am_sync.hip)
   CollectBufs* coll = nullptr;  // the batched per-handle calls
+  uint64_t stat_docs = 0;       // documents of the per-handle calls (run_one / run_many) since the last am_engine_stats
+  uint64_t stat_fast = 0;       // of those, merged by k_doc_fast
 };
 
 struct am_batch {
@@ -619,6 +621,13 @@ extern "C" int am_batch_digest(am_batch* b, uint64_t first_doc, uint64_t* digest
   return 0;
 }
 
+extern "C" int am_engine_stats(am_engine* e, uint64_t* out2) {
+  out2[0] = e->stat_docs;
+  out2[1] = e->stat_fast;
+  e->stat_docs = e->stat_fast = 0;  // reset on read
+  return 0;
+}
+
 extern "C" int am_batch_fast_flags(am_batch* b, uint8_t* flags) {
   if (!set_device(b->eng)) return 1;
   if (!b->ndocs) return 0;
@@ -760,6 +769,9 @@ struct PipeSlot {
   DevBuf<uint64_t> olen, ooff, plen, poff, tmp, totals;
   DevBuf<uint8_t> dout, dpatch;
   DevBuf<am_doc_summary> summ;
+  DevBuf<uint32_t> clen;                       // packed descriptors (am_pipe_submit_packed) and their scans
+  DevBuf<am_doc_span> spans;
+  DevBuf<uint64_t> c64, coff, ctmp;
   uint64_t* h_totals = nullptr;                // pinned: the two arena sizes of the last run
   hipEvent_t ev_c0 = nullptr, ev_d0 = nullptr, ev_d1 = nullptr, ev_comp = nullptr, ev_in = nullptr, ev_out = nullptr;
   bool busy = false, finalized = false;
@@ -783,6 +795,7 @@ struct am_pipe {
   uint32_t nms = 0;
   std::vector<hipEvent_t> rev;                 // resident batches: 4 events each (chain start, doc kernels, end)
   uint32_t nres = 0;                           // resident batches since the last am_pipe_resident_sync
+  uint32_t eng_h2d = 0, eng_home = 0;          // SDMA engine masks of the host-link copies (0: runtime's choice)
 };
 
 static void pipe_free(am_pipe* p) {
@@ -958,35 +971,69 @@ static bool pipe_retire(am_pipe* p, PipeSlot* sl, bool wait_home) {
   return true;
 }
 
-extern "C" int am_pipe_submit(am_pipe* p, const uint8_t* arena, uint64_t arena_len, const am_chunk_desc* chunks,
-                              uint32_t nchunks, const am_doc_desc* docs, uint32_t ndocs, am_doc_summary* summary,
-                              uint8_t* out, uint64_t out_cap, uint8_t* patches, uint64_t patch_cap, uint64_t* ticket,
-                              am_error* err) {
+// H2D of one input segment of the slot's batch on the input stream (after the slot's previous
+// compute chain, pipe_retire), and the hand-over to the compute stream
+static bool pipe_h2d(am_pipe* p, PipeSlot*, void* dst, const void* src, uint64_t n) {
+  return !n || hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, p->s_in) == hipSuccess;
+}
+static bool pipe_h2d_done(am_pipe* p, PipeSlot* sl) {
+  return hipEventRecord(sl->ev_in, p->s_in) == hipSuccess && hipStreamWaitEvent(p->s_c, sl->ev_in, 0) == hipSuccess;
+}
+
+extern "C" int am_pipe_engines(am_pipe* p, uint32_t* out2) {
+  out2[0] = p->eng_h2d;
+  out2[1] = p->eng_home;
+  return 0;
+}
+
+// The inputs of a submission: either full descriptors (am_pipe_submit) or packed ones
+// (am_pipe_submit_packed, expanded on the device after the H2D)
+struct PipeIn {
+  const am_chunk_desc* chunks = nullptr;
+  const am_doc_desc* docs = nullptr;
+  const uint32_t* clen = nullptr;
+  const am_doc_span* spans = nullptr;
+};
+
+static int pipe_submit(am_pipe* p, const uint8_t* arena, uint64_t arena_len, const PipeIn& in, uint32_t nchunks, uint32_t ndocs,
+                       bool any_diff, am_doc_summary* summary, uint8_t* out, uint64_t out_cap, uint8_t* patches,
+                       uint64_t patch_cap, uint64_t* ticket, am_error* err) {
   auto fail = [&](const char* m) { to_c(Err{AM_U_CAPACITY, false, m}, err); return 1; };
   if (!set_device(p->eng)) return fail("automerge_amd: no device");
   const am_pipe_caps& c = p->caps;
   if (arena_len > c.arena_bytes || nchunks > c.chunks || ndocs > c.docs)
     return fail("automerge_amd: batch exceeds the pipeline capacities");
+  // resident batches run on slot 0's workspace without a ticket: they finish first
+  if (p->nres) return fail("automerge_amd: resident batches in flight (am_pipe_resident_sync first)");
   PipeSlot* sl = p->slots[p->next % p->slots.size()];
+  const bool packed = in.clen != nullptr;
+  if (packed && !(sl->clen.ensure(c.chunks) && sl->spans.ensure(c.docs) && sl->c64.ensure(c.chunks) && sl->coff.ensure(c.chunks) &&
+                  sl->ctmp.ensure(am_scan_tmp_elems(c.chunks))))
+    return fail("automerge_amd: device allocation failed (packed descriptors)");
   if (!pipe_retire(p, sl, false)) return fail("automerge_amd: HIP error while retiring a batch");
   am_batch& b = sl->b;
   b.nchunks = nchunks;
   b.ndocs = ndocs;
-  b.any_diff = false;
-  for (uint32_t d = 0; d < ndocs && !b.any_diff; d++) b.any_diff = (docs[d].flags & (AM_DOC_WANT_DIFF | AM_DOC_WANT_PATCH)) != 0;
+  b.any_diff = any_diff;
   // inputs
-  if (arena_len && hipMemcpyAsync(b.arena.p, arena, arena_len, hipMemcpyHostToDevice, p->s_in) != hipSuccess) return fail("automerge_amd: H2D failed");
-  if (nchunks && hipMemcpyAsync(b.chunks.p, chunks, sizeof(am_chunk_desc) * nchunks, hipMemcpyHostToDevice, p->s_in) != hipSuccess)
+  if (!pipe_h2d(p, sl, b.arena.p, arena, arena_len)) return fail("automerge_amd: H2D failed");
+  if (packed) {
+    if (!pipe_h2d(p, sl, sl->clen.p, in.clen, sizeof(uint32_t) * nchunks) ||
+        !pipe_h2d(p, sl, sl->spans.p, in.spans, sizeof(am_doc_span) * ndocs))
+      return fail("automerge_amd: H2D failed");
+  } else if (!pipe_h2d(p, sl, b.chunks.p, in.chunks, sizeof(am_chunk_desc) * nchunks) ||
+             !pipe_h2d(p, sl, b.docs.p, in.docs, sizeof(am_doc_desc) * ndocs)) {
     return fail("automerge_amd: H2D failed");
-  if (ndocs && hipMemcpyAsync(b.docs.p, docs, sizeof(am_doc_desc) * ndocs, hipMemcpyHostToDevice, p->s_in) != hipSuccess)
-    return fail("automerge_amd: H2D failed");
-  if (hipEventRecord(sl->ev_in, p->s_in) != hipSuccess || hipStreamWaitEvent(p->s_c, sl->ev_in, 0) != hipSuccess)
-    return fail("automerge_amd: stream ordering failed");
+  }
+  if (!pipe_h2d_done(p, sl)) return fail("automerge_amd: stream ordering failed");
   // the whole chain on the compute stream; no host round trip
   BatchDev d = b.dev();
   d.ws_cap = c.ws_bytes;
   hipStream_t s = p->s_c;
   (void)hipEventRecord(sl->ev_c0, s);
+  if (packed)
+    am_launch_unpack(sl->clen.p, nchunks, arena_len, sl->spans.p, ndocs, sl->c64.p, sl->coff.p, sl->ctmp.p, sl->olen.p, sl->ooff.p,
+                     sl->tmp.p, sl->totals.p, b.chunks.p, b.docs.p, s);
   am_launch_chunks(d, s);
   am_launch_bounds(d, s);
   (void)hipEventRecord(sl->ev_d0, s);
@@ -1019,6 +1066,36 @@ extern "C" int am_pipe_submit(am_pipe* p, const uint8_t* arena, uint64_t arena_l
   return 0;
 }
 
+extern "C" int am_pipe_submit(am_pipe* p, const uint8_t* arena, uint64_t arena_len, const am_chunk_desc* chunks,
+                              uint32_t nchunks, const am_doc_desc* docs, uint32_t ndocs, am_doc_summary* summary,
+                              uint8_t* out, uint64_t out_cap, uint8_t* patches, uint64_t patch_cap, uint64_t* ticket,
+                              am_error* err) {
+  PipeIn in;
+  in.chunks = chunks;
+  in.docs = docs;
+  bool any_diff = false;
+  for (uint32_t d = 0; d < ndocs && !any_diff; d++) any_diff = (docs[d].flags & (AM_DOC_WANT_DIFF | AM_DOC_WANT_PATCH)) != 0;
+  return pipe_submit(p, arena, arena_len, in, nchunks, ndocs, any_diff, summary, out, out_cap, patches, patch_cap, ticket, err);
+}
+
+extern "C" int am_pipe_submit_packed(am_pipe* p, const uint8_t* arena, uint64_t arena_len, const uint32_t* chunk_len,
+                                     uint32_t nchunks, const am_doc_span* docs, uint32_t ndocs, am_doc_summary* summary,
+                                     uint8_t* out, uint64_t out_cap, uint8_t* patches, uint64_t patch_cap, uint64_t* ticket,
+                                     am_error* err) {
+  if ((nchunks && !chunk_len) || (ndocs && !docs)) {
+    to_c(Err{AM_U_CAPACITY, false, "automerge_amd: missing packed descriptors"}, err);
+    return 1;
+  }
+  PipeIn in;
+  static const uint32_t none = 0;
+  static const am_doc_span nospan{};
+  in.clen = nchunks ? chunk_len : &none;
+  in.spans = ndocs ? docs : &nospan;
+  bool any_diff = false;
+  for (uint32_t d = 0; d < ndocs && !any_diff; d++) any_diff = (docs[d].flags & (AM_DOC_WANT_DIFF | AM_DOC_WANT_PATCH)) != 0;
+  return pipe_submit(p, arena, arena_len, in, nchunks, ndocs, any_diff, summary, out, out_cap, patches, patch_cap, ticket, err);
+}
+
 // One batch whose inputs are already resident in device memory: the whole chain of am_pipe_submit
 // (k_chunks .. k_pipe_compact) on the pipeline's compute stream, with the merged documents, patch
 // logs and summaries compacted into the caller's device buffers and the two arena totals written to
@@ -1033,6 +1110,8 @@ extern "C" int am_pipe_run_resident(am_pipe* p, const uint8_t* d_arena, uint64_t
   const am_pipe_caps& c = p->caps;
   if (arena_len > c.arena_bytes || nchunks > c.chunks || ndocs > c.docs)
     return fail("automerge_amd: batch exceeds the pipeline capacities");
+  // 4 events per batch until am_pipe_resident_sync: a bounded number of batches between syncs
+  if (p->nres >= 4096) return fail("automerge_amd: 4096 resident batches without am_pipe_resident_sync");
   PipeSlot* sl = p->slots[0];
   if (sl->busy && !pipe_retire(p, sl, true)) return fail("automerge_amd: HIP error while retiring a batch");
   am_batch& b = sl->b;
@@ -1133,7 +1212,6 @@ struct am_doc {
   // objectMeta's children snapshots as this handle's last applyChanges left them (am_diff.h
   // diff_meta_pack; new.js:1812, 1857); empty: documentPatch's of the state (load / init)
   std::vector<uint8_t> meta;
-  bool meta_lost = false;  // a patchless call could not follow objectMeta (a PATCH_U_* input)
   int64_t max_op = 0;
   size_t nchanges = 0;
 };
@@ -1241,6 +1319,13 @@ bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified,
     // invalid UTF-8 in a key or message: run again with room for the U+FFFD replacements
     if (res.r.status != AM_U_UTF8 || (dd.flags & AM_DOC_FIX_UTF8)) break;
     dd.flags |= AM_DOC_FIX_UTF8;
+  }
+  {
+    uint8_t f = 0;
+    if (am_batch_fast_flags(b, &f) == 0) {
+      e->stat_docs++;
+      e->stat_fast += f;
+    }
   }
   res.chg_state.assign(cds.size(), 0);
   std::vector<uint8_t> hs(32 * cds.size());
@@ -1462,6 +1547,13 @@ bool run_many(am_engine* e, const std::vector<ManyJob>& jobs, std::vector<ManyOu
   if (!ok || !batch_collect(b, summ, out, pat)) {
     err = {AM_U_CAPACITY, false, "automerge_amd: result copy failed"};
     return false;
+  }
+  {
+    std::vector<uint8_t> fd(n);
+    if (am_batch_fast_flags(b, fd.data()) == 0) {
+      e->stat_docs += n;
+      for (uint8_t f : fd) e->stat_fast += f;
+    }
   }
   clk.mark("home");
   am_par_for(n, [&](size_t i) {
@@ -1787,15 +1879,8 @@ static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* le
   // BackendDoc.applyChanges (backend.js:116-121), whose updatePatchProperty calls refresh the
   // children snapshots and raise its errors. So every call replays the patch (P8) with the
   // handle's snapshots; loadChanges only drops the log.
-  if (patch && d->meta_lost) {
-    to_c(Err{AM_U_VALUE, false,
-             "automerge_amd: unsupported: this handle's objectMeta was not followed through an earlier "
-             "loadChanges whose patch shape the engine does not restate"},
-         err);
-    return 1;
-  }
-  const bool track = !d->meta_lost;
-  const int pmode = track ? 2 : 0;
+  const bool track = true;
+  const int pmode = 2;
   const std::vector<uint8_t>* meta = track ? &d->meta : nullptr;
   std::vector<am_known_hash> known;
   auto fill_known = [&]() {
@@ -1847,7 +1932,12 @@ static int apply_finish(am_doc* d, std::vector<std::vector<uint8_t>>& orig, bool
   if (track) {
     Err pe;
     if (patch_log_error(res.patch, pe)) {
-      if (patch || pe.code < AM_U_HASH_GRAPH) { to_c(pe, err); return 1; }
+      // loadChanges runs the same updatePatchProperty as applyChanges (backend.js:116-121), so what
+      // the replay reports -- a reference error, or a shape it does not restate (the reference throws
+      // there too, am_diff.h) -- fails the call either way and leaves the handle unchanged. Only the
+      // engine's own pool limit lets a patchless call commit: its objectMeta is then resynchronised
+      // to documentPatch's of the new state (as after save + load), never left unusable.
+      if (patch || pe.code != AM_U_CAPACITY) { to_c(pe, err); return 1; }
       lost = true;
     }
     if (patch) patch->swap(res.patch);
@@ -1875,8 +1965,7 @@ static int apply_finish(am_doc* d, std::vector<std::vector<uint8_t>>& orig, bool
   d->nchanges = res.r.nchanges;
   if (res.r.max_op > d->max_op) d->max_op = res.r.max_op;
   if (track) {
-    d->meta_lost = lost;
-    if (lost) d->meta.clear();
+    if (lost) d->meta.clear();  // documentPatch's snapshots of the new state
     else d->meta = std::move(res.meta);
   }
   if (err) err->code = 0;
@@ -2137,7 +2226,22 @@ static bool ensure_graph(am_doc* d, am_error* err);
 // computeHashGraph of n handles (all of one engine): one k_history batch per 4096; then every
 // handle's graph index is brought up to date on the host worker threads, so that the graph queries
 // that follow (getChanges, getMissingDeps, getChangeByHash) only read it.
-extern "C" int am_doc_compute_hash_graph_batch(size_t n, am_doc* const* docs, uint32_t* codes, char** msgs) {
+// A batch call that ran out of host memory (on the calling thread or a worker, am_par_for): every
+// call of the batch reports it in its place instead of the process aborting
+static int host_oom(size_t n, uint32_t* codes, char** msgs) {
+  try {
+    std::vector<Err> E(n, Err{AM_U_CAPACITY, false, "automerge_amd: out of host memory"});
+    return publish(E, codes, msgs);
+  } catch (const std::bad_alloc&) {
+    for (size_t i = 0; i < n; i++) {
+      codes[i] = AM_U_CAPACITY;
+      msgs[i] = nullptr;
+    }
+    return (int)n;
+  }
+}
+
+static int am_doc_compute_hash_graph_batch_impl(size_t n, am_doc* const* docs, uint32_t* codes, char** msgs) {
   std::vector<Err> E(n);
   std::vector<am_doc*> need;
   std::vector<size_t> at;
@@ -2162,10 +2266,17 @@ extern "C" int am_doc_compute_hash_graph_batch(size_t n, am_doc* const* docs, ui
   am_par_for(idx.size(), [&](size_t k) { (void)ensure_graph(idx[k], nullptr); });
   return publish(E, codes, msgs);
 }
+extern "C" int am_doc_compute_hash_graph_batch(size_t n, am_doc* const* docs, uint32_t* codes, char** msgs) {
+  try {
+    return am_doc_compute_hash_graph_batch_impl(n, docs, codes, msgs);
+  } catch (const std::bad_alloc&) {
+    return host_oom(n, codes, msgs);
+  }
+}
 
 // Backend.load of n documents (backend.js:104-107) in one GPU batch: docs[i] = the handle, or
 // nullptr with codes[i] / msgs[i] set. Returns the number that failed.
-extern "C" int am_doc_load_batch(am_engine* eng, size_t n, const uint8_t* const* data, const size_t* lens, am_doc** docs,
+static int am_doc_load_batch_impl(am_engine* eng, size_t n, const uint8_t* const* data, const size_t* lens, am_doc** docs,
                                  uint32_t* codes, char** msgs) {
   std::vector<Err> E(n);
   std::vector<std::vector<uint8_t>> staged;
@@ -2215,6 +2326,14 @@ extern "C" int am_doc_load_batch(am_engine* eng, size_t n, const uint8_t* const*
   }
   return publish(E, codes, msgs);
 }
+extern "C" int am_doc_load_batch(am_engine* eng, size_t n, const uint8_t* const* data, const size_t* lens, am_doc** docs,
+                                 uint32_t* codes, char** msgs) {
+  try {
+    return am_doc_load_batch_impl(eng, n, data, lens, docs, codes, msgs);
+  } catch (const std::bad_alloc&) {
+    return host_oom(n, codes, msgs);
+  }
+}
 
 // Backend.applyChanges / loadChanges (backend.js:27-32, 115-120) of n handles in one GPU batch:
 // handle i gets the changes bufs[off[i] .. off[i+1]). patches != nullptr: applyChanges, patches[i]
@@ -2222,7 +2341,7 @@ extern "C" int am_doc_load_batch(am_engine* eng, size_t n, const uint8_t* const*
 // appears more than once takes its later calls after the batch, in order; the handles whose call
 // needs the hash graph (loaded documents, new.js:1826-1832) have it computed in one batch and run
 // again. Returns the number of calls that failed (the handle unchanged).
-extern "C" int am_doc_apply_changes_batch(size_t n, am_doc* const* docs, const size_t* off, const uint8_t* const* bufs,
+static int am_doc_apply_changes_batch_impl(size_t n, am_doc* const* docs, const size_t* off, const uint8_t* const* bufs,
                                           const size_t* lens, uint8_t** patches, size_t* patch_lens, am_call_info* info,
                                           uint32_t* codes, char** msgs) {
   struct Call {
@@ -2251,7 +2370,7 @@ extern "C" int am_doc_apply_changes_batch(size_t n, am_doc* const* docs, const s
     if (info) info[i] = am_call_info{0, 0, 0, nullptr};
     am_doc* d = docs[i];
     const bool first = seen.insert(d).second;
-    if (d->eng != eng || !first || (patches && d->meta_lost)) { single.push_back(i); continue; }
+    if (d->eng != eng || !first) { single.push_back(i); continue; }
     calls.emplace_back();
     calls.back().i = i;
   }
@@ -2261,7 +2380,7 @@ extern "C" int am_doc_apply_changes_batch(size_t n, am_doc* const* docs, const s
     c.orig.reserve(off[c.i + 1] - off[c.i] + d->queue.size());
     for (size_t q = off[c.i]; q < off[c.i + 1]; q++) c.orig.emplace_back(bufs[q], bufs[q] + lens[q]);
     for (auto& q : d->queue) c.orig.push_back(q);
-    c.track = !d->meta_lost;
+    c.track = true;
     known_of(d, c.known);
   });
   clk.mark("inputs");
@@ -2358,9 +2477,18 @@ extern "C" int am_doc_apply_changes_batch(size_t n, am_doc* const* docs, const s
   clk.print("apply_changes_batch", n);
   return publish(E, codes, msgs);
 }
+extern "C" int am_doc_apply_changes_batch(size_t n, am_doc* const* docs, const size_t* off, const uint8_t* const* bufs,
+                                          const size_t* lens, uint8_t** patches, size_t* patch_lens, am_call_info* info,
+                                          uint32_t* codes, char** msgs) {
+  try {
+    return am_doc_apply_changes_batch_impl(n, docs, off, bufs, lens, patches, patch_lens, info, codes, msgs);
+  } catch (const std::bad_alloc&) {
+    return host_oom(n, codes, msgs);
+  }
+}
 
 // Backend.getPatch (backend.js:125-127) of n handles in one GPU batch; out[i] malloc'd.
-extern "C" int am_doc_get_patch_batch(size_t n, am_doc* const* docs, uint8_t** out, size_t* lens, am_call_info* info,
+static int am_doc_get_patch_batch_impl(size_t n, am_doc* const* docs, uint8_t** out, size_t* lens, am_call_info* info,
                                       uint32_t* codes, char** msgs) {
   std::vector<Err> E(n);
   std::vector<ManyJob> jobs;
@@ -2404,10 +2532,18 @@ extern "C" int am_doc_get_patch_batch(size_t n, am_doc* const* docs, uint8_t** o
   }
   return publish(E, codes, msgs);
 }
+extern "C" int am_doc_get_patch_batch(size_t n, am_doc* const* docs, uint8_t** out, size_t* lens, am_call_info* info,
+                                      uint32_t* codes, char** msgs) {
+  try {
+    return am_doc_get_patch_batch_impl(n, docs, out, lens, info, codes, msgs);
+  } catch (const std::bad_alloc&) {
+    return host_oom(n, codes, msgs);
+  }
+}
 
 // Backend.save (new.js:2025-2047) of n handles: the DEFLATE stage on the host, every checksum in one
 // GPU SHA-256 launch; out[i] malloc'd.
-extern "C" int am_doc_save_batch(size_t n, am_doc* const* docs, uint8_t** out, size_t* lens, uint32_t* codes, char** msgs) {
+static int am_doc_save_batch_impl(size_t n, am_doc* const* docs, uint8_t** out, size_t* lens, uint32_t* codes, char** msgs) {
   std::vector<Err> E(n);
   std::vector<std::vector<uint8_t>> bytes(n);
   std::vector<uint8_t> ready(n, 0);
@@ -2451,6 +2587,13 @@ extern "C" int am_doc_save_batch(size_t n, am_doc* const* docs, uint8_t** out, s
     lens[i] = bytes[i].size();
   }
   return publish(E, codes, msgs);
+}
+extern "C" int am_doc_save_batch(size_t n, am_doc* const* docs, uint8_t** out, size_t* lens, uint32_t* codes, char** msgs) {
+  try {
+    return am_doc_save_batch_impl(n, docs, out, lens, codes, msgs);
+  } catch (const std::bad_alloc&) {
+    return host_oom(n, codes, msgs);
+  }
 }
 
 extern "C" int am_doc_queued(const am_doc* d, size_t i, const uint8_t** data, size_t* len) {
@@ -2626,7 +2769,7 @@ extern "C" int am_stage_change(const uint8_t* in, size_t len, uint8_t** out, siz
 // and one GPU inflate batch for the DEFLATEd columns of all of them. outs[i] (malloc'd) = the staged
 // chunk, verified[i] = 1 when its checksum was verified here; codes[i] / msgs[i] as in
 // am_doc_load_batch. Returns the number that failed.
-extern "C" int am_stage_documents(am_engine* eng, size_t n, const uint8_t* const* data, const size_t* lens, uint8_t** outs,
+static int am_stage_documents_impl(am_engine* eng, size_t n, const uint8_t* const* data, const size_t* lens, uint8_t** outs,
                                   size_t* out_lens, uint8_t* verified, uint32_t* codes, char** msgs) {
   std::vector<std::vector<uint8_t>> st;
   std::vector<uint8_t> ver;
@@ -2642,6 +2785,14 @@ extern "C" int am_stage_documents(am_engine* eng, size_t n, const uint8_t* const
     out_lens[i] = st[i].size();
   });
   return publish(E, codes, msgs);
+}
+extern "C" int am_stage_documents(am_engine* eng, size_t n, const uint8_t* const* data, const size_t* lens, uint8_t** outs,
+                                  size_t* out_lens, uint8_t* verified, uint32_t* codes, char** msgs) {
+  try {
+    return am_stage_documents_impl(eng, n, data, lens, outs, out_lens, verified, codes, msgs);
+  } catch (const std::bad_alloc&) {
+    return host_oom(n, codes, msgs);
+  }
 }
 extern "C" int am_stage_document(am_engine* eng, const uint8_t* in, size_t len, uint8_t** out, size_t* outlen,
                                  int* verified, am_error* err) {

@@ -140,7 +140,7 @@ __host__ __device__ inline FastLayout fast_layout(const DocBounds& b, uint32_t n
 
 __host__ __device__ inline bool fast_eligible(const DocBounds& b, const am_doc_desc& dd) {
   // getPatch logs: fast_getpatch; applyChanges patches: fast_diff (both fall back to k_doc)
-  if (dd.flags & (AM_DOC_FIX_UTF8 | AM_DOC_PATCH_ROOM | AM_DOC_META)) return false;
+  if (dd.flags & (AM_DOC_FIX_UTF8 | AM_DOC_PATCH_ROOM)) return false;
   if (b.B == 0 || doc_scattered(b) || b.UC) return false;
   if (dd.base_chunk < 0 && dd.chg_count == 0) return false;
   if (b.span_hi - b.span_lo > FD_SPAN_MAX) return false;
@@ -707,10 +707,19 @@ static_assert(FM_U2 + 512 <= FM_OUTC, "U2 records");
 // Anything else returns false before any result is committed and the document goes to k_doc,
 // whose lane-0 replay covers every shape. Scratch: FD_DIFF_SCRATCH bytes at PS (the output image has
 // left).
+//
+// objectMeta (AM_DOC_META, new.js:884-931, 1461-1528; am_diff.h meta_restore / diff_meta_pack): in this
+// shape no call of updatePatchProperty rewrites a children snapshot -- a touched root key has only set /
+// inc rows (a snapshot exists only for keys that have had a make op), a list element is a `set`, and
+// the list's own key is not visited -- so the snapshots the call leaves are the ones it starts from,
+// renumbered to the merged document order: the handle's blob (mblob), or documentPatch's of the base
+// document when the handle has none (load / init: replayed per root key below). The closed form's
+// link of the list to the root reads root.children[list key], which must then be exactly {make op};
+// any other snapshot, a make op outside the root, or a snapshot of a touched key returns false.
 __device__ __forceinline__ bool fast_diff(const uint8_t* IN, uint8_t* PS, uint32_t ps_cap, uint8_t* out, uint64_t out_cap,
                                           uint8_t* M, uint32_t R, uint32_t nb, uint32_t NOUT, uint32_t NA, uint32_t NC,
                                           uint32_t nbc, uint32_t N, const int32_t* OUTC, const uint8_t* OUTA, const uint32_t* RO,
-                                          const ChgHdrC* chh) {
+                                          const ChgHdrC* chh, bool meta, const uint8_t* mblob, uint32_t mlen) {
   const FdRec P = fd_rec(M, PS + ps_cap);
   const uint32_t l = lane();
   const bool isrow_ = l < R;
@@ -797,6 +806,8 @@ __device__ __forceinline__ bool fast_diff(const uint8_t* IN, uint8_t* PS, uint32
   pbad |= touched && ((r_act != 1 && r_act != 5) || (r_key & 255) == 0);
   // ops of a touched key that its last call hands to updatePatchProperty
   const bool taken = touched && !(CONT[r_krank] && r_opr > LOPR[r_krank]);
+  // objectMeta carried across calls: make ops only in the root (actions of ACTIONS or beyond, even)
+  if (meta) pbad |= isrow && (r_act == 255 || ((r_act & 1) == 0 && (r_objc != FD_NULL || !keyed)));
   if (__any(pbad)) return false;
 
   // ---- counters (new.js:937-965): lane per succ entry of the merged document (entry q of output
@@ -976,6 +987,97 @@ __device__ __forceinline__ bool fast_diff(const uint8_t* IN, uint8_t* PS, uint32
   pbad |= sizeof(PatchHdr2) + (uint64_t)base > out_cap;
   if (__any(pbad)) return false;
 
+  // ---- objectMeta blob after the stream (lane 0; rows and positions < 64: one LEB128 byte each) ----
+  uint32_t mbytes = 0;
+  if (meta) {
+    bool mok = true;
+    if (l == 0) {
+      uint8_t* const mo = out + sizeof(PatchHdr2) + base;
+      const uint64_t mcap = out_cap - sizeof(PatchHdr2) - base;
+      uint32_t w = 5, nk = 0;  // "AMM1", entry count, entries
+      bool found_m = false;
+      auto put = [&](uint32_t v) {
+        if (v >= 128 || w >= mcap) { mok = false; return; }
+        mo[w++] = (uint8_t)v;
+      };
+      auto root_key_row = [&](uint32_t row) { return row < R && P.objc[row] == FD_NULL && (P.flags[row] & 4) != 0; };
+      if (mblob) {
+        // the handle's snapshots (base rows = this call's base document order) renumbered
+        uint32_t off = 0;
+        auto get = [&](uint32_t& v) {
+          v = 0;
+          for (uint32_t sh = 0; sh < 35; sh += 7) {
+            if (off >= mlen) { mok = false; return; }
+            const uint8_t b8 = mblob[off++];
+            v |= (uint32_t)(b8 & 0x7f) << sh;
+            if (!(b8 & 0x80)) return;
+          }
+          mok = false;
+        };
+        uint32_t cnt = 0;
+        mok = mlen >= 4 && mblob[0] == 'A' && mblob[1] == 'M' && mblob[2] == 'M' && mblob[3] == '1';
+        off = 4;
+        if (mok) get(cnt);
+        for (uint32_t k = 0; mok && k < cnt; k++) {
+          uint32_t orow = 0, erow = 0, n = 0;
+          get(orow); get(erow); get(n);
+          mok = mok && orow == 0 && erow < nb && root_key_row(erow) && !TCH[P.krank[erow]];
+          if (!mok) break;
+          const uint32_t kr_ = P.krank[erow];
+          const bool is_mkey = mli && kr_ == m_kr;
+          if (is_mkey && n != 1) mok = false;
+          put(0); put(POS[erow]); put(n);
+          for (uint32_t q = 0; mok && q < n; q++) {
+            uint32_t vr = 0;
+            get(vr);
+            mok = mok && vr < nb && root_key_row(vr) && P.krank[vr] == kr_;
+            if (mok) put(POS[vr]);
+            if (is_mkey) mok = mok && n == 1 && vr == mrow;
+          }
+          found_m |= is_mkey;
+          nk++;
+        }
+        mok = mok && off == mlen;
+      } else {
+        // documentPatch's snapshots of the base document (new.js:884-931 over each root key's rows in
+        // document order): a make op joins the snapshot; the snapshot becomes the visible ops so far
+        // once the key has a visible make op or a non-empty snapshot. Keys this call touches have no
+        // make rows (above), so their (absent) snapshots are the base document's as well.
+        uint32_t p = 0;
+        while (mok && p < NOUT) {
+          const uint32_t r0 = P.krow[p];
+          if (!root_key_row(r0)) { p++; continue; }
+          const uint32_t kr_ = P.krank[r0], p0 = p;
+          bool exists = false, has_child = false;
+          uint64_t snap = 0, vis = 0;
+          for (; p < NOUT && root_key_row(P.krow[p]) && P.krank[P.krow[p]] == kr_; p++) {
+            const uint32_t r = P.krow[p];
+            const uint32_t a = P.act[r];
+            const bool mk = (a & 1) == 0, visible = SCR[r] == 0;
+            if (mk) { exists = true; snap |= 1ull << p; }
+            if (visible) { vis |= 1ull << p; has_child |= mk; }
+            if (has_child || (exists && snap)) { snap = vis; exists = true; }
+          }
+          if (!exists) continue;
+          const bool is_mkey = mli && kr_ == m_kr;
+          if (is_mkey) mok = mok && snap == (1ull << POS[mrow]);
+          found_m |= is_mkey;
+          put(0); put(p0); put((uint32_t)__popcll(snap));
+          for (uint64_t x = snap; x; x &= x - 1) put((uint32_t)__builtin_ctzll(x));
+          nk++;
+        }
+      }
+      mok = mok && (!mli || found_m) && nk < 128 && mcap >= 5;
+      if (mok) {
+        mo[0] = 'A'; mo[1] = 'M'; mo[2] = 'M'; mo[3] = '1'; mo[4] = (uint8_t)nk;
+        mbytes = w;
+      }
+    }
+    pbad |= !mok;
+    mbytes = uni(__shfl(mbytes, 0, 64));
+  }
+  if (__any(pbad)) return false;
+
   // ---- write ----
   uint8_t* const o = out + sizeof(PatchHdr2);
   if (b_act) {
@@ -1034,7 +1136,7 @@ __device__ __forceinline__ bool fast_diff(const uint8_t* IN, uint8_t* PS, uint32
   }
   if (l == 0) {
     PatchHdr2 h;
-    h.magic = AM_PATCH_MAGIC; h.status = 0; h.arg0 = 0; h.arg1 = 0; h.max_op = 0; h.nbytes = base; h.meta_bytes = 0;
+    h.magic = AM_PATCH_MAGIC; h.status = 0; h.arg0 = 0; h.arg1 = 0; h.max_op = 0; h.nbytes = base; h.meta_bytes = mbytes;
     *reinterpret_cast<PatchHdr2*>(out) = h;
   }
   return true;
@@ -2457,9 +2559,20 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   }
   FPH(13);
   if (!kDiff && b.P) return;  // launched without the patch writers: k_doc writes the log
-  if (kDiff && b.P == 2 && !fast_diff(IN, S + F.cells, F.ob_cap, wsg + L.pwire, L.pwire_cap, M, R, nb, NOUT, NA, NC, nbc, N,
-                                     OUTC, OUTA, RO, chh))
-    return;  // outside the shapes fast_diff covers: k_doc replays the patch (am_diff.h)
+  if (kDiff && b.P == 2) {
+    // AM_DOC_META: the handle's objectMeta blob (an AM_CHUNK_RAW chunk), or documentPatch's
+    const bool meta = (dd.flags & AM_DOC_META) != 0;
+    const uint8_t* mblob = nullptr;
+    uint32_t mlen = 0;
+    if (meta && dd.meta_chunk) {
+      const am_chunk_desc mc = chunks[dd.meta_chunk - 1];
+      mblob = arena + mc.off;
+      mlen = mc.len;
+    }
+    if (!fast_diff(IN, S + F.cells, F.ob_cap, wsg + L.pwire, L.pwire_cap, M, R, nb, NOUT, NA, NC, nbc, N, OUTC, OUTA, RO, chh,
+                   meta, mblob, mlen))
+      return;  // outside the shapes fast_diff covers: k_doc replays the patch (am_diff.h)
+  }
   if (kDiff && b.P == 1 && !fast_getpatch(IN, S + F.cells, F.ob_cap, wsg + L.pwire, L.pwire_cap, M, NOUT, NSUCC, NA, NC, nbc,
                                           N, OUTC, OUTA, RO, chh))
     return;  // outside the shapes fast_getpatch covers: k_doc writes the log (P7, am_patch.h)

@@ -1116,6 +1116,57 @@ void am_launch_scan(const uint64_t* in, uint64_t* out, uint64_t* tmp, uint32_t n
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, tmp, nblk, total);
   hipLaunchKernelGGL(k_scan_add, dim3(nblk), dim3(SCAN_T), 0, s, out, tmp, n);
 }
+// Packed batch descriptors (am_pipe_submit_packed): 4 B per chunk and 8 B per document cross the
+// host link; the chunk offsets and each document's first chunk are two exclusive scans on the device.
+__global__ void __launch_bounds__(256) k_unpack_counts(const uint32_t* __restrict__ clen, uint32_t nchunks,
+                                                       const am_doc_span* __restrict__ spans, uint32_t ndocs,
+                                                       uint64_t* __restrict__ c64, uint64_t* __restrict__ d64) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nchunks) c64[i] = clen[i];
+  if (i < ndocs) d64[i] = (uint64_t)spans[i].chg_count + (spans[i].has_base ? 1u : 0u);
+}
+// A chunk that runs past the arena is cut at its end (k_chunks then reports the truncated container)
+// and a document whose chunks run past the batch keeps those it has: a wrong descriptor becomes a
+// per-document error, never an out-of-bounds read.
+__global__ void __launch_bounds__(256) k_unpack_write(const uint32_t* __restrict__ clen, const uint64_t* __restrict__ coff,
+                                                      uint32_t nchunks, uint64_t arena_len, const am_doc_span* __restrict__ spans,
+                                                      const uint64_t* __restrict__ dbeg, uint32_t ndocs,
+                                                      am_chunk_desc* __restrict__ chunks, am_doc_desc* __restrict__ docs) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nchunks) {
+    const uint64_t off = coff[i];
+    am_chunk_desc c;
+    c.off = off < arena_len ? off : arena_len;
+    c.len = off >= arena_len ? 0u : (uint32_t)(clen[i] < arena_len - off ? clen[i] : arena_len - off);
+    c.flags = 0;
+    chunks[i] = c;
+  }
+  if (i < ndocs) {
+    const am_doc_span sp = spans[i];
+    const uint64_t b = dbeg[i];
+    const uint32_t hb = sp.has_base ? 1u : 0u;
+    am_doc_desc d;
+    const uint64_t first = b < nchunks ? b : nchunks;
+    d.base_chunk = hb && first < nchunks ? (int64_t)first : -1;
+    d.chg_begin = (uint32_t)(first + hb < nchunks ? first + hb : nchunks);
+    d.chg_count = (uint32_t)(d.chg_begin + (uint64_t)sp.chg_count <= nchunks ? sp.chg_count : nchunks - d.chg_begin);
+    d.known_begin = d.known_count = 0;
+    d.flags = sp.flags & ~(uint32_t)AM_DOC_META;
+    d.meta_chunk = 0;
+    docs[i] = d;
+  }
+}
+void am_launch_unpack(const uint32_t* clen, uint32_t nchunks, uint64_t arena_len, const am_doc_span* spans, uint32_t ndocs,
+                      uint64_t* c64, uint64_t* coff, uint64_t* ctmp, uint64_t* d64, uint64_t* dbeg, uint64_t* dtmp,
+                      uint64_t* totals2, am_chunk_desc* chunks, am_doc_desc* docs, hipStream_t s) {
+  const uint32_t n = nchunks > ndocs ? nchunks : ndocs;
+  if (!n) return;
+  hipLaunchKernelGGL(k_unpack_counts, dim3((n + 255) / 256), dim3(256), 0, s, clen, nchunks, spans, ndocs, c64, d64);
+  am_launch_scan(c64, coff, ctmp, nchunks, totals2, s);
+  am_launch_scan(d64, dbeg, dtmp, ndocs, totals2 + 1, s);
+  hipLaunchKernelGGL(k_unpack_write, dim3((n + 255) / 256), dim3(256), 0, s, clen, coff, nchunks, arena_len, spans, dbeg, ndocs,
+                     chunks, docs);
+}
 // per document: 16-byte-rounded lengths of its merged chunk and of its patch log (wire form)
 __global__ void __launch_bounds__(256) k_pipe_lens(const am_doc_result* __restrict__ res, const DocBounds* __restrict__ bounds,
                                                    const uint8_t* __restrict__ ws, uint32_t ndocs, uint64_t* __restrict__ olen,

@@ -48,6 +48,11 @@ void am_launch_digest(const BatchDev& b, uint64_t first, uint64_t* d_out, hipStr
 void am_launch_sha256(const uint8_t* arena, const am_chunk_desc* msgs, uint32_t n, uint8_t* out, hipStream_t s);
 size_t am_scan_tmp_elems(uint32_t n);
 void am_launch_scan(const uint64_t* in, uint64_t* out, uint64_t* tmp, uint32_t n, uint64_t* total, hipStream_t s);
+// packed batch descriptors (am_pipe_submit_packed) expanded into am_chunk_desc / am_doc_desc;
+// c64/coff/ctmp: chunk scan buffers, d64/dbeg/dtmp: document scan buffers, totals2: 2 scratch u64
+void am_launch_unpack(const uint32_t* clen, uint32_t nchunks, uint64_t arena_len, const am_doc_span* spans, uint32_t ndocs,
+                      uint64_t* c64, uint64_t* coff, uint64_t* ctmp, uint64_t* d64, uint64_t* dbeg, uint64_t* dtmp,
+                      uint64_t* totals2, am_chunk_desc* chunks, am_doc_desc* docs, hipStream_t s);
 // pipelined batches: dense arenas of merged documents / patch logs + per-document summaries;
 // totals[0..1] = bytes of the two arenas
 void am_launch_pipe_compact(const BatchDev& b, uint64_t* olen, uint64_t* ooff, uint64_t* plen, uint64_t* poff, uint64_t* tmp,

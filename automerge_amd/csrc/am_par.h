@@ -7,6 +7,8 @@
 #include <algorithm>
 #include <atomic>
 #include <thread>
+#include <exception>
+#include <mutex>
 #include <vector>
 
 inline unsigned am_host_threads() {
@@ -22,16 +24,29 @@ void am_par_for(size_t n, F f) {
     for (size_t i = 0; i < n; i++) f(i);
     return;
   }
+  // an exception on a worker (std::bad_alloc, ...) stops the loop and is rethrown on the calling
+  // thread after the join, as the serial loop would throw it, instead of std::terminate
   std::atomic<size_t> next{0};
+  std::atomic<bool> stop{false};
+  std::exception_ptr first;
+  std::mutex mu;
   auto work = [&]() {
     for (;;) {
       const size_t i0 = next.fetch_add(64);
-      if (i0 >= n) return;
-      for (size_t i = i0; i < std::min(n, i0 + 64); i++) f(i);
+      if (i0 >= n || stop.load(std::memory_order_relaxed)) return;
+      try {
+        for (size_t i = i0; i < std::min(n, i0 + 64); i++) f(i);
+      } catch (...) {
+        std::lock_guard<std::mutex> g(mu);
+        if (!first) first = std::current_exception();
+        stop = true;
+        return;
+      }
     }
   };
   std::vector<std::thread> th;
   for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
   work();
   for (auto& x : th) x.join();
+  if (first) std::rethrow_exception(first);
 }

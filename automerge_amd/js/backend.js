@@ -423,11 +423,34 @@ function partition(items, prep) {
   return [idx, vals, out]
 }
 
+// A backend named more than once: as sequential calls. run(items) takes the first occurrence of each
+// backend; a later one runs in a following round, where a handle its earlier call froze throws the
+// outdated-document error in its own slot (util.js:1-10) and a handle whose earlier call failed
+// (unchanged) is applied.
+function rounds(backends, run) {
+  const out = new Array(backends.length)
+  let pending = backends.map((_, i) => i)
+  while (pending.length > 0) {
+    const seen = new Set(), now = [], later = []
+    for (const i of pending) {
+      const b = backends[i]
+      if (b && typeof b === 'object' && seen.has(b)) later.push(i)
+      else { now.push(i); if (b && typeof b === 'object') seen.add(b) }
+    }
+    run(now).forEach((r, k) => { out[now[k]] = r })
+    pending = later
+  }
+  return out
+}
+
 function loadBatch(datas) {
   return native.docLoadBatch(datas).map(r => r instanceof Error ? r : {state: r, heads: native.docHeads(r)})
 }
 
 function applyBatch(backends, changeLists, wantPatch) {
+  return rounds(backends, items => applyOnce(items.map(i => backends[i]), items.map(i => changeLists[i]), wantPatch))
+}
+function applyOnce(backends, changeLists, wantPatch) {
   const [idx, states, out] = partition(backends, b => backendState(b))
   const res = native.docApplyBatch(states, idx.map(i => changeLists[i]), wantPatch)
   res.forEach((r, k) => {
@@ -476,6 +499,10 @@ function generateSyncMessages(backends, syncStates) {
 }
 
 function receiveSyncMessages(backends, oldSyncStates, binaryMessages) {
+  return rounds(backends, items => receiveOnce(items.map(i => backends[i]), items.map(i => oldSyncStates[i]),
+                                               items.map(i => binaryMessages[i])))
+}
+function receiveOnce(backends, oldSyncStates, binaryMessages) {
   const [idx, vals, out] = partition(backends, (b, i) => {
     if (!b) throw new Error('generateSyncMessage called with no Automerge document')
     if (!oldSyncStates[i]) throw new Error('generateSyncMessage requires a syncState, which can be created with initSyncState()')

@@ -21,9 +21,35 @@ import numpy as np
 from . import _native as N
 from .batch import CHUNK_DT, DOC_DT
 
+DOC_META = 32  # AM_DOC_META: not accepted by a packed batch
+# am_doc_span (am_pipe_submit_packed): change chunks, am_doc_desc flags, base-document bit
+SPAN_DT = np.dtype([("chg_count", "<u4"), ("flags", "<u2"), ("has_base", "u1"), ("reserved", "u1")])
 SUMMARY_DT = np.dtype([("status", "<u4"), ("nqueued", "<u4"), ("out_len", "<u4"), ("patch_len", "<u4"),
                        ("out_off", "<u8"), ("patch_off", "<u8")])
 assert SUMMARY_DT.itemsize == C.sizeof(N.DocSummary)
+
+
+def pack(chunks, docs):
+    """(chunk_len, spans) of am_pipe_submit_packed for full descriptors whose chunks lie back to back
+    from arena offset 0 and whose documents take consecutive chunks (base first), or None when the
+    batch does not have that shape (then use submit)."""
+    off = chunks["off"].astype(np.int64)
+    ln = chunks["len"].astype(np.int64)
+    if len(chunks) and (off[0] != 0 or np.any(off[1:] != off[:-1] + ln[:-1]) or np.any(chunks["flags"] != 0)):
+        return None
+    hb = docs["base_chunk"] >= 0
+    cnt = docs["chg_count"].astype(np.int64)
+    first = np.concatenate([[0], np.cumsum(hb.astype(np.int64) + cnt)[:-1]]) if len(docs) else np.zeros(0, np.int64)
+    if (np.any(hb & (docs["base_chunk"] != first)) or np.any(docs["chg_begin"] != first + hb)
+            or np.any(docs["known_count"] != 0) or np.any(docs["flags"] >= (1 << 16))
+            or np.any(docs["flags"] & DOC_META)
+            or (len(docs) and first[-1] + hb[-1] + cnt[-1] != len(chunks))):
+        return None
+    spans = np.zeros(len(docs), SPAN_DT)
+    spans["chg_count"] = cnt
+    spans["flags"] = docs["flags"]
+    spans["has_base"] = hb
+    return ln.astype(np.uint32), spans
 
 
 class Pinned:
@@ -86,6 +112,27 @@ class Pipeline:
             N.raise_for(err)
         self._keep[t.value] = (arena, chunks, docs, summary, out, patches)
         return t.value
+
+    def submit_packed(self, arena, chunk_len, spans, summary, out, patches):
+        """Enqueues one batch with packed descriptors (am_pipe_submit_packed): `arena` holds the chunks
+        back to back in chunk order, `chunk_len` (u32) their lengths, `spans` (SPAN_DT) one entry per
+        document whose chunks (base first when has_base) follow those of the previous document."""
+        assert chunk_len.dtype == np.uint32 and spans.dtype == SPAN_DT and summary.dtype == SUMMARY_DT
+        assert len(summary) >= len(spans)
+        t = C.c_uint64()
+        err = N.Error()
+        if N.lib.am_pipe_submit_packed(self._p, arena.ctypes.data, arena.nbytes, chunk_len.ctypes.data, len(chunk_len),
+                                       spans.ctypes.data, len(spans), summary.ctypes.data, out.ctypes.data, out.nbytes,
+                                       patches.ctypes.data, patches.nbytes, C.byref(t), C.byref(err)):
+            N.raise_for(err)
+        self._keep[t.value] = (arena, chunk_len, spans, summary, out, patches)
+        return t.value
+
+    def engines(self):
+        """SDMA engine masks of the host-link copies: (H2D, copies home); 0 = the runtime's choice."""
+        m = (C.c_uint32 * 2)()
+        N.lib.am_pipe_engines(self._p, m)
+        return int(m[0]), int(m[1])
 
     def drain(self, nbatches=0):
         """Waits for every submitted batch; returns [(output bytes, patch bytes)] of the batches

@@ -8,15 +8,18 @@ list inserts + 1 conflicting title set each): 13 changes, 60 ops merged, ~2.1 KB
 document's SHA-256 (the container checksum) mod N, so N GPUs split the same job (strong scaling).
 
 A step is the whole job of a rank from host memory back to host memory, as a caller of the engine
-sees it: every batch of its shard goes through am_pipe_* (include/automerge_amd.h) -- H2D of the
-encoded chunks, SHA-256 of every chunk, header parse, causal queue, column decode, merge
-(sort / RGA / succ), canonical re-encode, checksum, the patch Backend.applyChanges returns (wire
-form of am_patch.h), compaction, and D2H of the merged documents, patches and per-document
-summaries. Copies of batch k+1 / k-1 overlap the kernels of batch k. Materializing the patches as
-JS objects is the host's job and is not timed here (it is reported separately by tools/).
+sees it ("load + applyChanges (batched, H2D included)"): every batch of its shard goes
+through am_pipe_submit_packed (include/automerge_amd.h) -- H2D of the encoded chunks and of 4 B per
+chunk + 8 B per document of descriptors (the chunk / document tables are expanded on the device),
+SHA-256 of every chunk, header parse, causal queue, column decode, merge (sort / RGA / succ),
+canonical re-encode, checksum, the patch Backend.applyChanges returns (wire form of am_patch.h),
+compaction, and D2H of the merged documents, patches and per-document summaries. Copies of batch
+k+1 / k-1 overlap the kernels of batch k. This is `value`. The same chain with the inputs already in
+HBM (am_pipe_run_resident) is reported beside it as `hbm_resident` and is never `value`.
+Materializing the patches as JS objects is the host's job and is not timed here (tools/).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--docs D] [--batch B] [--slots S]
-  python bench.py --mode resident [--workload c4|c2] --docs D   # inputs resident in HBM (kernels only)
+  python bench.py --mode resident [--workload c4|c2] --docs D   # value = the HBM-resident chain (not the contract)
 """
 import argparse
 import json
@@ -33,35 +36,46 @@ CPU_REF_JSON = os.path.join(ROOT, "profiles", "cpu_reference_node.json")
 
 
 def _oracle_sample(args):
-    """load + applyChanges + save of documents [lo, hi) of the bench's arrays by the oracle for at most
-    `seconds`; returns (documents done, seconds)."""
-    arena, chunks, docs, lo, hi, seconds = args
+    """load + applyChanges + save by the oracle of the workload's documents from index `first` on,
+    generated here in blocks of 1024, for at most `seconds`; returns (documents done, seconds)."""
+    wl, first, seconds = args
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as O
     import workload
+    gen = workload.c4 if wl == "c4" else workload.c2
     n = 0
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds and lo + n < hi:
-        base, changes = workload.doc_chunks(arena, chunks, docs, lo + n)
-        d = O.Doc.load(base) if base else O.Doc.init()
-        d.apply(changes)
-        d.save()
-        n += 1
+    while time.perf_counter() - t0 < seconds:
+        arena, chunks, docs, _ = gen(first + n, 1024, nthreads=1)
+        for i in range(len(docs)):
+            base, changes = workload.doc_chunks(arena, chunks, docs, i)
+            d = O.Doc.load(base) if base else O.Doc.init()
+            d.apply(changes)
+            d.save()
+            n += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
     return n, time.perf_counter() - t0
 
 
-def cpu_baseline(arena, chunks, docs, seconds=6.0, ops_per_doc=60, name="C4", procs=None):
-    """The oracle (CPU restatement of the reference algorithm, oracle/) timed on the host over a
-    bounded sample of the same documents: ops merged per second (load + applyChanges + save), on one
-    core and on `procs` cores at once (one process each, disjoint documents)."""
+def cpu_pool(procs):
+    """The worker processes of the all-cores CPU baseline, forked before this process touches the
+    GPU or imports torch (a fork of a GPU-initialised process is not safe on this pool)."""
     import multiprocessing as mp
-    procs = procs or min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16 per GPU
-    n1, t1 = _oracle_sample((arena, chunks, docs, 0, len(docs), seconds))
-    per = max(1, len(docs) // procs)
-    with mp.get_context("fork").Pool(procs) as pool:
-        res = pool.map(_oracle_sample, [(arena, chunks, docs, k * per, (k + 1) * per, seconds) for k in range(procs)])
+    return mp.get_context("fork").Pool(procs)
+
+
+def cpu_baseline(pool, procs, wl, seconds=6.0, ops_per_doc=60):
+    """The oracle (CPU restatement of the reference algorithm, oracle/) timed on the host over a
+    bounded sample of the same workload: ops merged per second (load + applyChanges + save), on one
+    core and on `procs` cores at once (one process each, disjoint documents)."""
+    n1, t1 = _oracle_sample((wl, 0, seconds))
+    res = pool.map(_oracle_sample, [(wl, k * 50000, seconds) for k in range(procs)])
+    pool.close()
+    pool.join()
     nall = sum(r[0] for r in res)
     tall = max(r[1] for r in res)
+    name = wl.upper()
     return {"value": n1 * ops_per_doc / t1, "unit": "ops/s", "cores": 1, "kind": "port", "host_cpus": os.cpu_count(),
             "sample": "%d %s documents (load + applyChanges + save) by oracle/liboracle.so, 1 thread, %.1f s" % (n1, name, t1),
             "all_cores": {"value": nall * ops_per_doc / tall, "unit": "ops/s", "cores": procs,
@@ -158,9 +172,10 @@ def main():
     ap.add_argument("--docs", type=int, default=1 << 20, help="documents of the whole job (sharded over the ranks)")
     ap.add_argument("--batch", type=int, default=0, help="documents per pipeline batch (0: auto)")
     ap.add_argument("--slots", type=int, default=3, help="batches in flight")
-    ap.add_argument("--mode", choices=["resident", "pipe"], default="resident",
-                    help="resident: inputs in HBM when the timed region starts (the `value`); pipe: from host memory")
-    ap.add_argument("--no-pcie", action="store_true", help="resident mode: skip the PCIe-inclusive pipe run")
+    ap.add_argument("--mode", choices=["pipe", "resident"], default="pipe",
+                    help="pipe: from host memory back to host memory (the `value`); resident: inputs in HBM")
+    ap.add_argument("--no-resident", action="store_true", help="pipe mode: skip the HBM-resident run reported beside it")
+    ap.add_argument("--full-desc", action="store_true", help="pipe mode: send full chunk / document descriptors")
     ap.add_argument("--workload", choices=["c4", "c2"], default="c4")
     ap.add_argument("--no-patch", action="store_true", help="merge without the applyChanges patch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -169,6 +184,9 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # the CPU baseline's workers are forked now, before torch is imported or the GPU is touched
+    procs = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16 per GPU
+    pool = cpu_pool(procs) if rank == 0 and not args.no_cpu_baseline else None
     # AM_BENCH_DEVICE / AM_DIST_BACKEND=gloo: every rank on one GPU with a CPU exchange (the N>1
     # rehearsal of tests/test_gpu_bench_ranks.py; RCCL refuses two ranks on one device)
     local = int(os.environ.get("AM_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
@@ -176,12 +194,14 @@ def main():
     import numpy as np
     import torch
     dist = None
+    dist_info = {"world_size": 1, "backend": None}
     if world > 1:
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend=backend)
+        dist_info = {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()), "rank": dist.get_rank()}
     torch.cuda.set_device(local)
     xdev = "cuda" if backend == "nccl" else "cpu"
 
@@ -230,18 +250,27 @@ def main():
     nb = len(parts)
     in_b = int(arena.nbytes)
     starts = np.cumsum([0] + [len(p[2]) for p in parts])
+    packed = [None if args.full_desc else pipe.pack(c, d) for _, c, d in parts]
+    desc_b = sum(int(k[0].nbytes + k[1].nbytes) if k is not None else int(c.nbytes + d.nbytes)
+                 for k, (_, c, d) in zip(packed, parts))
 
     def run_pipe(steps, warmup):
-        """The job from host memory back to host memory (am_pipe_submit / drain): PCIe-inclusive."""
-        pin_in = [(pipe.pinned_copy(a), pipe.pinned_copy(c), pipe.pinned_copy(d)) for a, c, d in parts]
+        """The job from host memory back to host memory (am_pipe_submit_packed / drain)."""
+        pin_in = []
+        for (a, c, d), k in zip(parts, packed):
+            desc = (pipe.pinned_copy(k[0]), pipe.pinned_copy(k[1])) if k is not None else (pipe.pinned_copy(c), pipe.pinned_copy(d))
+            pin_in.append((pipe.pinned_copy(a), desc, k is not None))
         pin_out = []
         for a, c, d in parts:
             sb = pipe.Pinned(len(d) * pipe.SUMMARY_DT.itemsize)
             pin_out.append((sb, sb.view(pipe.SUMMARY_DT, len(d)), pipe.Pinned(out_cap), pipe.Pinned(patch_cap)))
 
         def step():
-            for (pa, pc, pd), (_, summ, po, pp) in zip(pin_in, pin_out):
-                pl.submit(pa.arr, pc.arr, pd.arr, summ, po.u8, pp.u8)
+            for (pa, (p1, p2), is_packed), (_, summ, po, pp) in zip(pin_in, pin_out):
+                if is_packed:
+                    pl.submit_packed(pa.arr, p1.arr, p2.arr, summ, po.u8, pp.u8)
+                else:
+                    pl.submit(pa.arr, p1.arr, p2.arr, summ, po.u8, pp.u8)
             return pl.drain(nb)
 
         for _ in range(warmup):
@@ -256,11 +285,11 @@ def main():
         barrier()
         el = time.perf_counter() - t0
         ms_c, ms_d, nt = pl.times()
-        return el, totals, pin_out, ms_c, ms_d / max(nt, 1)
+        return el, totals, pin_out, ms_c / max(steps, 1), ms_d / max(nt, 1)
 
-    if args.mode == "resident":
-        # inputs resident in HBM (copied before the timed region); each step runs every batch of the
-        # shard through the whole chain (am_pipe_run_resident), outputs compacted in HBM
+    def run_resident(steps, warmup):
+        """Inputs resident in HBM (copied before the timed region); each step runs every batch of the
+        shard through the whole chain (am_pipe_run_resident), outputs compacted in HBM."""
         dev = []
         for a, c, d in parts:
             ta = torch.zeros(len(a) + 64, dtype=torch.uint8, device="cuda")
@@ -280,67 +309,75 @@ def main():
                                 ts.data_ptr(), to.data_ptr(), out_cap, tp.data_ptr(), patch_cap, tt.data_ptr())
             return pl.resident_sync()
 
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             step()
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ms_comp = ms_doc = 0.0
-        for _ in range(args.steps):
+        for _ in range(steps):
             a_, d_ = step()
             ms_comp += a_
             ms_doc += d_
         torch.cuda.synchronize()
         barrier()
-        elapsed = time.perf_counter() - t0
+        el = time.perf_counter() - t0
         # results home (outside the timed region): summaries, merged documents, patch logs
         summ_b = [x[6].cpu().numpy().view(pipe.SUMMARY_DT) for x in dev]
         tot_b = [x[9].cpu().numpy() for x in dev]
         outs_b = [x[7][:int(t[0])].cpu().numpy() for x, t in zip(dev, tot_b)]
         pats_b = [x[8][:int(t[1])].cpu().numpy() for x, t in zip(dev, tot_b)]
-        out_bytes = int(sum(int(t[0]) for t in tot_b))
-        patch_bytes = int(sum(int(t[1]) for t in tot_b))
-        summ_all = np.concatenate(summ_b)
-        t_doc = ms_doc / (args.steps * nb)
-        extra["kernel_ms_per_step"] = ms_comp / args.steps
-        extra["batches"] = nb
-        extra["batch_docs"] = batch
         del dev
-        if not args.no_pcie:
-            # the same job from host memory (H2D + chain + D2H, pipelined): PCIe-inclusive, never `value`
-            el_p, _, _, _, _ = run_pipe(max(2, args.steps // 2), 1)
-            sp = max(2, args.steps // 2)
-            hb = torch.empty(min(in_b, 1 << 30), dtype=torch.uint8).pin_memory()
-            db = torch.empty_like(hb, device="cuda")
-            db.copy_(hb, non_blocking=True)
-            torch.cuda.synchronize()
-            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-            e0.record()
-            db.copy_(hb, non_blocking=True)
-            e1.record()
-            hb.copy_(db, non_blocking=True)
-            e2.record()
-            torch.cuda.synchronize()
-            extra["pcie_inclusive"] = {
-                "what": "the same job from pinned host memory back to host memory through am_pipe_submit (H2D of "
-                        "arena + descriptors, chain, D2H of documents, patches, summaries; pipelined)",
-                "ops_per_s_rank0": ops_rank / (el_p / sp), "ms_per_step": el_p * 1000.0 / sp, "steps": sp,
-                "pcie_GBps": {"h2d": hb.numel() / (e0.elapsed_time(e1) * 1e-3) / 1e9,
-                              "d2h": hb.numel() / (e1.elapsed_time(e2) * 1e-3) / 1e9},
-                "bytes_per_step_rank0": {"h2d": in_b + int(chunks.nbytes) + int(docs.nbytes),
-                                         "d2h": out_bytes + patch_bytes + D * pipe.SUMMARY_DT.itemsize}}
-            del hb, db
-    else:
+        return el, summ_b, outs_b, pats_b, [(int(t[0]), int(t[1])) for t in tot_b], ms_comp / steps, ms_doc / (steps * nb)
+
+    def pcie_rates():
+        """One 1 GB pinned H2D and D2H copy each (torch's copies, the link's plain rate)."""
+        hb = torch.empty(min(in_b, 1 << 30), dtype=torch.uint8).pin_memory()
+        db = torch.empty_like(hb, device="cuda")
+        db.copy_(hb, non_blocking=True)
+        torch.cuda.synchronize()
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
+        db.copy_(hb, non_blocking=True)
+        e1.record()
+        hb.copy_(db, non_blocking=True)
+        e2.record()
+        torch.cuda.synchronize()
+        return {"h2d": hb.numel() / (e0.elapsed_time(e1) * 1e-3) / 1e9, "d2h": hb.numel() / (e1.elapsed_time(e2) * 1e-3) / 1e9}
+
+    extra["batches"] = nb
+    extra["batch_docs"] = batch
+    if args.mode == "pipe":
         elapsed, totals, pin_out, ms_comp, t_doc = run_pipe(args.steps, args.warmup)
         summ_b = [o[1] for o in pin_out]
         outs_b = [o[2].u8 for o in pin_out]
         pats_b = [o[3].u8 for o in pin_out]
         out_bytes = sum(t[0] for t in totals[:nb])
         patch_bytes = sum(t[1] for t in totals[:nb])
-        summ_all = np.concatenate(summ_b)
-        extra["kernel_ms_per_step"] = ms_comp / args.steps
-        extra["batches"] = nb
-        extra["batch_docs"] = batch
+        extra["kernel_ms_per_step"] = ms_comp
+        h2d = in_b + desc_b
+        d2h = out_bytes + patch_bytes + D * pipe.SUMMARY_DT.itemsize
+        rates = pcie_rates()
+        e_h2d, e_home = pl.engines()
+        extra["host_link"] = {
+            "bytes_per_step_rank0": {"h2d": h2d, "d2h": d2h, "descriptors": desc_b,
+                                     "packed_batches": sum(k is not None for k in packed)},
+            "GBps_alone": rates, "sdma_engine_mask": {"h2d": e_h2d, "home": e_home},
+            "h2d_ms": h2d / (rates["h2d"] * 1e9) * 1e3, "d2h_ms": d2h / (rates["d2h"] * 1e9) * 1e3,
+            "ms_per_step_over_max_h2d_kernels": (elapsed * 1000.0 / args.steps) / max(h2d / (rates["h2d"] * 1e9) * 1e3, ms_comp)}
+        if not args.no_resident:
+            el_r, _, _, _, tot_r, msc_r, msd_r = run_resident(max(2, args.steps), 1)
+            sr = max(2, args.steps)
+            extra["hbm_resident"] = {
+                "what": "the same chain with the inputs already in HBM (am_pipe_run_resident), outputs left in HBM; never `value`",
+                "ops_per_s_rank0": ops_rank / (el_r / sr), "ms_per_step": el_r * 1000.0 / sr, "steps": sr,
+                "kernel_ms_per_step": msc_r, "doc_kernel_ms_per_batch": msd_r}
+    else:
+        elapsed, summ_b, outs_b, pats_b, tot_b, ms_comp, t_doc = run_resident(args.steps, args.warmup)
+        out_bytes = sum(t[0] for t in tot_b)
+        patch_bytes = sum(t[1] for t in tot_b)
+        extra["kernel_ms_per_step"] = ms_comp
+    summ_all = np.concatenate(summ_b)
     statuses = summ_all["status"]
     alg_launch = (in_b + out_bytes + patch_bytes) / nb
     workspace = int(ws_need)
@@ -387,6 +424,7 @@ def main():
     if rank != 0:
         dist.destroy_process_group() if dist is not None else None
         return
+    extra["dist"] = dist_info
     ms_per_step = elapsed * 1000.0 / args.steps
     value = tot[1] / (elapsed / args.steps)
     achieved = alg_launch / (t_doc * 1e-3) / 1e9 if t_doc else None
@@ -402,7 +440,7 @@ def main():
         extra["decode_bytes_per_doc"] = {"input": din, "soa": dsoa}
     if tr is not None and t_doc:
         extra["fetch_GBps"] = 2 * tr["fetch_size_kib"] * 1024 / (t_doc * 1e-3) / 1e9  # measured HBM reads (PMC)
-    cpu = None if args.no_cpu_baseline else cpu_baseline(arena, chunks, docs, ops_per_doc=per_doc, name=args.workload.upper())
+    cpu = cpu_baseline(pool, procs, args.workload, ops_per_doc=per_doc) if pool is not None else None
     # the whole job against the oracle's digest of every document (tests/golden/c4_digest.json)
     want = pinned_digest(tot[0]) if args.workload == "c4" and digest is not None else None
     if want is not None:
@@ -410,8 +448,8 @@ def main():
                                   "how": "oracle load + applyChanges + save of all %d documents (tools/pin_c4_digest.py)" % tot[0]}
     wl = {"c4": "C4 1M-document job: load base doc + applyChanges of 12 concurrent changes (4 actors x 3), 60 ops/doc",
           "c2": "C2: applyChanges of 3 changes (10 map/counter/string sets + 2 concurrent inc/overwrite), 14 ops/doc"}
-    what = ("H2D + merge + applyChanges patch + D2H (pipelined)" if args.mode == "pipe" else
-            "inputs resident in HBM: merge + applyChanges patch + compaction in HBM, all 16 batch chains per step")
+    what = ("from host memory: H2D + merge + applyChanges patch + D2H (pipelined)" if args.mode == "pipe" else
+            "inputs resident in HBM: merge + applyChanges patch + compaction in HBM (not the contract metric)")
     if args.no_patch:
         what = what.replace(" + applyChanges patch", "")
     line = {

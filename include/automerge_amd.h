@@ -218,6 +218,10 @@ int am_batch_digest(am_batch *b, uint64_t first_doc, uint64_t *digest);
 /* Per document of the last run: 1 when the small-document kernel (k_doc_fast) merged it, 0 when
  * the general kernel did (documents outside its envelope, errors, getPatch requests). */
 int am_batch_fast_flags(am_batch *b, uint8_t *flags);
+/* Diagnostics of the batched per-handle calls since the last call (reset on read): out2[0] documents
+ * run, out2[1] of them merged by the small-document kernel k_doc_fast. Not part of the reference
+ * interface. */
+int am_engine_stats(am_engine *e, uint64_t *out2);
 /* Device pointer + size of the staged arena / merged outputs (for bench byte accounting). */
 uint64_t am_batch_workspace_bytes(am_batch *b);
 /* Launch shape of the staged batch's document kernels: out3[0] = k_doc dynamic LDS bytes,
@@ -270,6 +274,25 @@ void am_pipe_destroy(am_pipe *p);
 int am_pipe_submit(am_pipe *p, const uint8_t *arena, uint64_t arena_len, const am_chunk_desc *chunks, uint32_t nchunks,
                    const am_doc_desc *docs, uint32_t ndocs, am_doc_summary *summary, uint8_t *out, uint64_t out_cap,
                    uint8_t *patches, uint64_t patch_cap, uint64_t *ticket, am_error *err);
+/* am_pipe_submit with packed descriptors: the arena holds the batch's chunks back to back in chunk
+ * order and chunk_len[c] is the length of chunk c; a document's chunks are consecutive (its saved
+ * base document first when has_base, then its chg_count change chunks), in document order. The
+ * device derives the am_chunk_desc / am_doc_desc arrays (two scans), so the host link carries 4 B
+ * per chunk and 8 B per document of descriptors instead of 16 and 32. Same outputs and semantics as
+ * am_pipe_submit; AM_DOC_META is not accepted (no objectMeta chunks in a packed batch), and a
+ * length that runs past the arena is cut there (that chunk then fails its container check). */
+typedef struct am_doc_span {
+  uint32_t chg_count;               /* change chunks of the document */
+  uint16_t flags;                   /* am_doc_desc flags (AM_DOC_WANT_DIFF, AM_DOC_WANT_PATCH, ...) */
+  uint8_t has_base;                 /* 1: the first chunk is a saved document (Backend.load), 0: Backend.init() */
+  uint8_t reserved;
+} am_doc_span;
+int am_pipe_submit_packed(am_pipe *p, const uint8_t *arena, uint64_t arena_len, const uint32_t *chunk_len, uint32_t nchunks,
+                          const am_doc_span *docs, uint32_t ndocs, am_doc_summary *summary, uint8_t *out, uint64_t out_cap,
+                          uint8_t *patches, uint64_t patch_cap, uint64_t *ticket, am_error *err);
+/* The SDMA engines the pipeline's host-link copies run on (bit k = HSA_AMD_SDMA_ENGINE_k): [0] the
+ * H2D of the inputs, [1] the copies home; 0 = the runtime's choice / a copy kernel. */
+int am_pipe_engines(am_pipe *p, uint32_t *out2);
 /* Waits until every submitted batch is home. totals (optional, 2 per batch in submission order
  * since the last drain, up to cap batches): output / patch arena bytes. */
 int am_pipe_drain(am_pipe *p, uint64_t *totals, uint32_t cap, am_error *err);
@@ -280,7 +303,8 @@ int am_pipe_drain(am_pipe *p, uint64_t *totals, uint32_t cap, am_error *err);
  * summaries are compacted into d_out / d_patches / d_summary (layout of am_pipe_submit) and their
  * two arena totals into d_totals; nothing crosses the host link and the call does not wait.
  * am_pipe_resident_sync waits for the stream; ms2 = the chains / document kernels of the resident
- * batches since its last call, summed (HIP events). */
+ * batches since its last call, summed (HIP events). Resident batches share slot 0's workspace: at
+ * most 4096 run between two syncs, and am_pipe_submit refuses work while any is unsynced. */
 int am_pipe_run_resident(am_pipe *p, const uint8_t *d_arena, uint64_t arena_len, const am_chunk_desc *d_chunks,
                          uint32_t nchunks, const am_doc_desc *d_docs, uint32_t ndocs, int any_diff, am_doc_summary *d_summary,
                          uint8_t *d_out, uint64_t out_cap, uint8_t *d_patches, uint64_t patch_cap, uint64_t *d_totals,

@@ -301,3 +301,44 @@ def test_fast_and_general_getpatch_writers_agree(docs, objmeta):
     bad = [i for i in range(len(items)) if pf[i] != pg[i] or of[i] != og[i] or rf[i]["status"] != rg[i]["status"]]
     assert not bad, (int(flags.sum()), bad[:10])
     print("fast getPatch writer took %d of %d documents" % (int(flags.sum()), len(items)))
+
+
+def test_meta_handles_take_the_fast_kernel():
+    """Per-handle calls carry objectMeta (AM_DOC_META) and still run on k_doc_fast: C4 documents
+    loaded as handles, their 12 changes applied in two applyChangesBatch calls (the first starts from
+    documentPatch's snapshots, the second from the blob the first left). Patches, saved documents and
+    heads equal the general kernel's (AM_FAST=0, whose replay is pinned to the reference), and most
+    documents take the fast kernel."""
+    import os
+    import workload
+    from automerge_amd import _native as N
+    from automerge_amd import backend as B
+    arena, chunks, docs, _ = workload.c4(100, 400)
+    items = [workload.doc_chunks(arena, chunks, docs, i) for i in range(len(docs))]
+
+    def run(fast):
+        old = os.environ.get("AM_FAST")
+        os.environ["AM_FAST"] = "1" if fast else "0"
+        try:
+            N.engine_stats()
+            hs = B.loadBatch([base for base, _ in items])
+            r1 = B.applyChangesBatch(hs, [ch[:6] for _, ch in items])
+            r2 = B.applyChangesBatch([r[0] for r in r1], [ch[6:] for _, ch in items])
+            st = N.engine_stats()
+        finally:
+            if old is None:
+                del os.environ["AM_FAST"]
+            else:
+                os.environ["AM_FAST"] = old
+        out = []
+        for a, b in zip(r1, r2):
+            assert not isinstance(a, Exception) and not isinstance(b, Exception), (a, b)
+            out.append((_jsonable(a[1]), _jsonable(b[1]), B.save(b[0]).hex(), B.getHeads(b[0])))
+        return out, st
+
+    fast, st_fast = run(True)
+    slow, st_slow = run(False)
+    assert st_slow[1] == 0
+    assert st_fast[0] >= 2 * len(items) and st_fast[1] >= 0.9 * 2 * len(items), st_fast
+    bad = [i for i, (a, b) in enumerate(zip(fast, slow)) if a != b]
+    assert not bad, (len(bad), bad[:10])

@@ -17,8 +17,8 @@ def _parts(kind, first, n, batch, flags):
     return (arena, chunks, docs), bench.split_batches(arena, chunks, docs, batch)
 
 
-@pytest.mark.parametrize("kind", ["c4", "c2"])
-def test_pipeline_equals_batch_path(kind):
+@pytest.mark.parametrize("kind,packed", [("c4", False), ("c2", False), ("c4", True), ("c2", True)])
+def test_pipeline_equals_batch_path(kind, packed):
     from automerge_amd import pipe
     from automerge_amd.batch import WANT_DIFF, Batch
     whole, parts = _parts(kind, 40, 2500, 700, WANT_DIFF)
@@ -35,10 +35,15 @@ def test_pipeline_equals_batch_path(kind):
     for _ in range(2):  # the second pass reuses every slot
         keep = []
         for a, c, d in parts:
-            pa, pc, pd = pipe.pinned_copy(a), pipe.pinned_copy(c), pipe.pinned_copy(d)
             s = pipe.Pinned(len(d) * pipe.SUMMARY_DT.itemsize)
             po, pp = pipe.Pinned(1 << 20), pipe.Pinned(4 << 20)
-            pl.submit(pa.arr, pc.arr, pd.arr, s.view(pipe.SUMMARY_DT, len(d)), po.u8, pp.u8)
+            if packed:
+                cl, sp = pipe.pack(c, d)
+                pa, pc, pd = pipe.pinned_copy(a), pipe.pinned_copy(cl), pipe.pinned_copy(sp)
+                pl.submit_packed(pa.arr, pc.arr, pd.arr, s.view(pipe.SUMMARY_DT, len(d)), po.u8, pp.u8)
+            else:
+                pa, pc, pd = pipe.pinned_copy(a), pipe.pinned_copy(c), pipe.pinned_copy(d)
+                pl.submit(pa.arr, pc.arr, pd.arr, s.view(pipe.SUMMARY_DT, len(d)), po.u8, pp.u8)
             keep.append((pa, pc, pd, s, po, pp, len(d)))
         pl.drain(len(parts))
         outs.append(keep)
@@ -104,3 +109,32 @@ def test_pipeline_capacities():
         o, n = int(sm["out_off"][i]), int(sm["out_len"][i])
         assert o + n <= 64 * 1024 and int(sm["patch_off"][i]) + int(sm["patch_len"][i]) <= 24 * 1024
         assert bytes(small_out.u8[o:o + n]) == ref.doc_output(int(i), res[i])
+
+
+def test_packed_descriptors_that_lie():
+    """A packed chunk length that disagrees with the arena shifts every later chunk: those documents
+    fail their container checks (per-document errors, no out-of-bounds read), the earlier ones merge."""
+    from automerge_amd import pipe
+    from automerge_amd.batch import WANT_DIFF, Batch
+    _, parts = _parts("c4", 0, 200, 200, WANT_DIFF)
+    a, c, d = parts[0]
+    ref = Batch()
+    ref.stage(a, c, d)
+    kinfo = ref.kernel_info()
+    ws = int(ref.workspace_bytes())
+    pl = pipe.Pipeline(len(a), len(c), len(d), ws, 1 << 20, 1 << 20, kinfo["k_doc_fast_lds_per_doc"], slots=2)
+    cl, sp = pipe.pack(c, d)
+    bad = 13 * 100 + 5  # a change chunk of document 100
+    cl = cl.copy()
+    cl[bad] += 7
+    sp = sp.copy()
+    sp["chg_count"][-1] += 50  # the last document names chunks past the batch
+    s = pipe.Pinned(len(d) * pipe.SUMMARY_DT.itemsize)
+    po, pp = pipe.Pinned(1 << 20), pipe.Pinned(1 << 20)
+    sm = s.view(pipe.SUMMARY_DT, len(d))
+    pa, pc, pd = pipe.pinned_copy(a), pipe.pinned_copy(cl), pipe.pinned_copy(sp)
+    pl.submit_packed(pa.arr, pc.arr, pd.arr, sm, po.u8, pp.u8)
+    pl.drain(1)
+    st = sm["status"]
+    assert (st[:100] == 0).all()
+    assert (st[100:] != 0).all()
