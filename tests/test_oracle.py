@@ -123,3 +123,24 @@ def test_workload_vectors():
         doc.apply([bytes.fromhex(c) for c in rec["changeBytes"]])
         assert doc.save().hex() == rec["mergedBytes"]
         assert doc.heads() == rec["heads"]
+
+
+def test_mid_documents_oracle():
+    """The oracle against the reference's digests of the mid-size workload (tests/golden/mid.json):
+    save() bytes and heads of applyChanges(init(), all changes), for the first documents of each case."""
+    import hashlib
+    import json
+    import os
+    import workload as W
+    cases = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "mid.json")))
+    n = 0
+    for cs in cases:
+        k = min(cs["n"], 3)
+        arena, chunks, docs, _ = W.mid(cs["first"], k, cs["nactors"], cs["rounds"], cs["min_ops"], cs["max_ops"], nthreads=2)
+        for i in range(k):
+            _, ch = W.doc_chunks(arena, chunks, docs, i)
+            d = O.Doc.init()
+            d.apply(ch)
+            assert hashlib.sha256(d.save()).hexdigest() == cs["docs"][i]["full"]["save"], (cs["name"], i)
+            n += 1
+    assert n >= 9

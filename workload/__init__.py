@@ -20,6 +20,8 @@ for _name, _res, _args in (
         ("am_workload_c2", C.c_uint64, [C.c_uint64, C.c_uint32, _P, C.c_uint64, _P, _P, C.POINTER(C.c_uint64), C.c_int]),
         ("am_workload_text", C.c_uint64, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, C.c_uint64, _P, _P,
                                           C.POINTER(C.c_uint64), C.c_int]),
+        ("am_workload_mid", C.c_uint64, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, C.c_uint64,
+                                         _P, _P, C.POINTER(C.c_uint64), C.c_int]),
         ("am_workload_c4_shard", C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, _P, C.c_uint64, C.c_int]),
         ("am_workload_c4_list", C.c_uint64, [_P, C.c_uint32, _P, C.c_uint64, _P, _P, C.POINTER(C.c_uint64), C.c_int])):
     _f = getattr(lib, _name)
@@ -85,6 +87,23 @@ def text(first, n, nchanges, per_change=100, cross_every=10, nthreads=None):
     docs = np.empty(n, DOC_DT)
     got = lib.am_workload_text(first, n, nchanges, per_change, cross_every, arena.ctypes.data, need,
                                  chunks.ctypes.data, docs.ctypes.data, C.byref(ops), nthreads)
+    assert got == need
+    return arena, chunks, docs, int(ops.value)
+
+
+def mid(first, n, nactors=4, rounds=12, min_ops=8, max_ops=40, nthreads=None):
+    """Mid-size documents (am_workload.cpp gen_mid): Backend.init() + 1 + nactors * rounds change
+    chunks each, rounds of concurrent text / title edits by nactors actors (200-2,000 ops per
+    document with the defaults). Returns (arena, chunks, docs, ops)."""
+    nthreads = nthreads or min(16, os.cpu_count() or 1)
+    ops = C.c_uint64()
+    args = (first, n, nactors, rounds, min_ops, max_ops)
+    need = lib.am_workload_mid(*args, None, 0, None, None, C.byref(ops), nthreads)
+    assert need, "workload.mid: bad parameters"
+    arena = np.empty(need, np.uint8)
+    chunks = np.empty((1 + nactors * rounds) * n, CHUNK_DT)
+    docs = np.empty(n, DOC_DT)
+    got = lib.am_workload_mid(*args, arena.ctypes.data, need, chunks.ctypes.data, docs.ctypes.data, C.byref(ops), nthreads)
     assert got == need
     return arena, chunks, docs, int(ops.value)
 

@@ -413,6 +413,118 @@ void gen_text(uint32_t doc_index, uint32_t nchanges, uint32_t per_change, uint32
   out.ops = 1 + (uint64_t)nchanges * per_change;
 }
 
+// Mid-size documents (round-5 workload between C4's 62 and C3's 100k ops; VERDICT r4 Next 4):
+// `nactors` actors edit one text and one title in `rounds` rounds of concurrent changes. Change 0
+// (actor 0, seq 1): makeText at _root 'text' (1@A0), 'title' = 'mid' (2@A0). In round r every actor
+// makes one change whose deps are all heads after round r-1 (change 0 for round 0): the round's
+// changes are concurrent and the next round merges them. A change has min_ops + lcg % (max_ops -
+// min_ops + 1) ops; each op is, by lcg % 20: 0-2 (with a live element in the view) a delete of a
+// random live element; 3 a title set whose pred is every title op visible to the author; otherwise
+// an insert of one lowercase character (the first insert of a change after a random live element,
+// 1/8 at the head; the following ones after the previous insert). The author's view is the text
+// after round r-1 plus its own ops of the change; startOp = 1 + the largest op counter of rounds
+// < r. Changes >= 256 B are deflated as encodeChange writes them (columnar.js:738).
+// LCG call order per document (seed = doc index ^ 0x6d1d0000): make_actors(nactors); per change
+// one draw for the op count; per op one draw for the kind, one for a delete's element, (first
+// insert) one for head-or-not plus one for the element, then one for the character; a title set
+// draws one number for its value.
+void gen_mid(uint32_t doc_index, uint32_t nactors, uint32_t rounds, uint32_t min_ops, uint32_t max_ops, DocOut& out) {
+  uint32_t s = doc_index ^ 0x6d1d0000u;
+  std::vector<Actor> actors;
+  make_actors(s, (int)nactors, actors);
+  uint8_t h0[32];
+  out.changes.push_back(maybe_deflate(encode_change(
+      actors, 0, 1, 1, {},
+      {{-1, 0, "text", -1, 0, false, 4, 0, 0, "", {}}, {-1, 0, "title", -1, 0, false, 1, 6, 0, "mid", {}}}, h0)));
+  uint64_t nops = 2;
+  std::vector<uint64_t> live;                  // element ids (ctr << 8 | actor) after the last round
+  std::vector<std::pair<int64_t, int>> title = {{2, 0}};  // visible title ops after the last round
+  std::vector<std::vector<uint8_t>> heads = {std::vector<uint8_t>(h0, h0 + 32)};
+  int64_t maxop = 2;
+  std::vector<int64_t> seq(nactors, 0);
+  seq[0] = 1;
+  for (uint32_t r = 0; r < rounds; r++) {
+    std::vector<uint64_t> ins_all, del_all;
+    std::vector<std::pair<int64_t, int>> title_new, title_over;
+    std::vector<std::vector<uint8_t>> round_heads;
+    int64_t round_max = maxop;
+    std::vector<std::vector<uint8_t>> deps = heads;
+    std::sort(deps.begin(), deps.end());
+    for (uint32_t a = 0; a < nactors; a++) {
+      std::vector<uint64_t> view = live;  // the author's view: the text after round r-1 plus its own ops
+      std::unordered_map<uint64_t, uint32_t> at;
+      for (uint32_t i = 0; i < view.size(); i++) at[view[i]] = i;
+      auto vremove = [&](uint64_t e) {
+        auto it = at.find(e);
+        if (it == at.end()) return;
+        const uint32_t i = it->second;
+        at.erase(it);
+        const uint64_t last = view.back();
+        view.pop_back();
+        if (i < view.size()) { view[i] = last; at[last] = i; }
+      };
+      std::vector<std::pair<int64_t, int>> tvis = title;
+      const uint32_t n = min_ops + lcg(s) % (max_ops - min_ops + 1);
+      const int64_t start = maxop + 1;
+      std::vector<Op> ops;
+      bool have_ref = false;
+      uint64_t ref = 0;
+      for (uint32_t i = 0; i < n; i++) {
+        const int64_t ctr = start + i;
+        const uint32_t kind = lcg(s) % 20;
+        if (kind < 3 && !view.empty()) {
+          const uint64_t e = view[lcg(s) % view.size()];
+          const int ea = (int)(e & 255);
+          const int64_t ec = (int64_t)(e >> 8);
+          ops.push_back({0, 1, "", ea, ec, false, 3, 0, 0, "", {{ec, ea}}});
+          vremove(e);
+          del_all.push_back(e);
+        } else if (kind == 3) {
+          const std::string t = "m" + std::to_string(a) + "." + std::to_string(lcg(s) % 10000);
+          ops.push_back({-1, 0, "title", -1, 0, false, 1, 6, 0, t, tvis});
+          for (auto& p : tvis) title_over.push_back(p);
+          tvis = {{ctr, (int)a}};
+        } else {
+          if (!have_ref) {
+            have_ref = true;
+            if (lcg(s) % 8 == 0 || view.empty()) ref = ~0ull;
+            else ref = view[lcg(s) % view.size()];
+          }
+          const char c = (char)(97 + lcg(s) % 26);
+          if (ref == ~0ull) ops.push_back({0, 1, "", -1, 0, true, 1, 6, 0, std::string(1, c), {}});
+          else ops.push_back({0, 1, "", (int)(ref & 255), (int64_t)(ref >> 8), true, 1, 6, 0, std::string(1, c), {}});
+          const uint64_t e = ((uint64_t)ctr << 8) | a;
+          at[e] = (uint32_t)view.size();
+          view.push_back(e);
+          ins_all.push_back(e);
+          ref = e;
+        }
+      }
+      if (!tvis.empty() && tvis.size() == 1 && tvis[0].second == (int)a && tvis[0].first >= start) title_new.push_back(tvis[0]);
+      uint8_t h[32];
+      out.changes.push_back(maybe_deflate(encode_change(actors, (int)a, ++seq[a], start, deps, ops, h)));
+      round_heads.push_back(std::vector<uint8_t>(h, h + 32));
+      round_max = std::max(round_max, start + (int64_t)n - 1);
+      nops += n;
+    }
+    // the merged state after the round
+    std::unordered_map<uint64_t, bool> gone;
+    for (uint64_t e : del_all) gone[e] = true;
+    std::vector<uint64_t> nl;
+    for (uint64_t e : live) if (!gone.count(e)) nl.push_back(e);
+    for (uint64_t e : ins_all) if (!gone.count(e)) nl.push_back(e);
+    live.swap(nl);
+    std::vector<std::pair<int64_t, int>> nt;
+    for (auto& p : title)
+      if (std::find(title_over.begin(), title_over.end(), p) == title_over.end()) nt.push_back(p);
+    for (auto& p : title_new) nt.push_back(p);
+    title.swap(nt);
+    heads = round_heads;
+    maxop = round_max;
+  }
+  out.ops = nops;
+}
+
 // Lays out documents [base?][changes...] back to back in the arena
 uint64_t layout(std::vector<DocOut>& outs, uint8_t* arena, uint64_t cap, am_chunk_desc* chunks, am_doc_desc* docs,
                 uint64_t* ops_out) {
@@ -529,6 +641,15 @@ uint64_t am_workload_text(uint64_t first, uint32_t n, uint32_t nchanges, uint32_
 /* Document sharding of the C4 job: the documents of [first, first + n) whose
  * base document's SHA-256 (its container checksum, columnar.js:659-686) has first byte % world ==
  * rank, in index order. Writes up to cap indexes; returns how many belong to the shard. */
+/* Mid-size documents (gen_mid above): Backend.init() + 1 + nactors * rounds change chunks each. */
+uint64_t am_workload_mid(uint64_t first, uint32_t n, uint32_t nactors, uint32_t rounds, uint32_t min_ops, uint32_t max_ops,
+                         uint8_t* arena, uint64_t cap, am_chunk_desc* chunks, am_doc_desc* docs, uint64_t* ops, int nthreads) {
+  if (nactors < 1 || nactors > 200 || max_ops < min_ops || min_ops < 1) return 0;
+  auto gen = [=](uint32_t d, DocOut& o) { gen_mid(d, nactors, rounds, min_ops, max_ops, o); };
+  return generate(gen, mix_key(6, nactors * 1000003ull + rounds, min_ops, max_ops), first, n, arena, cap, chunks, docs, ops,
+                  nthreads);
+}
+
 uint64_t am_workload_c4_shard(uint64_t first, uint64_t n, uint32_t world, uint32_t rank, uint64_t* ids, uint64_t cap,
                               int nthreads) {
   if (world == 0) return 0;

@@ -29,6 +29,10 @@ uint64_t am_workload_c5(uint64_t first_doc, uint32_t ndocs, uint32_t per_side, u
 uint64_t am_workload_text(uint64_t first_doc, uint32_t ndocs, uint32_t nchanges, uint32_t per_change,
                           uint32_t cross_every, uint8_t *arena, uint64_t cap, am_chunk_desc *chunks,
                           am_doc_desc *docs, uint64_t *ops_out, int nthreads);
+/* Mid-size documents (gen_mid): Backend.init() + 1 + nactors * rounds change chunks; nactors actors
+ * edit one text and the title in rounds of concurrent changes of min_ops..max_ops ops. */
+uint64_t am_workload_mid(uint64_t first, uint32_t n, uint32_t nactors, uint32_t rounds, uint32_t min_ops, uint32_t max_ops,
+                         uint8_t *arena, uint64_t cap, am_chunk_desc *chunks, am_doc_desc *docs, uint64_t *ops, int nthreads);
 /* Shard of the C4 job: indexes in [first, first + n) whose base document's checksum byte 0
  * (SHA-256 of the chunk) % world == rank. */
 uint64_t am_workload_c4_shard(uint64_t first, uint64_t n, uint32_t world, uint32_t rank, uint64_t *ids, uint64_t cap,
