@@ -168,7 +168,20 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--check", type=int, default=200)
     ap.add_argument("--e2e", action="store_true", help="the whole sync of the pairs (generate/receive rounds)")
+    ap.add_argument("--dump", help="write the C5 pairs (u32 length + bytes: base, side A's, side B's changes) to this "
+                                   "file for tools/cpu_reference_sync.js, and exit")
     args = ap.parse_args()
+    if args.dump:
+        import struct
+        import workload
+        arena, chunks, docs, _ = workload.c5(0, args.pairs, args.per_side)
+        with open(args.dump, "wb") as f:
+            f.write(struct.pack("<II", args.pairs, args.per_side))
+            for i in range(args.pairs):
+                base, ch = workload.doc_chunks(arena, chunks, docs, i)
+                for b in [base] + ch:
+                    f.write(struct.pack("<I", len(b)) + b)
+        return
     if args.e2e:
         print(json.dumps(e2e(args)), flush=True)
         return
