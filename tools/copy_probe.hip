@@ -71,7 +71,11 @@ int main(int argc, char** argv) {
   auto best = [&](auto f) { double b = 1e30; f(); for (int r = 0; r < reps; r++) { double t0 = now(); f(); b = std::min(b, now() - t0); } return b; };
   std::string out = "{";
   char buf[256];
-  auto add = [&](const char* k, double v) { std::snprintf(buf, sizeof buf, "%s\"%s\": %.2f", out.size() > 1 ? ", " : "", k, v); out += buf; };
+  auto add = [&](const std::string& k, double v) {
+    char t[256];
+    std::snprintf(t, sizeof t, "%s\"%s\": %.2f", out.size() > 1 ? ", " : "", k.c_str(), v);
+    out += t;
+  };
 
   add("h2d_hip", gbps(best([&] { CK(hipMemcpyAsync(d_in, h_in, N, hipMemcpyHostToDevice, s1)); CK(hipStreamSynchronize(s1)); }), 1));
   add("d2h_hip", gbps(best([&] { CK(hipMemcpyAsync(h_out, d_out, N, hipMemcpyDeviceToHost, s2)); CK(hipStreamSynchronize(s2)); }), 1));
@@ -100,13 +104,13 @@ int main(int argc, char** argv) {
     hsa_status_t r = hsa_amd_memory_async_copy_on_engine(d_in, gpu, h_in, host, N, 0, nullptr, sig, (hsa_amd_sdma_engine_id_t)(1u << a), true);
     if (r != HSA_STATUS_SUCCESS) { hsa_signal_store_screlease(sig, 0); continue; }
     hsa_wait();
-    std::snprintf(buf, sizeof buf, "h2d_engine%d", a); add(buf, gbps(now() - t0, 1));
+    add("h2d_engine" + std::to_string(a), gbps(now() - t0, 1));
     hsa_signal_store_screlease(sig, 1);
     t0 = now();
     r = hsa_amd_memory_async_copy_on_engine(h_out, host, d_out, gpu, N, 0, nullptr, sig, (hsa_amd_sdma_engine_id_t)(1u << a), true);
     if (r != HSA_STATUS_SUCCESS) { hsa_signal_store_screlease(sig, 0); continue; }
     hsa_wait();
-    std::snprintf(buf, sizeof buf, "d2h_engine%d", a); add(buf, gbps(now() - t0, 1));
+    add("d2h_engine" + std::to_string(a), gbps(now() - t0, 1));
   }
   for (int a : eng) for (int b : eng) {
     if (a == b) continue;
@@ -115,7 +119,7 @@ int main(int argc, char** argv) {
       if (hsa_amd_memory_async_copy_on_engine(d_in, gpu, h_in, host, N, 0, nullptr, sig, (hsa_amd_sdma_engine_id_t)(1u << a), true) != HSA_STATUS_SUCCESS) hsa_signal_subtract_screlease(sig, 1);
       if (hsa_amd_memory_async_copy_on_engine(h_out, host, d_out, gpu, N, 0, nullptr, sig, (hsa_amd_sdma_engine_id_t)(1u << b), true) != HSA_STATUS_SUCCESS) hsa_signal_subtract_screlease(sig, 1);
       hsa_wait(); });
-    std::snprintf(buf, sizeof buf, "both_engines_%d_%d", a, b); add(buf, gbps(t, 2));
+    add("both_engines_" + std::to_string(a) + "_" + std::to_string(b), gbps(t, 2));
     if (gbps(t, 2) > best_pair) { best_pair = gbps(t, 2); ba = a; bb = b; }
   }
   // CU copy kernels over mapped pinned memory
