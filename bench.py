@@ -271,16 +271,20 @@ def main():
                     pl.submit_packed(pa.arr, p1.arr, p2.arr, summ, po.u8, pp.u8)
                 else:
                     pl.submit(pa.arr, p1.arr, p2.arr, summ, po.u8, pp.u8)
-            return pl.drain(nb)
 
         for _ in range(warmup):
             step()
+        pl.drain(nb * warmup)
         pl.times()
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        # the steps stream through the pipeline back to back (a caller's stream of batches: the next
+        # step's first H2D overlaps this step's last kernels and copies home); every batch of every
+        # step is home when the clock stops
         for _ in range(steps):
-            totals = step()
+            step()
+        totals = pl.drain(nb * steps)[-nb:]
         torch.cuda.synchronize()
         barrier()
         el = time.perf_counter() - t0
