@@ -513,17 +513,56 @@ extern "C" int am_batch_run(am_batch* b) {
   if (!set_device(e)) return 1;
   hipStream_t s = e->stream;
   BatchDev d = b->dev();
+  // AM_DEBUG_SYNC=1 (diagnosis): synchronise after every stage and name the one that failed;
+  // AM_DEBUG_WS_PAD=<bytes>: the kernels see the workspace that many bytes into a larger allocation
+  static const bool dbg = std::getenv("AM_DEBUG_SYNC") != nullptr;
+  static const uint64_t pad = [] { const char* v = std::getenv("AM_DEBUG_WS_PAD"); return v ? std::strtoull(v, nullptr, 10) & ~4095ull : 0ull; }();
+  if (pad) {
+    if (!b->ws.ensure(b->ws_need + pad + 16)) return 1;
+    d.ws = b->ws.p + pad;
+    d.ws_cap = b->ws.cap - pad;
+  }
+  // AM_DEBUG_WS_CANARY=<bytes>: the workspace is filled with 0xA5 and followed by that many canary
+  // bytes; am_batch_ws_canary reports the first one a kernel wrote
+  static const uint64_t canary = [] { const char* v = std::getenv("AM_DEBUG_WS_CANARY"); return v ? std::strtoull(v, nullptr, 10) : 0ull; }();
+  if (canary) {
+    if (!b->ws.ensure(b->ws_need + canary + 16)) return 1;
+    (void)hipMemsetAsync(b->ws.p, 0xA5, b->ws_need + canary, s);
+    d.ws = b->ws.p;  // (ensure may have moved it)
+    d.ws_cap = b->ws_need;
+  }
+  auto check = [&](const char* what) {
+    if (!dbg) return true;
+    const hipError_t r = hipStreamSynchronize(s);
+    if (r != hipSuccess) std::fprintf(stderr, "[am_debug] %s: %s (ndocs %u, ws %llu)\n", what, hipGetErrorString(r), b->ndocs,
+                                      (unsigned long long)b->ws_need);
+    return r == hipSuccess;
+  };
   (void)hipEventRecord(e->ev[0], s);
   am_launch_chunks(d, s);
+  if (!check("k_chunks")) return 1;
   (void)hipEventRecord(e->ev[1], s);
   am_launch_bounds(d, s);
+  if (!check("k_bounds")) return 1;
   (void)hipEventRecord(e->ev[2], s);
   am_launch_doc(d, s);
+  if (!check("k_doc_fast / k_doc")) return 1;
   (void)hipEventRecord(e->ev[3], s);
   am_launch_out_hash(d, s);
+  if (!check("k_out_hash_ws")) return 1;
   (void)hipEventRecord(e->ev[4], s);
   b->timed = true;
   return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// Diagnostics (AM_DEBUG_WS_CANARY): offset past the workspace end of the first canary byte a kernel
+// changed, or -1
+extern "C" int64_t am_batch_ws_canary(am_batch* b, uint64_t n) {
+  std::vector<uint8_t> h(n);
+  if (!set_device(b->eng) || hipMemcpy(h.data(), b->ws.p + b->ws_need, n, hipMemcpyDeviceToHost) != hipSuccess) return -2;
+  for (uint64_t i = 0; i < n; i++)
+    if (h[i] != 0xA5) return (int64_t)i;
+  return -1;
 }
 
 extern "C" int am_batch_sync(am_batch* b, am_error* err) {
@@ -577,6 +616,18 @@ extern "C" int am_batch_doc_heads(am_batch* b, uint32_t doc, uint8_t* dst32, uin
   WsLayout L = ws_layout(bd);
   uint32_t k = r.nheads < cap ? r.nheads : cap;
   return hipMemcpy(dst32, b->ws.p + r.ws_off + L.heads, 32ull * k, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+
+// Diagnostics: the first 48 bytes (PatchHdr2) of document doc's patch-log slot, as they are
+extern "C" int am_batch_doc_patch_raw(am_batch* b, uint32_t doc, uint8_t* dst48) {
+  if (!set_device(b->eng) || doc >= b->ndocs) return 1;
+  am_doc_result r;
+  DocBounds bd;
+  if (hipMemcpy(&r, b->results.p + doc, sizeof r, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(&bd, b->bounds.p + doc, sizeof bd, hipMemcpyDeviceToHost) != hipSuccess || !bd.P)
+    return 1;
+  const WsLayout L = ws_layout(bd);
+  return hipMemcpy(dst48, b->ws.p + r.ws_off + L.pwire, 48, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
 
 extern "C" int am_batch_doc_patch(am_batch* b, uint32_t doc, uint8_t* dst, uint64_t cap, uint64_t* len) {
@@ -738,6 +789,20 @@ extern "C" int am_batch_doc_plan(am_batch* b, uint32_t doc, uint64_t* out10) {
   return 0;
 }
 
+// Diagnostics: the DocBounds of a staged document (96 bytes) and its WsLayout (all u64 fields, in
+// declaration order); returns the number of u64 written to lay_out (cap permitting)
+extern "C" int am_batch_doc_layout(am_batch* b, uint32_t doc, void* bounds_out, uint64_t* lay_out, uint32_t cap) {
+  if (!set_device(b->eng) || doc >= b->ndocs) return -1;
+  DocBounds db;
+  if (hipMemcpy(&db, b->bounds.p + doc, sizeof db, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  std::memcpy(bounds_out, &db, sizeof db);
+  static_assert(sizeof(WsLayout) % 8 == 0, "WsLayout of u64");
+  const WsLayout L = ws_layout(db);
+  const uint32_t n = (uint32_t)(sizeof L / 8);
+  std::memcpy(lay_out, &L, 8ull * (n < cap ? n : cap));
+  return (int)n;
+}
+
 // k_doc_fast LDS slice of every document of the staged batch (diagnostics): out[doc] =
 // fast_layout(...).total, 0 when the document is outside the fast kernel's envelope
 extern "C" int am_batch_fast_slices(am_batch* b, uint32_t* out) {
@@ -783,6 +848,9 @@ struct PipeSlot {
   bool home_sdma = false;                      // the copies home went to the SDMA engines
   hsa_signal_t insig{};                        // SDMA copies of the batch's inputs (engine mode)
   bool in_sdma = false;                        // some input segment went to an SDMA engine
+  bool launched = false;                       // its compute chain is queued (pipe_launch)
+  bool packed = false;                         // packed descriptors (am_pipe_submit_packed)
+  uint64_t arena_len = 0;
 };
 }  // namespace
 
@@ -799,8 +867,12 @@ struct am_pipe {
   uint32_t nres = 0;                           // resident batches since the last am_pipe_resident_sync
   uint32_t eng_h2d = 0, eng_home = 0;          // SDMA engine masks of the host-link copies (0: runtime's choice)
   int eng_state = 0;                           // engine mode: 0 not chosen yet, 1 on, -1 off
+  PipeSlot* pending = nullptr;                 // inputs queued, compute chain not yet (pipe_submit)
+  PipeSlot* launched = nullptr;                // the slot whose chain was queued last
   hsa_agent_t gpu{}, host{};
 };
+
+static bool sdma_wait(hsa_signal_t sig);
 
 static void pipe_free(am_pipe* p) {
   if (!p) return;
@@ -823,6 +895,11 @@ extern "C" void am_pipe_destroy(am_pipe* p) {
   if (!p) return;
   set_device(p->eng);
   (void)hipDeviceSynchronize();
+  // SDMA copies of the engine mode are outside the HIP streams: wait for them before freeing
+  for (PipeSlot* sl : p->slots) {
+    if (sl->insig.handle) (void)sdma_wait(sl->insig);
+    if (sl->home.handle) (void)sdma_wait(sl->home);
+  }
   pipe_free(p);
 }
 
@@ -928,7 +1005,7 @@ static bool pipe_finalize(am_pipe* p, PipeSlot* sl) {
     }
     sl->home_sdma = true;
     if (!sdma) {  // a copy was refused: wait for the others, then copy everything the HIP way
-      hsa_signal_wait_scacquire(sl->home, HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+      if (!sdma_wait(sl->home)) return false;
       sl->home_sdma = false;
     }
   }
@@ -948,12 +1025,22 @@ static bool pipe_finalize(am_pipe* p, PipeSlot* sl) {
   return true;
 }
 
+// Waits until the SDMA copies counted by `sig` are done; false when one reported an error (the
+// runtime sets the signal negative, which EQ 0 would wait for forever)
+static bool sdma_wait(hsa_signal_t sig) {
+  const hsa_signal_value_t v = hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+  if (v < 0) {
+    hsa_signal_store_screlease(sig, 0);
+    return false;
+  }
+  return true;
+}
+
 // the copies home of a finalized batch are complete (host wait)
 static bool pipe_wait_home(PipeSlot* sl) {
   if (sl->home_sdma) {
-    hsa_signal_wait_scacquire(sl->home, HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
     sl->home_sdma = false;
-    return true;
+    return sdma_wait(sl->home);
   }
   return hipEventSynchronize(sl->ev_out) == hipSuccess;
 }
@@ -1035,11 +1122,16 @@ static bool pipe_h2d(am_pipe* p, PipeSlot* sl, void* dst, const void* src, uint6
 // (the previous batch's kernels keep the GPU busy meanwhile; its copies home are queued right after)
 static bool pipe_h2d_done(am_pipe* p, PipeSlot* sl) {
   if (sl->in_sdma) {
-    hsa_signal_wait_scacquire(sl->insig, HSA_SIGNAL_CONDITION_EQ, 0, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
     sl->in_sdma = false;
+    if (!sdma_wait(sl->insig)) return false;
   }
-  return hipEventRecord(sl->ev_in, p->s_in) == hipSuccess && hipStreamWaitEvent(p->s_c, sl->ev_in, 0) == hipSuccess;
+  return hipStreamWaitEvent(p->s_c, sl->ev_in, 0) == hipSuccess;
 }
+// after the last input segment of a batch: the input stream's event for its segments (recorded now,
+// before a later batch's copies join the stream)
+static bool pipe_h2d_issued(am_pipe* p, PipeSlot* sl) { return hipEventRecord(sl->ev_in, p->s_in) == hipSuccess; }
+// the batch whose inputs are queued but whose chain is not (pipe_submit) gets its chain now
+static bool pipe_flush_pending(am_pipe* p);
 
 extern "C" int am_pipe_engines(am_pipe* p, uint32_t* out2) {
   out2[0] = p->eng_h2d;
@@ -1056,6 +1148,47 @@ struct PipeIn {
   const am_doc_span* spans = nullptr;
 };
 
+// The compute chain of a slot whose inputs were queued by pipe_submit: waits for its H2D (engine
+// mode: on the host), queues every kernel on the compute stream, then queues the copies home of the
+// batch launched before it (its kernels are ahead on the stream).
+static bool pipe_launch(am_pipe* p, PipeSlot* sl) {
+  am_batch& b = sl->b;
+  const am_pipe_caps& c = p->caps;
+  if (!pipe_h2d_done(p, sl)) return false;
+  BatchDev d = b.dev();
+  d.ws_cap = c.ws_bytes;
+  hipStream_t s = p->s_c;
+  (void)hipEventRecord(sl->ev_c0, s);
+  if (sl->packed)
+    am_launch_unpack(sl->clen.p, b.nchunks, sl->arena_len, sl->spans.p, b.ndocs, sl->c64.p, sl->coff.p, sl->ctmp.p, sl->olen.p,
+                     sl->ooff.p, sl->tmp.p, sl->totals.p, b.chunks.p, b.docs.p, s);
+  am_launch_chunks(d, s);
+  am_launch_bounds(d, s);
+  (void)hipEventRecord(sl->ev_d0, s);
+  am_launch_doc(d, s);
+  (void)hipEventRecord(sl->ev_d1, s);
+  am_launch_out_hash(d, s);
+  // documents past the caller's buffers (or the device arenas) report AM_U_CAPACITY
+  am_launch_pipe_compact(d, sl->olen.p, sl->ooff.p, sl->plen.p, sl->poff.p, sl->tmp.p, sl->totals.p, sl->dout.p,
+                         std::min<uint64_t>(c.out_bytes, sl->h_out ? sl->h_out_cap : 0), sl->dpatch.p,
+                         std::min<uint64_t>(c.patch_bytes, sl->h_patch ? sl->h_patch_cap : 0), sl->summ.p, s);
+  if (hipMemcpyAsync(sl->h_totals, sl->totals.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s) != hipSuccess) return false;
+  if (hipEventRecord(sl->ev_comp, s) != hipSuccess || hipGetLastError() != hipSuccess) return false;
+  sl->launched = true;
+  PipeSlot* prev = p->launched;
+  p->launched = sl;
+  return !prev || !prev->busy || pipe_finalize(p, prev);
+}
+
+static bool pipe_flush_pending(am_pipe* p) {
+  PipeSlot* pend = p->pending;
+  p->pending = nullptr;
+  return !pend || pipe_launch(p, pend);
+}
+
+// Queues batch `ticket`'s inputs, then the compute chain of the batch submitted before it: the
+// input engine always holds the next batch's copy while the previous one is being waited for, so
+// the host link never idles between batches.
 static int pipe_submit(am_pipe* p, const uint8_t* arena, uint64_t arena_len, const PipeIn& in, uint32_t nchunks, uint32_t ndocs,
                        bool any_diff, am_doc_summary* summary, uint8_t* out, uint64_t out_cap, uint8_t* patches,
                        uint64_t patch_cap, uint64_t* ticket, am_error* err) {
@@ -1071,11 +1204,14 @@ static int pipe_submit(am_pipe* p, const uint8_t* arena, uint64_t arena_len, con
   if (packed && !(sl->clen.ensure(c.chunks) && sl->spans.ensure(c.docs) && sl->c64.ensure(c.chunks) && sl->coff.ensure(c.chunks) &&
                   sl->ctmp.ensure(am_scan_tmp_elems(c.chunks))))
     return fail("automerge_amd: device allocation failed (packed descriptors)");
+  if (sl == p->pending && !pipe_flush_pending(p)) return fail("automerge_amd: HIP error while launching a batch");
   if (!pipe_retire(p, sl, false)) return fail("automerge_amd: HIP error while retiring a batch");
   am_batch& b = sl->b;
   b.nchunks = nchunks;
   b.ndocs = ndocs;
   b.any_diff = any_diff;
+  sl->packed = packed;
+  sl->arena_len = arena_len;
   // inputs
   if (!pipe_h2d(p, sl, b.arena.p, arena, arena_len)) return fail("automerge_amd: H2D failed");
   if (packed) {
@@ -1086,29 +1222,9 @@ static int pipe_submit(am_pipe* p, const uint8_t* arena, uint64_t arena_len, con
              !pipe_h2d(p, sl, b.docs.p, in.docs, sizeof(am_doc_desc) * ndocs)) {
     return fail("automerge_amd: H2D failed");
   }
-  if (!pipe_h2d_done(p, sl)) return fail("automerge_amd: stream ordering failed");
-  // the whole chain on the compute stream; no host round trip
-  BatchDev d = b.dev();
-  d.ws_cap = c.ws_bytes;
-  hipStream_t s = p->s_c;
-  (void)hipEventRecord(sl->ev_c0, s);
-  if (packed)
-    am_launch_unpack(sl->clen.p, nchunks, arena_len, sl->spans.p, ndocs, sl->c64.p, sl->coff.p, sl->ctmp.p, sl->olen.p, sl->ooff.p,
-                     sl->tmp.p, sl->totals.p, b.chunks.p, b.docs.p, s);
-  am_launch_chunks(d, s);
-  am_launch_bounds(d, s);
-  (void)hipEventRecord(sl->ev_d0, s);
-  am_launch_doc(d, s);
-  (void)hipEventRecord(sl->ev_d1, s);
-  am_launch_out_hash(d, s);
-  // documents past the caller's buffers (or the device arenas) report AM_U_CAPACITY
-  am_launch_pipe_compact(d, sl->olen.p, sl->ooff.p, sl->plen.p, sl->poff.p, sl->tmp.p, sl->totals.p, sl->dout.p,
-                         std::min<uint64_t>(c.out_bytes, out ? out_cap : 0), sl->dpatch.p,
-                         std::min<uint64_t>(c.patch_bytes, patches ? patch_cap : 0), sl->summ.p, s);
-  if (hipMemcpyAsync(sl->h_totals, sl->totals.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s) != hipSuccess)
-    return fail("automerge_amd: D2H failed");
-  if (hipEventRecord(sl->ev_comp, s) != hipSuccess || hipGetLastError() != hipSuccess) return fail("automerge_amd: kernel launch failed");
+  if (!pipe_h2d_issued(p, sl)) return fail("automerge_amd: stream ordering failed");
   sl->busy = true;
+  sl->launched = false;
   sl->finalized = false;
   sl->ticket = p->next;
   sl->h_summ = summary;
@@ -1117,13 +1233,11 @@ static int pipe_submit(am_pipe* p, const uint8_t* arena, uint64_t arena_len, con
   sl->h_patch = patches;
   sl->h_patch_cap = patch_cap;
   if (ticket) *ticket = p->next;
-  // the previous batch: its kernels are ahead of ours on the compute stream; queue its copies home
-  // (on the other engine: they overlap the next batch's H2D)
-  if (p->next > 0) {
-    PipeSlot* prev = p->slots[(p->next - 1) % p->slots.size()];
-    if (prev->busy && !pipe_finalize(p, prev)) return fail("automerge_amd: HIP error while finishing a batch");
-  }
   p->next++;
+  // the batch submitted before this one: its chain now (its inputs are on their way or there)
+  PipeSlot* pend = p->pending;
+  p->pending = sl;
+  if (pend && !pipe_launch(p, pend)) return fail("automerge_amd: HIP error while launching a batch");
   if (err) err->code = 0;
   return 0;
 }
@@ -1174,6 +1288,7 @@ extern "C" int am_pipe_run_resident(am_pipe* p, const uint8_t* d_arena, uint64_t
     return fail("automerge_amd: batch exceeds the pipeline capacities");
   // 4 events per batch until am_pipe_resident_sync: a bounded number of batches between syncs
   if (p->nres >= 4096) return fail("automerge_amd: 4096 resident batches without am_pipe_resident_sync");
+  if (!pipe_flush_pending(p)) return fail("automerge_amd: HIP error while launching a batch");
   PipeSlot* sl = p->slots[0];
   if (sl->busy && !pipe_retire(p, sl, true)) return fail("automerge_amd: HIP error while retiring a batch");
   am_batch& b = sl->b;
@@ -1228,6 +1343,10 @@ extern "C" int am_pipe_resident_sync(am_pipe* p, float* ms2, am_error* err) {
 
 extern "C" int am_pipe_drain(am_pipe* p, uint64_t* totals, uint32_t cap, am_error* err) {
   if (!set_device(p->eng)) { to_c(Err{AM_U_CAPACITY, false, "automerge_amd: no device"}, err); return 1; }
+  if (!pipe_flush_pending(p)) {
+    to_c(Err{AM_U_CAPACITY, false, "automerge_amd: HIP error while launching a batch"}, err);
+    return 1;
+  }
   const size_t S = p->slots.size();
   // in submission order
   for (uint64_t t = p->next >= S ? p->next - S : 0; t < p->next; t++) {

@@ -53,6 +53,7 @@ struct DVis { int32_t row; int32_t next; };
 struct DCs { int64_t op_ctr; int64_t value; int32_t op_actor; int32_t nleft; int32_t next; int32_t pad; };
 struct DCm { int64_t ctr; int32_t actor; int32_t state; int32_t next; int32_t pad; };
 
+#define DIFF_NCAPS_MAX 24
 struct DiffScratch {
   DObj* obj; uint32_t nobj, cap_obj;
   DKid* kid; uint32_t nkid, cap_kid;
@@ -79,6 +80,9 @@ struct DiffScratch {
   int32_t* estart;                    // F position -> F position of its element's insert row, -1: map row
   int32_t* hash; uint32_t hmask;      // element id -> F position of its insert row (open addressing)
   uint32_t* ev_off; int32_t* ev;      // succ entries bucketed by the stream time of their op
+#ifdef AM_DIFF_CHECK
+  uint64_t dcap[DIFF_NCAPS_MAX];      // diagnostics build: the pool sizes, checked on every unchecked write
+#endif
 };
 
 // sizes of the pools for R rows and E pred/succ entries (host and device agree)
@@ -157,6 +161,9 @@ AM_PHD inline void diff_scratch_bind(uint8_t* p, uint64_t R, uint64_t E, DiffScr
   w.hash = reinterpret_cast<int32_t*>(take(c[21] * 4)); w.hmask = (uint32_t)c[21] - 1;
   w.ev_off = reinterpret_cast<uint32_t*>(take(c[22] * 4));
   w.ev = reinterpret_cast<int32_t*>(take(c[23] * 4));
+#ifdef AM_DIFF_CHECK
+  for (int i = 0; i < DIFF_NCAPS; i++) w.dcap[i] = c[i];
+#endif
   w.nobj = w.nkid = w.nkv = w.nprop = w.npe = w.ned = w.nmv = w.npst = w.nvis = w.ncs = w.ncm = w.noid = 0;
 }
 
@@ -190,8 +197,23 @@ struct Diff {
   // the rows and succ entries whose op precedes stream position W, so seek and the doc cursor
   // cost O(log n) instead of O(rows).
   AM_PHD static uint32_t lsb(uint32_t i) { return i & (~i + 1u); }
+#ifdef AM_DIFF_CHECK
+  // diagnostics build: an index outside pool `k` fails the replay with status 240 + k (arg0 = index,
+  // arg1 = the pool's size) instead of writing past it
+  AM_PHD bool dchk(int k, uint64_t i) {
+    if (i < w.dcap[k]) return true;
+    if (ok) { o.status = 240 + k; o.arg0 = (int64_t)i; o.arg1 = (int64_t)w.dcap[k]; ok = false; }
+    return false;
+  }
+#define DCHK(k, i) if (!dchk(k, (uint64_t)(i))) return
+#define DCHKF(k, i) if (!dchk(k, (uint64_t)(i))) return false
+#else
+#define DCHK(k, i)
+#define DCHKF(k, i)
+#endif
   AM_PHD void bit_add(int32_t* b, uint32_t i, int32_t v) {
     const uint32_t n = s.nout();
+    DCHK(16, n);
     for (++i; i <= n; i += lsb(i)) b[i] += v;
   }
   AM_PHD int32_t bit_pre(const int32_t* b, uint32_t i) const {  // sum over F positions [0, i)
@@ -226,8 +248,10 @@ struct Diff {
     }
   }
   AM_PHD void elem_row_live(int32_t f, int32_t d) {
+    DCHK(20, f);
     const int32_t e = w.estart[f];
     if (e < 0) return;
+    DCHK(19, e);
     const int32_t before = w.live[e];
     w.live[e] += d;
     if (before == 0 && d > 0) bit_add(w.bitv, (uint32_t)e, 1);
@@ -235,6 +259,9 @@ struct Diff {
   }
   AM_PHD void fast_init() {
     const uint32_t n = s.nout(), nstream = s.nrows() - s.nb();
+    DCHK(16, n);
+    DCHK(18, n);
+    DCHK(22, nstream);
     for (uint32_t i = 0; i <= n; i++) { w.bitp[i] = 0; w.bitv[i] = 0; }
     for (uint32_t h = 0; h <= w.hmask; h++) w.hash[h] = -1;
     for (uint32_t t = 0; t <= nstream; t++) w.ev_off[t] = 0;
@@ -261,7 +288,10 @@ struct Diff {
     for (uint32_t f = 0; f < n; f++)  // bucket fill: ev_off[t] is the running cursor, restored below
       for (uint32_t k = 0; k < s.f_nsucc(f); k++) {
         const int64_t t = s.f_succ_time(f, k);
-        if (t >= 0 && t < (int64_t)nstream) w.ev[w.ev_off[t]++] = (int32_t)f;
+        if (t >= 0 && t < (int64_t)nstream) {
+          DCHK(23, w.ev_off[t]);
+          w.ev[w.ev_off[t]++] = (int32_t)f;
+        }
       }
     for (uint32_t t = nstream; t > 0; t--) w.ev_off[t] = w.ev_off[t - 1];
     w.ev_off[0] = 0;
@@ -278,6 +308,7 @@ struct Diff {
     const uint32_t nstream = s.nrows() - s.nb();
     while ((int64_t)cur_t < W && cur_t < nstream) {
       const uint32_t t = cur_t++;
+      DCHK(11, srow(t));
       const int32_t f = w.fpos[srow(t)];
       if (f >= 0) {
         bit_add(w.bitp, (uint32_t)f, 1);
@@ -504,6 +535,7 @@ struct Diff {
       const uint32_t act = w.ed[k].action;
       if (act == PR_INSERT || act == PR_UPDATE) {
         if (w.ed[k].index != index) return fail(PATCH_U_VALUE);  // 'last edit has unexpected index'
+        DCHKF(13, nu);
         w.tmp[nu++] = k;
         edit_pop(ob);
         if (act == PR_INSERT) break;
@@ -1137,7 +1169,10 @@ struct Diff {
         }
       }
       uint32_t ne = 0;
-      for (int32_t e = d.edit_tail; e >= 0; e = w.ed[e].prev) w.tmp[ne++] = e;
+      for (int32_t e = d.edit_tail; e >= 0; e = w.ed[e].prev) {
+        DCHKF(13, ne);
+        w.tmp[ne++] = e;
+      }
       for (uint32_t q = ne; q-- > 0;) {
         const DEdit& e = w.ed[w.tmp[q]];
         PatchRec r = {};
@@ -1147,7 +1182,10 @@ struct Diff {
         } else if (e.action == PR_MULTI) {
           r.c1 = e.ec; r.a1 = e.ea; r.dt = e.mdt; r.n = e.nmv;
           uint32_t nv = 0;  // values, oldest first
-          for (int32_t m = e.mv_tail; m >= 0 && nv < e.nmv; m = w.mv[m].prev) w.tmp[ne + nv++] = m;
+          for (int32_t m = e.mv_tail; m >= 0 && nv < e.nmv; m = w.mv[m].prev) {
+            DCHKF(13, ne + nv);
+            w.tmp[ne + nv++] = m;
+          }
           for (uint32_t k = nv; k-- > 0;) {
             const DVal& v = w.mv[w.tmp[ne + k]].v;
             if (!patch_push_val(o, v.vtag, v.dt, v.v0, v.v1)) { ok = false; return false; }
@@ -1236,14 +1274,19 @@ struct Diff {
   bool meta_mode = false;
 
   AM_PHD bool run() {
+    DCHKF(11, s.nrows() ? s.nrows() - 1 : 0);
     for (uint32_t r = 0; r < s.nrows(); r++) w.fpos[r] = -1;
-    for (uint32_t f = 0; f < s.nout(); f++) w.fpos[s.frow((int32_t)f)] = (int32_t)f;
+    for (uint32_t f = 0; f < s.nout(); f++) {
+      DCHKF(11, s.frow((int32_t)f));
+      w.fpos[s.frow((int32_t)f)] = (int32_t)f;
+    }
     if (meta_mode && meta_in) {
       if (!build_objects() || !meta_restore(meta_in, meta_len)) return false;
     } else if (!build_meta()) {
       return false;
     }
     fast_init();
+    if (!ok) return false;
     uint32_t pos = 0;
     const uint32_t nstream = s.nrows() - s.nb();
     for (uint32_t p = 0; p < s.npass() && ok; p++) {

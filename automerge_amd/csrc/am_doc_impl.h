@@ -1210,6 +1210,10 @@ __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restric
     s.out_len = 0;
     s.ph_last = clock64();
     s.xs_used = 0;
+#ifdef AM_DIFF_CHECK
+    s.dbg_phase = 0xffffu;
+    s.dbg_canary = 0xffffu;
+#endif
     if (ws_off[doc] + s.L.total > ws_cap) set_err(s, AM_U_CAPACITY);
     // chunk-level errors: the base document first (load), then changes in order (new.js:1798)
     if (s.has_base) {
@@ -1974,6 +1978,10 @@ __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restric
       patch_scan(src, po, w, pmax);
       wire_out(po, pmax, wsg + L.pwire, L.pwire_cap);
     }
+    PH(13);
+#ifdef AM_DIFF_CHECK
+    if (t == 0 && s.b.R > 1100) printf("[dcheck] doc %u R %u before P8: P %u status %u\n", doc, s.b.R, s.b.P, s.status);
+#endif
     // P8: the patch applyChanges returns (am_diff.h), lane 0, after the merge
     if (s.b.P == 2 && t == 0) {
       uint8_t* pbase = wsg + L.patch;
@@ -1996,10 +2004,43 @@ __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restric
         mi = arena + mc.off;
         ml = mc.len;
       }
+      bool p8_skip = false;
+#ifdef AM_DIFF_CHECK
+      // diagnostics build: the replay's inputs against the layout's bounds (status 250 + which), and
+      // the document's shared bounds / layout against a fresh copy (status 260 + which: a corrupted
+      // DocShared); the header then goes to the layout's true patch slot
+      const uint64_t chk[4] = {s.nrows, NOUT, NSUCC, s.npass};
+      const uint64_t lim[4] = {s.b.R, s.b.R, (uint64_t)s.b.E + 1, (uint64_t)s.b.N + 1};
+      bool pre_ok = true;
+      for (int q = 0; q < 4 && pre_ok; q++)
+        if (chk[q] > lim[q]) { po.status = 250 + q; po.arg0 = (int64_t)chk[q]; po.arg1 = (int64_t)lim[q]; pre_ok = false; }
+      {
+        const DocBounds gb = bounds[doc];
+        const WsLayout GL = ws_layout(gb);
+        const uint64_t a[6] = {gb.R, gb.E, GL.pwire, GL.dscr, GL.total, GL.patch};
+        const uint64_t bv[6] = {s.b.R, s.b.E, L.pwire, L.dscr, L.total, L.patch};
+        for (int q = 0; q < 6 && pre_ok; q++)
+          if (a[q] != bv[q]) { po.status = 260 + q; po.arg0 = (int64_t)bv[q]; po.arg1 = (int64_t)a[q]; pre_ok = false; }
+        if (!pre_ok && po.status >= 260) {
+          wire_out(po, 0, wsg + GL.pwire, GL.pwire_cap);
+          p8_skip = true;
+        }
+      }
+      po.nrec = po.nmval = po.nheap = 0;
+      if (pre_ok)
+#endif
       diff_scan(src, po, dw, meta, mi, ml);
       uint8_t* const pw = wsg + L.pwire;
-      const uint64_t wl = patch_pack(po, 0, pw, L.pwire_cap);
-      if (!wl) {
+      const uint64_t wl = p8_skip ? 1 : patch_pack(po, 0, pw, L.pwire_cap);
+#ifdef AM_DIFF_CHECK
+      if (s.dbg_canary == 0xffffu && dbg_canary_hit(wsg + L.total)) s.dbg_canary = 50;  // P8
+      if (s.b.R > 1100)
+        printf("[dcheck] doc %u R %u P8 done: status %u nrec %u nmval %u nheap %u wl %llu pwire %llu cap %llu total %llu\n", doc,
+               s.b.R, po.status, (unsigned)po.nrec, (unsigned)po.nmval, (unsigned)po.nheap, (unsigned long long)wl,
+               (unsigned long long)L.pwire, (unsigned long long)L.pwire_cap, (unsigned long long)L.total);
+#endif
+      if (p8_skip) {
+      } else if (!wl) {
         wire_out(po, 0, pw, L.pwire_cap);
       } else if (meta && !po.status) {
         // the snapshots this call leaves, after the stream (PatchHdr2.meta_bytes)
@@ -2022,6 +2063,11 @@ done:
   if (t == 0) {
     am_doc_result r;
     r.status = s.status;
+#ifdef AM_DIFF_CHECK
+    if (s.dbg_phase != 0xffffu) r.status = 280 + s.dbg_phase;
+    if (s.dbg_canary == 0xffffu && dbg_canary_hit(wsg + s.L.total)) s.dbg_canary = 99;  // after the last marker
+    if (s.dbg_canary != 0xffffu) r.status = 300 + s.dbg_canary;
+#endif
     r.err_change = s.errchg;
     r.arg0 = s.arg0;
     r.arg1 = s.arg1;

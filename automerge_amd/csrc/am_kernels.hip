@@ -695,6 +695,27 @@ __device__ unsigned long long am_phase_cycles[32];
       s.ph_last = now_;                                                        \
     }                                                                          \
   } while (0)
+#elif defined(AM_DIFF_CHECK)
+// (AM_DEBUG_WS_CANARY runs of one document: the 16 bytes after its workspace hold 0xA5)
+__device__ __forceinline__ bool dbg_canary_hit(const uint8_t* p) {
+  for (int i = 0; i < 16; i++) if (p[i] != 0xA5) return true;
+  return false;
+}
+// diagnostics build: at every phase marker thread 0 compares the document's shared bounds with the
+// global copy and records the first phase after which they differ (s.dbg_phase; result status 280 + k)
+#define PH(k)                                                                                            \
+  do {                                                                                                   \
+    __syncthreads();                                                                                     \
+    if (threadIdx.x == 0 && s.dbg_phase == 0xffffu) {                                                    \
+      const DocBounds gb_ = bounds[doc];                                                                 \
+      if (gb_.R != s.b.R || gb_.E != s.b.E || gb_.P != s.b.P || gb_.N != s.b.N || gb_.C != s.b.C ||      \
+          ws_layout(gb_).total != s.L.total || ws_layout(gb_).pwire != s.L.pwire)                        \
+        s.dbg_phase = (k);                                                                               \
+    }                                                                                                    \
+    if (threadIdx.x == 0 && s.dbg_canary == 0xffffu && dbg_canary_hit(wsg + s.L.total))                 \
+      s.dbg_canary = (k);                                                                                \
+    __syncthreads();                                                                                     \
+  } while (0)
 #else
 #define PH(k) \
   do {        \
@@ -727,6 +748,9 @@ struct DocShared {
   uint64_t ph_last;
   uint32_t xs_used;                       // bytes of replaced strings after the staged input (b.U)
   uint32_t nunk_inst, nunk_ids;           // unknown op columns: instances, distinct output columns
+#ifdef AM_DIFF_CHECK
+  uint32_t dbg_phase, dbg_canary;
+#endif
 };
 
 __device__ static void set_err(DocShared& s, uint32_t code, int64_t a0 = 0, int64_t a1 = 0, uint64_t actor_off = 0,

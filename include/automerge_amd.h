@@ -222,6 +222,14 @@ int am_batch_fast_flags(am_batch *b, uint8_t *flags);
  * run, out2[1] of them merged by the small-document kernel k_doc_fast. Not part of the reference
  * interface. */
 int am_engine_stats(am_engine *e, uint64_t *out2);
+/* Diagnostics (AM_DEBUG_WS_CANARY=<n> in the environment of am_batch_run): offset past the end of
+ * the batch workspace of the first of n canary bytes a kernel wrote, -1 when none. */
+int64_t am_batch_ws_canary(am_batch *b, uint64_t n);
+/* Diagnostics: document doc's workspace bounds (96 bytes, the engine's DocBounds) and layout (u64
+ * offsets; returns how many the layout has, writing at most cap). */
+int am_batch_doc_layout(am_batch *b, uint32_t doc, void *bounds_out, uint64_t *lay_out, uint32_t cap);
+/* Diagnostics: the raw 48-byte header of document doc's patch-log slot. */
+int am_batch_doc_patch_raw(am_batch *b, uint32_t doc, uint8_t *dst48);
 /* Device pointer + size of the staged arena / merged outputs (for bench byte accounting). */
 uint64_t am_batch_workspace_bytes(am_batch *b);
 /* Launch shape of the staged batch's document kernels: out3[0] = k_doc dynamic LDS bytes,

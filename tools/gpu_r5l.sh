@@ -1,0 +1,7 @@
+#!/bin/bash
+set -o pipefail
+O=gpurun_out/r5
+mkdir -p $O
+for f in 0 patch diff; do
+AM_DEBUG_WS_CANARY=4194304 timeout -k 10 200 python -u tools/mid_canary.py --docs 2048,2055,2141,2147,2237,2344 --flags $f > $O/canary_$f.log 2>&1 || exit 1
+done
