@@ -973,6 +973,7 @@ static void* mapped(void* host) {
 // kernels then wait on their own memory traffic (k_chunks ran 6x slower under it).
 static bool pipe_finalize(am_pipe* p, PipeSlot* sl) {
   if (sl->finalized) return true;
+  if (!sl->launched) return false;  // its chain is not queued: nothing to finalize (a caller's bug)
   if (hipEventSynchronize(sl->ev_comp) != hipSuccess) return false;
   const uint64_t to = sl->h_totals[0], tp = sl->h_totals[1];
   const uint32_t nd = sl->b.ndocs;
@@ -1069,11 +1070,13 @@ static bool pipe_retire(am_pipe* p, PipeSlot* sl, bool wait_home) {
   return true;
 }
 
-// Engine mode (AM_PIPE_ENGINES, default on): the inputs and the copies home go to two different
-// SDMA engines (hsa_amd_memory_async_copy_on_engine), so the two directions of the host link run at
-// the same time; left to the runtime, both can land on one engine and the step becomes H2D + D2H
-// (BENCH_r04: 42.8 + 21.9 ms). The engines are the first two that the runtime reports free for the
-// two directions, its preferred ones first. Any failure turns the mode off for the pipeline.
+// Engine mode (AM_PIPE_ENGINES, default on): the copies home go to an SDMA engine of their own
+// (hsa_amd_memory_async_copy_on_engine), apart from the runtime's preferred H2D engine that the
+// input copies use, so the two directions of the host link run at the same time; left to the
+// runtime, both can land on one engine and the step becomes H2D + D2H (BENCH_r04: 42.8 + 21.9 ms;
+// tools/copy_probe.hip measured 57 GB/s for both directions together on one engine, 97 on two).
+// The engines are the first ones the runtime reports free, its preferred ones first. Any failure
+// turns the mode off for the pipeline.
 static void pipe_choose_engines(am_pipe* p, const void* pinned_src, const void* dev_dst) {
   if (p->eng_state) return;
   p->eng_state = -1;
@@ -1087,6 +1090,8 @@ static void pipe_choose_engines(am_pipe* p, const void* pinned_src, const void* 
     return;
   (void)hsa_amd_memory_get_preferred_copy_engine(gpu, host, &pf_in);
   (void)hsa_amd_memory_get_preferred_copy_engine(host, gpu, &pf_out);
+  // the inputs go through the runtime's copy path, which takes the preferred H2D engine: the copies
+  // home take another one
   auto lowest = [](uint32_t m) { return m & (~m + 1); };
   uint32_t in = lowest(pf_in & st_in);
   if (!in) in = lowest(st_in);
@@ -1100,22 +1105,16 @@ static void pipe_choose_engines(am_pipe* p, const void* pinned_src, const void* 
   p->eng_state = 1;
 }
 
-// H2D of one input segment of the slot's batch (after the slot's previous compute chain, which
-// pipe_retire waited for): the input SDMA engine in engine mode, else the input stream
+// H2D of one input segment of the slot's batch on the input stream, ordered after the slot's
+// previous compute chain (pipe_retire) and handed to the compute stream by an event: the runtime's
+// own copy path, which also makes the new bytes visible to the kernels that follow it. (An input
+// copy on an engine of our own, outside the streams, left stale input lines visible to the next
+// batch's kernels in tests/test_gpu_pipe.py; only the copies home, read by the host, take an
+// engine of their own.)
 static bool pipe_h2d(am_pipe* p, PipeSlot* sl, void* dst, const void* src, uint64_t n) {
+  (void)sl;
   if (!n) return true;
   pipe_choose_engines(p, src, dst);
-  hsa_agent_t host;
-  if (p->eng_state > 0 && sl->insig.handle && hsa_owner(src, host)) {
-    hsa_signal_add_screlease(sl->insig, 1);
-    if (hsa_amd_memory_async_copy_on_engine(dst, p->gpu, src, host, n, 0, nullptr, sl->insig,
-                                            (hsa_amd_sdma_engine_id_t)p->eng_h2d, false) == HSA_STATUS_SUCCESS) {
-      sl->in_sdma = true;
-      return true;
-    }
-    hsa_signal_subtract_screlease(sl->insig, 1);
-    p->eng_state = -1;
-  }
   return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, p->s_in) == hipSuccess;
 }
 // The hand-over of the inputs to the compute stream: the engine copies are waited for on the host
@@ -1177,7 +1176,9 @@ static bool pipe_launch(am_pipe* p, PipeSlot* sl) {
   sl->launched = true;
   PipeSlot* prev = p->launched;
   p->launched = sl;
-  return !prev || !prev->busy || pipe_finalize(p, prev);
+  // (with two slots the previous batch's slot may already be retired and refilled by the next
+  // submission: its new batch is not launched yet and must not be finalized)
+  return !prev || !prev->busy || !prev->launched || prev->finalized || pipe_finalize(p, prev);
 }
 
 static bool pipe_flush_pending(am_pipe* p) {

@@ -119,17 +119,10 @@ AM_PHD inline void diff_caps(uint64_t R, uint64_t E, uint64_t caps[DIFF_NCAPS], 
   caps[22] = R + 2;         // ev_off
   caps[23] = E + 2;         // ev
 }
-AM_PHD inline uint64_t diff_scratch_bytes(uint64_t R, uint64_t E, uint64_t ps = 1) {
-  uint64_t c[DIFF_NCAPS];
-  diff_caps(R, E, c, ps);
-  const uint64_t sz[DIFF_NCAPS] = {sizeof(DObj), sizeof(DKid), sizeof(DKV), sizeof(DProp), sizeof(DPE), sizeof(DEdit),
-                                   sizeof(DMV), sizeof(DPst), sizeof(DVis), sizeof(DCs), sizeof(DCm), 4, 4, 4, 8, 1,
-                                   4, 4, 4, 4, 4, 4, 4, 4};
-  uint64_t t = 0;
-  for (int i = 0; i < DIFF_NCAPS; i++) t += (c[i] * sz[i] + 15) & ~(uint64_t)15;
-  return t;
-}
-AM_PHD inline void diff_scratch_bind(uint8_t* p, uint64_t R, uint64_t E, DiffScratch& w, uint64_t ps = 1) {
+// Binds the pools at p (16-byte aligned each) and returns their total bytes; the workspace layout
+// sizes the region with the same function (diff_scratch_bytes), so the two can never disagree (they
+// once rounded cops / seen_off as one pool and bound them as two: 16 bytes past the region).
+AM_PHD inline uint64_t diff_scratch_bind(uint8_t* p, uint64_t R, uint64_t E, DiffScratch& w, uint64_t ps = 1) {
   uint64_t c[DIFF_NCAPS];
   diff_caps(R, E, c, ps);
   uint64_t o = 0;
@@ -165,6 +158,11 @@ AM_PHD inline void diff_scratch_bind(uint8_t* p, uint64_t R, uint64_t E, DiffScr
   for (int i = 0; i < DIFF_NCAPS; i++) w.dcap[i] = c[i];
 #endif
   w.nobj = w.nkid = w.nkv = w.nprop = w.npe = w.ned = w.nmv = w.npst = w.nvis = w.ncs = w.ncm = w.noid = 0;
+  return o;
+}
+AM_PHD inline uint64_t diff_scratch_bytes(uint64_t R, uint64_t E, uint64_t ps = 1) {
+  DiffScratch w;
+  return diff_scratch_bind(nullptr, R, E, w, ps);
 }
 
 // ---- the replay ----

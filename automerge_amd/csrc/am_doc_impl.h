@@ -1950,8 +1950,9 @@ __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restric
       uint8_t* dst = out + uids[3 * NU + u];
       for (uint32_t q = t; q < uids[2 * NU + u]; q += T) dst[q] = src[q];
     }
-    // P7: getPatch log (lane 0; the merge arrays of the union region are dead, reuse them)
-    if (s.b.P && t == 0) {
+    // P7: getPatch log (lane 0; the merge arrays of the union region are dead, reuse them). Only for
+    // getPatch (P == 1): the applyChanges patch (P == 2) is P8's, which writes the same slot.
+    if (s.b.P == 1 && t == 0) {
       const uint64_t R1 = (uint64_t)s.b.R + 1, E1 = (uint64_t)s.b.E + 1;
       uint8_t* ps = hp<uint8_t>(s, L.pscr);
       PatchScratch w;

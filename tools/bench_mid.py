@@ -25,15 +25,17 @@ def main():
     ap.add_argument("--min-ops", type=int, default=8)
     ap.add_argument("--max-ops", type=int, default=40)
     ap.add_argument("--check", type=int, default=8)
+    ap.add_argument("--flags", choices=["diff", "patch", "none"], default="diff",
+                    help="diff: the applyChanges patch (default); patch: getPatch; none: merge only")
     a = ap.parse_args()
     import numpy as np
     import workload as W
-    from automerge_amd.batch import WANT_DIFF, Batch
+    from automerge_amd.batch import WANT_DIFF, WANT_PATCH, Batch
     t0 = time.perf_counter()
     arena, chunks, docs, ops = W.mid(0, a.docs, a.actors, a.rounds, a.min_ops, a.max_ops)
     gen_s = time.perf_counter() - t0
     docs = docs.copy()
-    docs["flags"] |= WANT_DIFF
+    docs["flags"] |= {"diff": WANT_DIFF, "patch": WANT_PATCH, "none": 0}[a.flags]
     b = Batch()
     rec = {}
     times = []
@@ -51,6 +53,7 @@ def main():
     el = min(times)
     rec.update({"workload": "mid: %d docs, %d actors x %d rounds, %d-%d ops per change" % (a.docs, a.actors, a.rounds, a.min_ops,
                                                                                           a.max_ops),
+                "flags": a.flags,
                 "ops": ops, "ops_per_doc": ops / a.docs, "ms_per_step": el * 1e3, "ops_per_s": ops / el,
                 "docs_per_s": a.docs / el, "errors": int((st != 0).sum()), "gen_s": gen_s,
                 "fast_fraction": float(np.mean(fast)),
