@@ -1278,22 +1278,43 @@ struct Diff {
       DCHKF(11, s.frow((int32_t)f));
       w.fpos[s.frow((int32_t)f)] = (int32_t)f;
     }
+#if defined(AM_DIFF_CHECK) && defined(__HIP_DEVICE_COMPILE__)
+#define DPROF(k) prof[k] = clock64()
+    uint64_t prof[6];
+#else
+#define DPROF(k)
+#endif
+    DPROF(0);
     if (meta_mode && meta_in) {
       if (!build_objects() || !meta_restore(meta_in, meta_len)) return false;
     } else if (!build_meta()) {
       return false;
     }
+    DPROF(1);
     fast_init();
     if (!ok) return false;
-    uint32_t pos = 0;
+    DPROF(2);
+    uint32_t pos = 0, ncalls = 0;
     const uint32_t nstream = s.nrows() - s.nb();
     for (uint32_t p = 0; p < s.npass() && ok; p++) {
       const uint32_t pend = s.pass_end(p) < nstream ? s.pass_end(p) : nstream;
-      while (pos < pend && ok)
+      while (pos < pend && ok) {
+        ncalls++;
         if (!apply_ops(pos, pend)) return false;
+      }
     }
+    DPROF(3);
     if (!setup_patches()) return false;
-    return emit();
+    DPROF(4);
+    const bool r = emit();
+    DPROF(5);
+#if defined(AM_DIFF_CHECK) && defined(__HIP_DEVICE_COMPILE__)
+    if (s.nrows() > 1100 && s.nrows() < 1120)
+      printf("[p8prof] rows %u out %u stream %u merge-calls %u: meta %llu init %llu ops %llu setup %llu emit %llu cycles\n",
+             s.nrows(), s.nout(), nstream, ncalls, (unsigned long long)(prof[1] - prof[0]), (unsigned long long)(prof[2] - prof[1]),
+             (unsigned long long)(prof[3] - prof[2]), (unsigned long long)(prof[4] - prof[3]), (unsigned long long)(prof[5] - prof[4]));
+#endif
+    return r;
   }
 };
 

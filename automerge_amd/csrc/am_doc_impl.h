@@ -1181,6 +1181,98 @@ __device__ static bool radix_docorder(DocShared& s, SortRec* sr, uint32_t n, uin
 }
 
 // One document by the whole workgroup (the body of k_doc below).
+// P8 (applyChanges patch, am_diff.h) of one document whose merged rows are described by src: the
+// replay into the working-form pools, the wire form at L.pwire and, with AM_DOC_META, the objectMeta
+// blob after it. One lane. (The few layout values it needs travel as scalars: a WsLayout passed by
+// reference would live in scratch memory.)
+struct P8Args {
+  uint8_t* patch;                  // working-form pools (L.patch)
+  uint64_t nrec, nmval, heap;      // their capacities
+  uint8_t* dscr;                   // replay scratch (L.dscr)
+  uint8_t* pwire;                  // wire form (L.pwire)
+  uint64_t pwire_cap;
+  uint32_t R, E, ps;
+  const uint8_t* meta;             // the handle's objectMeta blob (AM_DOC_META), or null
+  uint32_t meta_len;
+  bool meta_mode;
+};
+__device__ __forceinline__ P8Args p8_args(uint8_t* wsg, const WsLayout& L, const DocBounds& b, const am_doc_desc& dd,
+                                          const am_chunk_desc* chunks, const uint8_t* arena) {
+  P8Args a;
+  a.patch = wsg + L.patch;
+  a.nrec = L.patch_nrec; a.nmval = L.patch_nmval; a.heap = L.patch_heap;
+  a.dscr = wsg + L.dscr;
+  a.pwire = wsg + L.pwire;
+  a.pwire_cap = L.pwire_cap;
+  a.R = b.R; a.E = b.E; a.ps = (b.U & 2) ? 8 : 1;
+  a.meta_mode = (dd.flags & AM_DOC_META) != 0;
+  a.meta = nullptr;
+  a.meta_len = 0;
+  if (a.meta_mode && dd.meta_chunk) {
+    const am_chunk_desc mc = chunks[dd.meta_chunk - 1];
+    a.meta = arena + mc.off;
+    a.meta_len = mc.len;
+  }
+  return a;
+}
+// po_ / dw_: where the replay keeps its pool descriptors (k_diff passes LDS; null: locals)
+__device__ static void p8_run(const DiffSrc& src, const P8Args a, PatchOut* po_ = nullptr, DiffScratch* dw_ = nullptr) {
+  PatchOut po_local;
+  DiffScratch dw_local;
+  PatchOut& po = po_ ? *po_ : po_local;
+  DiffScratch& dw = dw_ ? *dw_ : dw_local;
+  po.rec = reinterpret_cast<PatchRec*>(a.patch + 64);
+  po.mval = reinterpret_cast<PatchVal*>(a.patch + 64 + 64 * a.nrec);
+  po.heap = a.patch + 64 + 64 * a.nrec + 32 * a.nmval;
+  po.cap_rec = a.nrec; po.cap_mval = a.nmval; po.cap_heap = a.heap;
+  diff_scratch_bind(a.dscr, a.R, a.E, dw, a.ps);
+  diff_scan(src, po, dw, a.meta_mode, a.meta, a.meta_len);
+  uint8_t* const pw = a.pwire;
+  const uint64_t wl = patch_pack(po, 0, pw, a.pwire_cap);
+  if (!wl) {
+    wire_out(po, 0, pw, a.pwire_cap);
+  } else if (a.meta_mode && !po.status) {
+    // the snapshots this call leaves, after the stream (PatchHdr2.meta_bytes)
+    const uint64_t mb = diff_meta_pack(src, dw, pw + wl, a.pwire_cap - wl);
+    if (!mb) {
+      po.status = PATCH_U_CAPACITY;
+      patch_pack(po, 0, pw, a.pwire_cap);
+    } else {
+      for (int q = 0; q < 8; q++) pw[offsetof(PatchHdr2, meta_bytes) + q] = (uint8_t)(mb >> (8 * q));
+    }
+  }
+}
+
+// k_diff (global mode): P8 of every global-mode document k_doc merged with AM_DOC_WANT_DIFF, one
+// wave per document (lane 0 replays; the other lanes exit), from the rows k_doc left in the
+// document's workspace and the counts it recorded at L.djob
+__device__ static void k_diff_one(uint32_t doc, const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
+                                  const am_doc_desc* __restrict__ docs, const DocBounds* __restrict__ bounds,
+                                  const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base, uint32_t lds_bytes,
+                                  const am_doc_result* __restrict__ results, const uint8_t* __restrict__ fast_done) {
+  if (fast_done && fast_done[doc]) return;
+  const DocBounds b = bounds[doc];
+  if (b.P != 2) return;
+  const WsLayout L = ws_layout(b);
+  if (L.hot_total <= lds_bytes && !doc_scattered(b)) return;  // an LDS-mode document: replayed in k_doc
+  if (results[doc].status) return;
+  uint8_t* const wsg = ws_base + ws_off[doc];
+  const uint32_t* job = reinterpret_cast<const uint32_t*>(wsg + L.djob);
+  // the arena view of the global mode (its staged copy when invalid UTF-8 was replaced)
+  const APtr A{((b.U & 1) && !doc_scattered(b)) ? wsg + L.input - b.span_lo : arena, 0};
+  // the replay's descriptors in LDS: as locals they sit in scratch memory, one dependent load away
+  // on every pool access of the serial chain
+  __shared__ DiffSrc src;
+  __shared__ PatchOut po;
+  __shared__ DiffScratch dw;
+  src = DiffSrc{reinterpret_cast<const Row*>(wsg + L.rows), reinterpret_cast<const Ent*>(wsg + L.ents),
+              reinterpret_cast<const SortRec*>(wsg + L.sortrec), reinterpret_cast<const uint32_t*>(wsg + L.succ_cnt),
+              reinterpret_cast<const Ent*>(wsg + L.outent), reinterpret_cast<const int32_t*>(wsg + L.etime),
+              reinterpret_cast<const uint32_t*>(wsg + L.passend), job[0], job[1], job[2], job[3], job[4], job[5],
+              reinterpret_cast<const ActorRef*>(wsg + L.actors), job[6], reinterpret_cast<const ChgRow*>(wsg + L.chg), job[7], A};
+  p8_run(src, p8_args(wsg, L, b, docs[doc], chunks, arena), &po, &dw);
+}
+
 __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
                                           const am_doc_desc* __restrict__ docs, const am_known_hash* __restrict__ known,
                                           const ChunkInfo* __restrict__ info, const DocBounds* __restrict__ bounds,
@@ -1979,79 +2071,20 @@ __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restric
       patch_scan(src, po, w, pmax);
       wire_out(po, pmax, wsg + L.pwire, L.pwire_cap);
     }
-    PH(13);
-#ifdef AM_DIFF_CHECK
-    if (t == 0 && s.b.R > 1100) printf("[dcheck] doc %u R %u before P8: P %u status %u\n", doc, s.b.R, s.b.P, s.status);
-#endif
-    // P8: the patch applyChanges returns (am_diff.h), lane 0, after the merge
+    // P8: the patch applyChanges returns (am_diff.h), one lane, after the merge. LDS-mode documents
+    // replay it here; a global-mode document leaves its counts for k_diff, a one-wave-per-document
+    // launch after this one (the replay is one lane's chain of dependent global loads: at one
+    // lane per 4-wave workgroup too few of them were in flight)
     if (s.b.P == 2 && t == 0) {
-      uint8_t* pbase = wsg + L.patch;
-      PatchOut po;
-      po.rec = reinterpret_cast<PatchRec*>(pbase + 64);
-      po.mval = reinterpret_cast<PatchVal*>(pbase + 64 + 64 * L.patch_nrec);
-      po.heap = pbase + 64 + 64 * L.patch_nrec + 32 * L.patch_nmval;
-      po.cap_rec = L.patch_nrec; po.cap_mval = L.patch_nmval; po.cap_heap = L.patch_heap;
-      DiffScratch dw;
-      diff_scratch_bind(wsg + L.dscr, s.b.R, s.b.E, dw, (s.b.U & 2) ? 8 : 1);
-      DiffSrc src{rows, ents, sr, succ_cnt, outent, reinterpret_cast<const int32_t*>(wsg + L.etime),
-                  reinterpret_cast<const uint32_t*>(wsg + L.passend), s.npass, s.nb, s.nrows, NOUT, NSUCC,
-                  s.nb_act < s.nb ? 0u : s.nb, actors, s.nactors, chg, NC, A};
-      // objectMeta of the handle (AM_DOC_META): the snapshots its previous call left, if any
-      const bool meta = (dd.flags & AM_DOC_META) != 0;
-      const uint8_t* mi = nullptr;
-      uint32_t ml = 0;
-      if (meta && dd.meta_chunk) {
-        const am_chunk_desc mc = chunks[dd.meta_chunk - 1];
-        mi = arena + mc.off;
-        ml = mc.len;
-      }
-      bool p8_skip = false;
-#ifdef AM_DIFF_CHECK
-      // diagnostics build: the replay's inputs against the layout's bounds (status 250 + which), and
-      // the document's shared bounds / layout against a fresh copy (status 260 + which: a corrupted
-      // DocShared); the header then goes to the layout's true patch slot
-      const uint64_t chk[4] = {s.nrows, NOUT, NSUCC, s.npass};
-      const uint64_t lim[4] = {s.b.R, s.b.R, (uint64_t)s.b.E + 1, (uint64_t)s.b.N + 1};
-      bool pre_ok = true;
-      for (int q = 0; q < 4 && pre_ok; q++)
-        if (chk[q] > lim[q]) { po.status = 250 + q; po.arg0 = (int64_t)chk[q]; po.arg1 = (int64_t)lim[q]; pre_ok = false; }
-      {
-        const DocBounds gb = bounds[doc];
-        const WsLayout GL = ws_layout(gb);
-        const uint64_t a[6] = {gb.R, gb.E, GL.pwire, GL.dscr, GL.total, GL.patch};
-        const uint64_t bv[6] = {s.b.R, s.b.E, L.pwire, L.dscr, L.total, L.patch};
-        for (int q = 0; q < 6 && pre_ok; q++)
-          if (a[q] != bv[q]) { po.status = 260 + q; po.arg0 = (int64_t)bv[q]; po.arg1 = (int64_t)a[q]; pre_ok = false; }
-        if (!pre_ok && po.status >= 260) {
-          wire_out(po, 0, wsg + GL.pwire, GL.pwire_cap);
-          p8_skip = true;
-        }
-      }
-      po.nrec = po.nmval = po.nheap = 0;
-      if (pre_ok)
-#endif
-      diff_scan(src, po, dw, meta, mi, ml);
-      uint8_t* const pw = wsg + L.pwire;
-      const uint64_t wl = p8_skip ? 1 : patch_pack(po, 0, pw, L.pwire_cap);
-#ifdef AM_DIFF_CHECK
-      if (s.dbg_canary == 0xffffu && dbg_canary_hit(wsg + L.total)) s.dbg_canary = 50;  // P8
-      if (s.b.R > 1100)
-        printf("[dcheck] doc %u R %u P8 done: status %u nrec %u nmval %u nheap %u wl %llu pwire %llu cap %llu total %llu\n", doc,
-               s.b.R, po.status, (unsigned)po.nrec, (unsigned)po.nmval, (unsigned)po.nheap, (unsigned long long)wl,
-               (unsigned long long)L.pwire, (unsigned long long)L.pwire_cap, (unsigned long long)L.total);
-#endif
-      if (p8_skip) {
-      } else if (!wl) {
-        wire_out(po, 0, pw, L.pwire_cap);
-      } else if (meta && !po.status) {
-        // the snapshots this call leaves, after the stream (PatchHdr2.meta_bytes)
-        const uint64_t mb = diff_meta_pack(src, dw, pw + wl, L.pwire_cap - wl);
-        if (!mb) {
-          po.status = PATCH_U_CAPACITY;
-          patch_pack(po, 0, pw, L.pwire_cap);
-        } else {
-          for (int q = 0; q < 8; q++) pw[offsetof(PatchHdr2, meta_bytes) + q] = (uint8_t)(mb >> (8 * q));
-        }
+      if constexpr (kHotLds) {
+        DiffSrc src{rows, ents, sr, succ_cnt, outent, reinterpret_cast<const int32_t*>(wsg + L.etime),
+                    reinterpret_cast<const uint32_t*>(wsg + L.passend), s.npass, s.nb, s.nrows, NOUT, NSUCC,
+                    s.nb_act < s.nb ? 0u : s.nb, actors, s.nactors, chg, NC, A};
+        p8_run(src, p8_args(wsg, L, s.b, dd, chunks, arena));
+      } else {
+        uint32_t* job = reinterpret_cast<uint32_t*>(wsg + L.djob);
+        job[0] = s.npass; job[1] = s.nb; job[2] = s.nrows; job[3] = NOUT;
+        job[4] = NSUCC; job[5] = s.nb_act < s.nb ? 0u : s.nb; job[6] = s.nactors; job[7] = NC;
       }
     }
     // heads for the host (hot region may be LDS): mirror into the global workspace

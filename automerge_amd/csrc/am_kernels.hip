@@ -807,6 +807,19 @@ constexpr uint32_t kDocT = DOC_T_GLB;
 #include "am_doc_impl.h"
 #undef K_DOC_WAVES_ATTR
 }  // namespace glb_mode
+// P8 of the global-mode documents (glb_mode::k_diff_one): one wave per document, lane 0 replays.
+// The replay is a chain of dependent loads, so resident waves decide its speed: registers capped for
+// AM_DIFF_WAVES waves per SIMD (the rest of the state in scratch)
+#ifndef AM_DIFF_WAVES
+#define AM_DIFF_WAVES 8
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AM_DIFF_WAVES, 8))) k_diff(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
+                                             const am_doc_desc* __restrict__ docs, const DocBounds* __restrict__ bounds,
+                                             const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base, uint32_t lds_bytes,
+                                             const am_doc_result* __restrict__ results, const uint8_t* __restrict__ fast_done) {
+  if (threadIdx.x) return;
+  glb_mode::k_diff_one(blockIdx.x, arena, chunks, docs, bounds, ws_off, ws_base, lds_bytes, results, fast_done);
+}
 #include "am_doc_fast.h"
 #include "am_hist_dev.h"
 
@@ -1060,9 +1073,13 @@ void am_launch_doc(const BatchDev& b, hipStream_t s) {
     }
     hipLaunchKernelGGL(lds_mode::k_doc, dim3(grid), dim3(DOC_T), b.lds_bytes, s, b.arena, b.chunks, b.docs, b.known,
                        b.info, b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd, rest);
-    if (b.max_hot_host > b.lds_bytes)
+    if (b.max_hot_host > b.lds_bytes) {
       hipLaunchKernelGGL(glb_mode::k_doc, dim3(b.ndocs), dim3(DOC_T_GLB), 0, s, b.arena, b.chunks, b.docs, b.known, b.info,
                          b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd, nullptr);
+      if (b.any_diff)
+        hipLaunchKernelGGL(k_diff, dim3(b.ndocs), dim3(64), 0, s, b.arena, b.chunks, b.docs, b.bounds, b.ws_off, b.ws,
+                           b.lds_bytes, b.results, fd);
+    }
   }
 }
 __global__ void __launch_bounds__(256) k_out_hash_ws(am_doc_result* __restrict__ res, uint32_t ndocs, uint8_t* __restrict__ ws,

@@ -60,6 +60,7 @@ struct WsLayout {
   uint64_t pwire, pwire_cap;  // the same log in wire form (PatchHdr2 + stream, am_patch.h)
   uint64_t etime, passend, dscr;  // applyChanges patch (P == 2): succ-entry times, pass ends, replay pools
   uint64_t enc_x;             // encode scratch of waves 1..3 of a large document (0: wave 0 encodes alone)
+  uint64_t djob;              // P == 2, global mode: the counts k_doc leaves for k_diff (8 x u32)
   uint64_t colbuf[OC_NCOLS + DC_NCOLS];
   // unknown op columns (UC > 0): instance table, decoded values, per-(source, column) instance
   // map, the output columns' ids / lengths / positions, per-row group offsets, encoded output
@@ -207,8 +208,9 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
     L.etime = take(4 * (E + 1));
     L.passend = take(4 * (N + 1));
     L.dscr = take(diff_scratch_bytes(R, E, (b.U & 2) ? 8 : 1));
+    L.djob = take(32);
   } else {
-    L.etime = L.passend = L.dscr = 0;
+    L.etime = L.passend = L.dscr = L.djob = 0;
   }
   // large documents: waves 1..3 of the global-mode workgroup encode columns of their own (P6)
   L.enc_x = nm >= 1024 ? take(3 * 32 * nm) : 0;

@@ -1,0 +1,6 @@
+#!/bin/bash
+set -o pipefail
+O=gpurun_out/r5
+mkdir -p $O
+timeout -k 10 300 python -u tools/bench_mid.py --docs 8192 --steps 2 --check 8 --flags diff > $O/mid_diff2.json 2> $O/mid_diff2.err || exit 1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_mid.py tests/test_gpu_text.py tests/test_gpu_apply_patch.py tests/test_gpu_backend_batch.py > $O/tests_u.log 2>&1 || exit 1
