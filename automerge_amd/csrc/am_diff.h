@@ -20,6 +20,9 @@
 // sized from the row and entry counts; running out reports PATCH_U_CAPACITY, never a wrong patch.
 #pragma once
 #include "am_patch.h"
+#if defined(__HIP_DEVICE_COMPILE__)
+#include "am_wave.h"
+#endif
 
 // ---- pools ----
 struct DVal { uint32_t vtag, dt; int64_t v0, v1; };  // a patch value as the log stores it
@@ -52,6 +55,14 @@ struct DPst { int32_t elem_row; int32_t vis_head, vis_tail; int32_t has_child; i
 struct DVis { int32_t row; int32_t next; };
 struct DCs { int64_t op_ctr; int64_t value; int32_t op_actor; int32_t nleft; int32_t next; int32_t pad; };
 struct DCm { int64_t ctr; int32_t actor; int32_t state; int32_t next; int32_t pad; };
+
+// a workgroup barrier in the wide replay (k_diff's workgroup is one wave: it orders the lanes'
+// global writes before the next loop's reads)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DSYNC() do { if constexpr (Wide) __syncthreads(); } while (0)
+#else
+#define DSYNC() do { } while (0)
+#endif
 
 #define DIFF_NCAPS_MAX 24
 struct DiffScratch {
@@ -176,7 +187,15 @@ AM_PHD inline uint64_t diff_scratch_bytes(uint64_t R, uint64_t E, uint64_t ps = 
 //   pred_actor(i, k); rank(a); patch_value's val_len / copy_value / value_int / value_f64_bits;
 //   nactors(); actor_len(a); copy_actor(a, dst); nchg(); chg_actor(c); chg_seq(c); npass();
 //   pass_end(p) (stream index where pass p ends)
-template <class Src>
+//
+// Wide (k_diff): all 64 lanes of the wave run the replay's chain in lockstep -- every lane loads and
+// stores the same addresses and takes the same branches, so the chain costs what one lane's does --
+// and the steps that are scans or searches spread over the lanes: the presence sets below (a bit per
+// F position instead of Fenwick trees: a prefix count or a k-th lookup is two rounds of independent
+// loads and a wave scan, not log2(n) dependent loads), the per-row setup (fast_init, F positions,
+// the documentPatch objectMeta pass), 64-way searches over F and the linear pool lookups. Serial
+// (LDS-mode documents in k_doc, one lane of a larger workgroup): the same replay on Fenwick trees.
+template <class Src, bool Wide = false>
 struct Diff {
   const Src& s;
   DiffScratch& w;
@@ -184,6 +203,19 @@ struct Diff {
   bool ok;
   uint32_t cur_t = 0;   // succ / row events of stream times < cur_t are in the trees
   int32_t ptotal = 0;   // present rows
+  uint32_t nw = 0;      // wide presence sets: 64-bit words over F (the counts per 4096 positions follow)
+  int64_t lo_oc = -3;   // fast_seek: the first F position of the last object sought
+  int32_t lo_oa = -3, lo_f = 0;
+#if defined(AM_DIFF_CHECK) && defined(__HIP_DEVICE_COMPILE__)
+  // diagnostics build: cycles per replay section (apply_ops), printed for large documents
+  uint64_t pacc[10] = {};
+  uint64_t pt = 0;
+#define DPT() pt = clock64()
+#define DPA(k) do { const uint64_t t_ = clock64(); pacc[k] += t_ - pt; pt = t_; } while (0)
+#else
+#define DPT()
+#define DPA(k)
+#endif
   AM_PHD Diff(const Src& src, DiffScratch& ws, PatchOut& out) : s(src), w(ws), o(out), ok(true) {}
 
   // ---- replay state in Fenwick trees over F positions ----
@@ -227,11 +259,119 @@ struct Diff {
       if (pos + step <= n && b[pos + step] < k) { pos += step; k -= b[pos]; }
     return pos;
   }
+  // ---- presence sets: bitp (present rows), bitv (visible elements) over F positions ----
+  // Wide layout in the same pool: nw 64-bit words, then one int32 count per 64 words (the pool's
+  // R + 2 int32 always hold them: 8 * ceil(R / 64) + 4 * ceil(R / 4096) <= 4 * (R + 2)).
+  AM_PHD void set_add(int32_t* b, uint32_t i, int32_t d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (Wide) {
+      DCHK(16, i >> 6 < nw ? 0 : ~0ull);
+      uint64_t* wd = reinterpret_cast<uint64_t*>(b);
+      const uint64_t bit = 1ull << (i & 63);
+      wd[i >> 6] = d > 0 ? wd[i >> 6] | bit : wd[i >> 6] & ~bit;
+      b[2 * nw + (i >> 12)] += d;
+      return;
+    }
+#endif
+    bit_add(b, i, d);
+  }
+  AM_PHD int32_t set_pre(const int32_t* b, uint32_t i) const {  // members at F positions [0, i)
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (Wide) {
+      const uint64_t* wd = reinterpret_cast<const uint64_t*>(b);
+      const int32_t* cn = b + 2 * nw;
+      const uint32_t wi = i >> 6, si = wi >> 6, l = wave::lane_id();
+      uint32_t acc = 0;
+      for (uint32_t q = l; q < si; q += 64) acc += (uint32_t)cn[q];
+      if ((si << 6) + l < wi) acc += (uint32_t)__popcll(wd[(si << 6) + l]);
+      if ((i & 63) && l == 0) acc += (uint32_t)__popcll(wd[wi] & ((1ull << (i & 63)) - 1));
+      return (int32_t)wave::sum_all(acc);
+    }
+#endif
+    return bit_pre(b, i);
+  }
+  AM_PHD uint32_t set_kth(const int32_t* b, int32_t k) const {  // F position of the k-th (1-based) member
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (Wide) {
+      const uint64_t* wd = reinterpret_cast<const uint64_t*>(b);
+      const int32_t* cn = b + 2 * nw;
+      const uint32_t l = wave::lane_id(), nsb = (nw + 63) >> 6;
+      uint32_t sb = nsb ? nsb - 1 : 0;
+      for (uint32_t base = 0; base < nsb; base += 64) {
+        const uint32_t c = base + l < nsb ? (uint32_t)cn[base + l] : 0u;
+        const uint32_t inc = wave::incl_add(c);
+        const uint64_t m = __ballot(inc >= (uint32_t)k);
+        if (m) {
+          const uint32_t j = (uint32_t)__builtin_ctzll(m);
+          sb = base + j;
+          k -= (int32_t)wave::bcast(inc - c, (int)j);
+          break;
+        }
+        k -= (int32_t)wave::bcast(inc, 63);
+      }
+      const uint32_t wq = (sb << 6) + l;
+      const uint64_t x = wq < nw ? wd[wq] : 0ull;
+      const uint32_t c = (uint32_t)__popcll(x);
+      const uint32_t inc = wave::incl_add(c);
+      const uint64_t m = __ballot(inc >= (uint32_t)k);
+      const uint32_t j = m ? (uint32_t)__builtin_ctzll(m) : 63u;
+      k -= (int32_t)wave::bcast(inc - c, (int)j);
+      const uint64_t word = wave::bcast(x, (int)j);
+      const uint64_t upto = l == 63 ? word : word & ((2ull << l) - 1);
+      const uint64_t m2 = __ballot(((word >> l) & 1) && (int32_t)__popcll(upto) == k);
+      return (((sb << 6) + j) << 6) + (m2 ? (uint32_t)__builtin_ctzll(m2) : 0u);
+    }
+#endif
+    return bit_kth(b, k);
+  }
   // first present F position >= f, or nout()
   AM_PHD int32_t next_present(int32_t f) const {
     if (f >= (int32_t)s.nout()) return (int32_t)s.nout();
-    const int32_t k = bit_pre(w.bitp, (uint32_t)f);
-    return k >= ptotal ? (int32_t)s.nout() : (int32_t)bit_kth(w.bitp, k + 1);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (Wide) {
+      const uint64_t* wd = reinterpret_cast<const uint64_t*>(w.bitp);
+      const uint32_t wi = (uint32_t)f >> 6, l = wave::lane_id();
+      const uint64_t x = wd[wi] & (~0ull << (f & 63));
+      if (x) return (int32_t)((wi << 6) + (uint32_t)__builtin_ctzll(x));
+      for (uint32_t base = wi + 1; base < nw; base += 64) {
+        const uint64_t y = base + l < nw ? wd[base + l] : 0ull;
+        const uint64_t m = __ballot(y != 0);
+        if (m) {
+          const uint32_t j = (uint32_t)__builtin_ctzll(m);
+          return (int32_t)(((base + j) << 6) + (uint32_t)__builtin_ctzll(wave::bcast(y, (int)j)));
+        }
+      }
+      return (int32_t)s.nout();
+    }
+#endif
+    const int32_t k = set_pre(w.bitp, (uint32_t)f);
+    return k >= ptotal ? (int32_t)s.nout() : (int32_t)set_kth(w.bitp, k + 1);
+  }
+  // first index in [a, b) where pred is false (pred holds on a prefix of [a, b)); wide: 64 probes
+  // per round
+  template <class P>
+  AM_PHD int32_t first_false(int32_t a, int32_t b, P pred) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (Wide) {
+      const int32_t l = (int32_t)wave::lane_id();
+      while (a < b) {
+        const int32_t step = (b - a + 63) / 64;
+        const int32_t m = a + l * step;
+        const uint64_t bal = __ballot(m < b && pred(m));
+        const int32_t t = (int32_t)__popcll(bal);
+        if (t == 0) return a;
+        const int32_t nb = a + t * step < b ? a + t * step : b;
+        a = a + (t - 1) * step + 1;
+        b = nb;
+      }
+      return a;
+    }
+#endif
+    while (a < b) {
+      const int32_t m = (a + b) / 2;
+      if (pred(m)) a = m + 1; else b = m;
+    }
+    return a;
   }
   AM_PHD uint32_t hslot(int64_t ctr, int32_t actor) const {
     uint64_t h = (uint64_t)ctr * 0x9E3779B97F4A7C15ull ^ ((uint64_t)(uint32_t)actor + 1u) * 0xC2B2AE3D27D4EB4Full;
@@ -251,11 +391,14 @@ struct Diff {
     if (e < 0) return;
     DCHK(19, e);
     const int32_t before = w.live[e];
-    w.live[e] += d;
-    if (before == 0 && d > 0) bit_add(w.bitv, (uint32_t)e, 1);
-    else if (before > 0 && w.live[e] == 0) bit_add(w.bitv, (uint32_t)e, -1);
+    w.live[e] = before + d;
+    if (before == 0 && d > 0) set_add(w.bitv, (uint32_t)e, 1);
+    else if (before > 0 && before + d == 0) set_add(w.bitv, (uint32_t)e, -1);
   }
   AM_PHD void fast_init() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (Wide) { fast_init_wide(); return; }
+#endif
     const uint32_t n = s.nout(), nstream = s.nrows() - s.nb();
     DCHK(16, n);
     DCHK(18, n);
@@ -302,6 +445,99 @@ struct Diff {
       }
     cur_t = 0;
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+  // fast_init over the lanes: the same pools, rows 64 at a time (estart by a segmented scan, the
+  // hash by CAS, the succ buckets by atomic counts then a scan, the presence words by ballots)
+  __device__ void fast_init_wide() {
+    const uint32_t n = s.nout(), nstream = s.nrows() - s.nb(), l = wave::lane_id();
+    nw = (n + 63) >> 6;
+    const uint32_t nsb = (nw + 63) >> 6;
+    uint64_t* wp = reinterpret_cast<uint64_t*>(w.bitp);
+    uint64_t* wv = reinterpret_cast<uint64_t*>(w.bitv);
+    int32_t* cp = w.bitp + 2 * nw;
+    int32_t* cv = w.bitv + 2 * nw;
+    DCHK(22, nstream);
+    for (uint32_t q = l; q < nsb; q += 64) { cp[q] = 0; cv[q] = 0; }
+    for (uint32_t h = l; h <= w.hmask; h += 64) w.hash[h] = -1;
+    for (uint32_t t = l; t <= nstream; t += 64) w.ev_off[t] = 0;
+    for (uint32_t f = l; f < n; f += 64) w.live[f] = 0;
+    __syncthreads();
+    int32_t carry = -1;  // estart of the previous row
+    int64_t coc = 0;
+    int32_t coa = 0;
+    ptotal = 0;
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t f = base + l;
+      const bool in = f < n;
+      const int32_t r = in ? s.frow((int32_t)f) : 0;
+      const bool hk = in && s.has_key(r), ins = in && s.insert(r);
+      const int64_t oc = in ? s.obj_ctr(r) : 0;
+      const int32_t oa = in ? s.obj_actor(r) : 0;
+      const int64_t poc = wave::up1(oc, coc);
+      const int32_t poa = wave::up1(oa, coa);
+      // estart: -1 (map row, or a list row whose predecessor is in another object), f (insert
+      // row), else the predecessor's: the last resetting row at or before this lane, or the carry
+      const bool reset = !in || hk || ins || poc != oc || poa != oa;
+      const int32_t v = in && !hk && ins ? (int32_t)f : -1;
+      const uint64_t rm = __ballot(reset);
+      const uint64_t upto = l == 63 ? rm : rm & ((2ull << l) - 1);
+      const int32_t sv = __shfl(v, upto ? 63 - __builtin_clzll(upto) : 0);
+      const int32_t es = upto ? sv : carry;
+      uint32_t nsc = 0;
+      if (in) {
+        w.estart[f] = es;
+        if (!hk && ins) {
+          uint32_t h = hslot(s.id_ctr(r), s.id_actor(r));
+          while (atomicCAS(&w.hash[h], -1, (int32_t)f) >= 0) h = (h + 1) & w.hmask;
+        }
+        for (uint32_t k = 0; k < s.f_nsucc(f); k++) {
+          const int64_t t = s.f_succ_time(f, k);
+          if (t < 0) nsc++;
+          else if (t < (int64_t)nstream) atomicAdd(&w.ev_off[t + 1], 1u);
+        }
+        w.nsc[f] = (int32_t)nsc;
+      }
+      carry = wave::bcast(es, 63);
+      coc = wave::bcast(oc, 63);
+      coa = wave::bcast(oa, 63);
+      const bool pres = in && rtime(r) < 0;
+      const uint64_t word = __ballot(pres);
+      wp[base >> 6] = word;
+      const int32_t pc = (int32_t)__popcll(word);
+      cp[base >> 12] += pc;
+      ptotal += pc;
+      if (pres && nsc == 0 && es >= 0) atomicAdd(&w.live[es], 1);
+    }
+    __syncthreads();
+    for (uint32_t base = 0; base < n; base += 64) {
+      const uint32_t f = base + l;
+      const uint64_t word = __ballot(f < n && w.live[f] > 0);
+      wv[base >> 6] = word;
+      cv[base >> 12] += (int32_t)__popcll(word);
+    }
+    uint32_t run = 0;  // ev_off[t + 1] += ev_off[t]: bucket starts
+    for (uint32_t base = 0; base <= nstream; base += 64) {
+      const uint32_t t = base + l;
+      const uint32_t inc = wave::incl_add(t <= nstream ? w.ev_off[t] : 0u) + run;
+      if (t <= nstream) w.ev_off[t] = inc;
+      run = wave::bcast(inc, 63);
+    }
+    __syncthreads();
+    for (uint32_t f = l; f < n; f += 64)  // bucket fill (the order inside a bucket does not matter)
+      for (uint32_t k = 0; k < s.f_nsucc(f); k++) {
+        const int64_t t = s.f_succ_time(f, k);
+        if (t >= 0 && t < (int64_t)nstream) w.ev[atomicAdd(&w.ev_off[t], 1u)] = (int32_t)f;
+      }
+    __syncthreads();
+    for (uint32_t c = (nstream >> 6) + 1; c-- > 0;) {  // ev_off[t] = ev_off[t - 1], top chunk first
+      const uint32_t t = (c << 6) + l;
+      const uint32_t x = t >= 1 && t <= nstream ? w.ev_off[t - 1] : 0u;
+      if (t <= nstream) w.ev_off[t] = x;
+    }
+    __syncthreads();
+    cur_t = 0;
+  }
+#endif
   AM_PHD void advance(int64_t W) {
     const uint32_t nstream = s.nrows() - s.nb();
     while ((int64_t)cur_t < W && cur_t < nstream) {
@@ -309,7 +545,7 @@ struct Diff {
       DCHK(11, srow(t));
       const int32_t f = w.fpos[srow(t)];
       if (f >= 0) {
-        bit_add(w.bitp, (uint32_t)f, 1);
+        set_add(w.bitp, (uint32_t)f, 1);
         ptotal++;
         if (w.nsc[f] == 0) elem_row_live(f, 1);
       }
@@ -321,32 +557,31 @@ struct Diff {
   }
   // seek of the op at stream row `first` from the trees: (skip, visible) as seek() computes them.
   // Returns false when the op has no F anchor (its element is unknown): seek() then decides.
-  AM_PHD bool fast_seek(int32_t first, uint32_t& skip, int64_t& vis) const {
+  AM_PHD bool fast_seek(int32_t first, uint32_t& skip, int64_t& vis) {
     const int64_t q_oc = s.obj_ctr(first);
     const int32_t q_oa = s.obj_actor(first);
     const int32_t n = (int32_t)s.nout();
-    auto obj_before = [&](int32_t r) {  // document order of objects: _root, then (ctr, actor)
-      if (q_oa < 0 || q_oc < 0) return false;
-      const int64_t oc = s.obj_ctr(r);
-      const int32_t oa = s.obj_actor(r);
-      if (oc < 0 || oa < 0) return true;
-      return oc < q_oc || (oc == q_oc && act_lt(oa, q_oa));
-    };
-    int32_t lo = 0, hi = n;
-    while (lo < hi) {
-      const int32_t m = (lo + hi) / 2;
-      if (obj_before(s.frow(m))) lo = m + 1; else hi = m;
+    // the object's first F position (F is fixed for the whole replay: kept for the last object)
+    if (q_oc != lo_oc || q_oa != lo_oa) {
+      lo_f = first_false(0, n, [&](int32_t m) {  // document order of objects: _root, then (ctr, actor)
+        if (q_oa < 0 || q_oc < 0) return false;
+        const int32_t r = s.frow(m);
+        const int64_t oc = s.obj_ctr(r);
+        const int32_t oa = s.obj_actor(r);
+        if (oc < 0 || oa < 0) return true;
+        return oc < q_oc || (oc == q_oc && act_lt(oa, q_oa));
+      });
+      lo_oc = q_oc;
+      lo_oa = q_oa;
     }
+    const int32_t lo = lo_f;
     int32_t target;
     if (s.has_key(first)) {
-      int32_t a = lo, b = n;
-      while (a < b) {
-        const int32_t m = (a + b) / 2;
+      const int32_t a = first_false(lo, n, [&](int32_t m) {
         const int32_t r = s.frow(m);
-        if (s.obj_ctr(r) == q_oc && s.obj_actor(r) == q_oa && s.has_key(r) && s.key_cmp(r, first) < 0) a = m + 1;
-        else b = m;
-      }
-      skip = (uint32_t)bit_pre(w.bitp, (uint32_t)a);
+        return s.obj_ctr(r) == q_oc && s.obj_actor(r) == q_oa && s.has_key(r) && s.key_cmp(r, first) < 0;
+      });
+      skip = (uint32_t)set_pre(w.bitp, (uint32_t)a);
       vis = 0;
       return true;
     }
@@ -357,8 +592,8 @@ struct Diff {
       target = elem_find(s.key_ctr(first), s.key_actor(first));
     }
     if (target < 0) return false;
-    skip = (uint32_t)bit_pre(w.bitp, (uint32_t)target);
-    vis = (int64_t)(bit_pre(w.bitv, (uint32_t)target) - bit_pre(w.bitv, (uint32_t)lo));
+    skip = (uint32_t)set_pre(w.bitp, (uint32_t)target);
+    vis = (int64_t)(set_pre(w.bitv, (uint32_t)target) - set_pre(w.bitv, (uint32_t)lo));
     return true;
   }
 
@@ -396,6 +631,17 @@ struct Diff {
 
   // ---- objectMeta / patches ----
   AM_PHD int32_t obj_find(int64_t ctr, int32_t actor) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (Wide) {
+      const uint32_t l = wave::lane_id();
+      for (uint32_t base = 0; base < w.nobj; base += 64) {
+        const uint32_t k = base + l;
+        const uint64_t m = __ballot(k < w.nobj && w.obj[k].ctr == ctr && w.obj[k].actor == actor);
+        if (m) return (int32_t)(base + (uint32_t)__builtin_ctzll(m));
+      }
+      return -1;
+    }
+#endif
     for (uint32_t k = 0; k < w.nobj; k++) if (w.obj[k].ctr == ctr && w.obj[k].actor == actor) return (int32_t)k;
     return -1;
   }
@@ -586,6 +832,17 @@ struct Diff {
   // contiguous in document order, so only the last entry can match.
   AM_PHD int32_t pst_get(int32_t row, bool whole_doc) const {
     if (whole_doc) return w.npst && elem_eq(w.pst[w.npst - 1].elem_row, row) ? (int32_t)w.npst - 1 : -1;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (Wide) {
+      const uint32_t l = wave::lane_id();
+      for (uint32_t base = 0; base < w.npst; base += 64) {
+        const uint32_t k = base + l;
+        const uint64_t m = __ballot(k < w.npst && elem_eq(w.pst[k].elem_row, row));
+        if (m) return (int32_t)(base + (uint32_t)__builtin_ctzll(m));
+      }
+      return -1;
+    }
+#endif
     for (uint32_t k = 0; k < w.npst; k++) if (elem_eq(w.pst[k].elem_row, row)) return (int32_t)k;
     return -1;
   }
@@ -899,11 +1156,14 @@ struct Diff {
     const int32_t f_oa = s.obj_actor(first);
     uint32_t skip;
     int64_t visible;
+    DPT();
     advance(W);
+    DPA(0);
     if (!fast_seek(first, skip, visible) &&
         !seek(f_oc, f_oa, first, s.key_ctr(first), s.key_actor(first), insert, s.id_ctr(first), s.id_actor(first), W, skip,
               visible))
       return fail(PATCH_U_VALUE);  // Reference element not found (the merge reports it first)
+    DPA(1);
     if (s.has_key(first)) visible = 0;
     int64_t list_index = visible;
     const int32_t ob = obj_find(f_oa < 0 ? -1 : f_oc, f_oa);
@@ -912,7 +1172,7 @@ struct Diff {
     bool found_list_elem = false, elem_visible = false;
     w.npst = 0; w.nvis = 0; w.ncs = 0; w.ncm = 0;  // propState = {}
     // the first doc op: the present row after `skip` present rows
-    Cur dc{(int32_t)skip < ptotal ? (int32_t)bit_kth(w.bitp, (int32_t)skip + 1) : (int32_t)s.nout()};
+    Cur dc{(int32_t)skip < ptotal ? (int32_t)set_kth(w.bitp, (int32_t)skip + 1) : (int32_t)s.nout()};
     int32_t doc_f = dc.f < (int32_t)s.nout() ? dc.f : -1;  // F position of docOp, -1: null
     if (doc_f >= 0) dc.f++;
     uint32_t doc_old = doc_f >= 0 ? nsucc_at(doc_f, W) : 0u;
@@ -921,7 +1181,11 @@ struct Diff {
     bool have_lck = false;
     int32_t lck_row = -1;
     if (!oid_add(ob)) return false;
+    DPA(2);
     for (;;) {
+#if defined(AM_DIFF_CHECK) && defined(__HIP_DEVICE_COMPILE__)
+      pacc[7]++;
+#endif
       if (nc == 0) {
         found_list_elem = false;
         seen_top = 0;
@@ -960,6 +1224,7 @@ struct Diff {
           pos++;  // readNextChangeOp
         }
       }
+      DPA(3);
       if (nc > 0) change_op = w.cops[0];
       const int32_t dr = doc_f >= 0 ? s.frow(doc_f) : -1;
       const bool in_obj = dr >= 0 && s.obj_actor(dr) == s.obj_actor(change_op) && s.obj_ctr(dr) == s.obj_ctr(change_op);
@@ -1010,6 +1275,7 @@ struct Diff {
       } else {
         take_doc = true;
       }
+      DPA(4);
       if (take_doc) {
         if (s.insert(dr) && elem_visible) { elem_visible = false; list_index++; }
         if (nsucc_at(doc_f, (int64_t)pos) == 0) elem_visible = true;
@@ -1017,6 +1283,7 @@ struct Diff {
         doc_f = dc.f < (int32_t)s.nout() ? dc.f : -1;
         if (doc_f >= 0) { dc.f++; doc_old = nsucc_at(doc_f, W); }
       }
+      DPA(5);
       if (take_chg > 0) {
         for (uint32_t i = 0; i < take_chg; i++) {
           const int32_t op = w.cops[i];
@@ -1029,6 +1296,7 @@ struct Diff {
         for (uint32_t k = 0; k + take_chg < nc; k++) { w.cops[k] = w.cops[k + take_chg]; w.seen_off[k] = w.seen_off[k + take_chg]; }
         nc -= take_chg;
       }
+      DPA(6);
     }
     return true;
   }
@@ -1042,7 +1310,57 @@ struct Diff {
     int64_t list_index = 0;
     int32_t ob = 0;
     w.npst = 0; w.nvis = 0; w.ncs = 0; w.ncm = 0;
-    for (uint32_t i = 0; i < s.nmeta_rows(); i++) {
+    const uint32_t nm = s.nmeta_rows();
+#if defined(__HIP_DEVICE_COMPILE__)
+    // wide: only the rows of key / element groups (runs of one key or element in one object) that
+    // hold a make op reach update_property -- in whole-document mode it changes nothing for the rest
+    // (no objectMeta entry, no children snapshot; propState is matched against its last entry only,
+    // and a group never recurs in its object). Group starts go to cops, the make flags to tmp.
+    if constexpr (Wide) {
+      const uint32_t l = wave::lane_id();
+      DCHKF(14, nm);
+      for (uint32_t r = l; r < nm; r += 64) w.tmp[r] = 0;
+      int32_t carry = 0;
+      for (uint32_t base = 0; base < nm; base += 64) {
+        const uint32_t r = base + l;
+        const bool in = r < nm;
+        const bool st = in && (r == 0 || s.obj_ctr((int32_t)r) != s.obj_ctr((int32_t)r - 1) ||
+                               s.obj_actor((int32_t)r) != s.obj_actor((int32_t)r - 1) || !elem_eq((int32_t)r - 1, (int32_t)r));
+        const uint64_t sm = __ballot(st || !in);
+        const uint64_t upto = l == 63 ? sm : sm & ((2ull << l) - 1);
+        const int32_t g = upto ? (int32_t)base + 63 - __builtin_clzll(upto) : carry;
+        if (in) w.cops[r] = g;
+        carry = wave::bcast(g, 63);
+      }
+      __syncthreads();
+      for (uint32_t r = l; r < nm; r += 64)
+        if (is_make(s.action((int32_t)r))) w.tmp[w.cops[r]] = 1;
+      __syncthreads();
+    }
+#endif
+    uint32_t mbase = 0;
+    uint64_t mmask = 0;
+    bool mset = false;
+    auto next_row = [&](uint32_t i) -> uint32_t {  // the next row at or after i that update_property needs
+#if defined(__HIP_DEVICE_COMPILE__)
+      if constexpr (Wide) {
+        while (i < nm) {
+          if (!mset || i < mbase || i >= mbase + 64) {
+            mset = true;
+            mbase = i;
+            const uint32_t r = i + wave::lane_id();
+            mmask = __ballot(r < nm && w.tmp[w.cops[r]] != 0);
+          }
+          const uint64_t rest = mmask & (~0ull << (i - mbase));
+          if (rest) return mbase + (uint32_t)__builtin_ctzll(rest);
+          i = mbase + 64;
+        }
+        return nm;
+      }
+#endif
+      return i;
+    };
+    for (uint32_t i = next_row(0); i < nm; i = next_row(i + 1)) {
       const int32_t r = (int32_t)i;
       const int64_t oc = s.obj_ctr(r);
       const int32_t oa = s.obj_actor(r);
@@ -1205,7 +1523,15 @@ struct Diff {
   // (meta_restore); the objects themselves (parent, parentKey, type) follow from the make ops.
   AM_PHD bool build_objects() {
     if (obj_new(-1, -1, 0) < 0) return false;
-    for (uint32_t i = 0; i < s.nmeta_rows(); i++) {
+    const uint32_t nm = s.nmeta_rows();
+    for (uint32_t base = 0; base < nm; base += 64) {
+      uint64_t mm = ~0ull;  // the chunk's make rows (wide: one ballot; serial: each row tested below)
+#if defined(__HIP_DEVICE_COMPILE__)
+      if constexpr (Wide) mm = __ballot(base + wave::lane_id() < nm && is_make(s.action((int32_t)(base + wave::lane_id()))));
+#endif
+      for (; mm; mm &= mm - 1) {
+      const uint32_t i = base + (uint32_t)__builtin_ctzll(mm);
+      if (i >= nm) break;
       const int32_t r = (int32_t)i;
       const int64_t a = s.action(r);
       if (!is_make(a)) continue;
@@ -1213,10 +1539,11 @@ struct Diff {
       const int32_t oa = s.obj_actor(r);
       const int32_t ob = obj_find(oa < 0 ? -1 : s.obj_ctr(r), oa);
       if (ob < 0) return fail(PATCH_U_VALUE);
-      const int32_t nm = obj_new(s.id_ctr(r), s.id_actor(r), obj_type_of_action(a));
-      if (nm < 0) return false;
-      w.obj[nm].parent = ob;
-      w.obj[nm].pk_row = r;
+      const int32_t no = obj_new(s.id_ctr(r), s.id_actor(r), obj_type_of_action(a));
+      if (no < 0) return false;
+      w.obj[no].parent = ob;
+      w.obj[no].pk_row = r;
+      }
     }
     return true;
   }
@@ -1273,14 +1600,23 @@ struct Diff {
 
   AM_PHD bool run() {
     DCHKF(11, s.nrows() ? s.nrows() - 1 : 0);
-    for (uint32_t r = 0; r < s.nrows(); r++) w.fpos[r] = -1;
-    for (uint32_t f = 0; f < s.nout(); f++) {
+#if defined(AM_DIFF_CHECK) && defined(__HIP_DEVICE_COMPILE__)
+    const uint64_t prof6 = clock64();
+#endif
+    uint32_t l0 = 0, step = 1;  // wide: the lanes split the per-row loops
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (Wide) { l0 = wave::lane_id(); step = 64; }
+#endif
+    for (uint32_t r = l0; r < s.nrows(); r += step) w.fpos[r] = -1;
+    DSYNC();
+    for (uint32_t f = l0; f < s.nout(); f += step) {
       DCHKF(11, s.frow((int32_t)f));
       w.fpos[s.frow((int32_t)f)] = (int32_t)f;
     }
+    DSYNC();
 #if defined(AM_DIFF_CHECK) && defined(__HIP_DEVICE_COMPILE__)
 #define DPROF(k) prof[k] = clock64()
-    uint64_t prof[6];
+    uint64_t prof[7];
 #else
 #define DPROF(k)
 #endif
@@ -1295,6 +1631,7 @@ struct Diff {
     if (!ok) return false;
     DPROF(2);
     uint32_t pos = 0, ncalls = 0;
+    (void)ncalls;
     const uint32_t nstream = s.nrows() - s.nb();
     for (uint32_t p = 0; p < s.npass() && ok; p++) {
       const uint32_t pend = s.pass_end(p) < nstream ? s.pass_end(p) : nstream;
@@ -1309,10 +1646,14 @@ struct Diff {
     const bool r = emit();
     DPROF(5);
 #if defined(AM_DIFF_CHECK) && defined(__HIP_DEVICE_COMPILE__)
-    if (s.nrows() > 1100 && s.nrows() < 1120)
-      printf("[p8prof] rows %u out %u stream %u merge-calls %u: meta %llu init %llu ops %llu setup %llu emit %llu cycles\n",
-             s.nrows(), s.nout(), nstream, ncalls, (unsigned long long)(prof[1] - prof[0]), (unsigned long long)(prof[2] - prof[1]),
-             (unsigned long long)(prof[3] - prof[2]), (unsigned long long)(prof[4] - prof[3]), (unsigned long long)(prof[5] - prof[4]));
+    if (((s.nrows() > 1100 && s.nrows() < 1104) || s.nrows() > 20000) && (!Wide || wave::lane_id() == 0))
+      printf("[p8prof] wide %d rows %u out %u stream %u merge-calls %u loops %llu: fpos %llu meta %llu init %llu ops %llu setup %llu emit %llu"
+             " | advance %llu seek %llu start %llu pull %llu match+doc-upd %llu doc-next %llu chg-upd %llu cycles\n",
+             (int)Wide, s.nrows(), s.nout(), nstream, ncalls, (unsigned long long)pacc[7], (unsigned long long)(prof[0] - prof6),
+             (unsigned long long)(prof[1] - prof[0]), (unsigned long long)(prof[2] - prof[1]),
+             (unsigned long long)(prof[3] - prof[2]), (unsigned long long)(prof[4] - prof[3]), (unsigned long long)(prof[5] - prof[4]),
+             (unsigned long long)pacc[0], (unsigned long long)pacc[1], (unsigned long long)pacc[2], (unsigned long long)pacc[3],
+             (unsigned long long)pacc[4], (unsigned long long)pacc[5], (unsigned long long)pacc[6]);
 #endif
     return r;
   }
@@ -1320,13 +1661,13 @@ struct Diff {
 
 // meta: the call keeps objectMeta for its handle (restored from meta_in when given, documentPatch's
 // otherwise); diff_meta_pack then writes what the call leaves.
-template <class Src>
+template <bool Wide = false, class Src>
 AM_PHD inline bool diff_scan(const Src& src, PatchOut& o, DiffScratch& w, bool meta = false, const uint8_t* meta_in = nullptr,
                              uint32_t meta_len = 0) {
   o.nrec = o.nmval = o.nheap = 0;
   o.status = 0;
   o.arg0 = o.arg1 = 0;
-  Diff<Src> d(src, w, o);
+  Diff<Src, Wide> d(src, w, o);
   d.meta_mode = meta;
   d.meta_in = meta_in;
   d.meta_len = meta_len;

@@ -1215,7 +1215,9 @@ __device__ __forceinline__ P8Args p8_args(uint8_t* wsg, const WsLayout& L, const
   }
   return a;
 }
-// po_ / dw_: where the replay keeps its pool descriptors (k_diff passes LDS; null: locals)
+// po_ / dw_: where the replay keeps its pool descriptors (k_diff passes LDS; null: locals).
+// Wide: every lane of the wave runs it (k_diff); else one lane.
+template <bool Wide = false>
 __device__ static void p8_run(const DiffSrc& src, const P8Args a, PatchOut* po_ = nullptr, DiffScratch* dw_ = nullptr) {
   PatchOut po_local;
   DiffScratch dw_local;
@@ -1226,7 +1228,7 @@ __device__ static void p8_run(const DiffSrc& src, const P8Args a, PatchOut* po_ 
   po.heap = a.patch + 64 + 64 * a.nrec + 32 * a.nmval;
   po.cap_rec = a.nrec; po.cap_mval = a.nmval; po.cap_heap = a.heap;
   diff_scratch_bind(a.dscr, a.R, a.E, dw, a.ps);
-  diff_scan(src, po, dw, a.meta_mode, a.meta, a.meta_len);
+  diff_scan<Wide>(src, po, dw, a.meta_mode, a.meta, a.meta_len);
   uint8_t* const pw = a.pwire;
   const uint64_t wl = patch_pack(po, 0, pw, a.pwire_cap);
   if (!wl) {
@@ -1244,12 +1246,14 @@ __device__ static void p8_run(const DiffSrc& src, const P8Args a, PatchOut* po_ 
 }
 
 // k_diff (global mode): P8 of every global-mode document k_doc merged with AM_DOC_WANT_DIFF, one
-// wave per document (lane 0 replays; the other lanes exit), from the rows k_doc left in the
+// wave per document (the wide replay: all 64 lanes, see am_diff.h), from the rows k_doc left in the
 // document's workspace and the counts it recorded at L.djob
+template <bool Wide>
 __device__ static void k_diff_one(uint32_t doc, const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
                                   const am_doc_desc* __restrict__ docs, const DocBounds* __restrict__ bounds,
                                   const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base, uint32_t lds_bytes,
                                   const am_doc_result* __restrict__ results, const uint8_t* __restrict__ fast_done) {
+  if (!Wide && threadIdx.x) return;
   if (fast_done && fast_done[doc]) return;
   const DocBounds b = bounds[doc];
   if (b.P != 2) return;
@@ -1270,7 +1274,7 @@ __device__ static void k_diff_one(uint32_t doc, const uint8_t* __restrict__ aren
               reinterpret_cast<const Ent*>(wsg + L.outent), reinterpret_cast<const int32_t*>(wsg + L.etime),
               reinterpret_cast<const uint32_t*>(wsg + L.passend), job[0], job[1], job[2], job[3], job[4], job[5],
               reinterpret_cast<const ActorRef*>(wsg + L.actors), job[6], reinterpret_cast<const ChgRow*>(wsg + L.chg), job[7], A};
-  p8_run(src, p8_args(wsg, L, b, docs[doc], chunks, arena), &po, &dw);
+  p8_run<Wide>(src, p8_args(wsg, L, b, docs[doc], chunks, arena), &po, &dw);
 }
 
 __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,

@@ -15,6 +15,7 @@
 //   k_out_hash_ws thread per document: container checksum of the merged document (columnar.js:659)
 #include <hip/hip_runtime.h>
 #include <cstdlib>
+#include <cstring>
 
 #include "am_dev_util.h"
 #include "am_layout.h"
@@ -807,18 +808,19 @@ constexpr uint32_t kDocT = DOC_T_GLB;
 #include "am_doc_impl.h"
 #undef K_DOC_WAVES_ATTR
 }  // namespace glb_mode
-// P8 of the global-mode documents (glb_mode::k_diff_one): one wave per document, lane 0 replays.
-// The replay is a chain of dependent loads, so resident waves decide its speed: registers capped for
-// AM_DIFF_WAVES waves per SIMD (the rest of the state in scratch)
+// P8 of the global-mode documents (glb_mode::k_diff_one): one wave per document. Wide: all lanes run
+// the replay (scans and searches spread over them: few, large documents); else lane 0 alone (many
+// documents: the waves themselves fill the machine). The chain is dependent loads, so resident waves
+// decide its speed: registers capped for AM_DIFF_WAVES waves per SIMD
 #ifndef AM_DIFF_WAVES
 #define AM_DIFF_WAVES 8
 #endif
+template <bool Wide>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AM_DIFF_WAVES, 8))) k_diff(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
                                              const am_doc_desc* __restrict__ docs, const DocBounds* __restrict__ bounds,
                                              const uint64_t* __restrict__ ws_off, uint8_t* __restrict__ ws_base, uint32_t lds_bytes,
                                              const am_doc_result* __restrict__ results, const uint8_t* __restrict__ fast_done) {
-  if (threadIdx.x) return;
-  glb_mode::k_diff_one(blockIdx.x, arena, chunks, docs, bounds, ws_off, ws_base, lds_bytes, results, fast_done);
+  glb_mode::k_diff_one<Wide>(blockIdx.x, arena, chunks, docs, bounds, ws_off, ws_base, lds_bytes, results, fast_done);
 }
 #include "am_doc_fast.h"
 #include "am_hist_dev.h"
@@ -1076,9 +1078,20 @@ void am_launch_doc(const BatchDev& b, hipStream_t s) {
     if (b.max_hot_host > b.lds_bytes) {
       hipLaunchKernelGGL(glb_mode::k_doc, dim3(b.ndocs), dim3(DOC_T_GLB), 0, s, b.arena, b.chunks, b.docs, b.known, b.info,
                          b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd, nullptr);
-      if (b.any_diff)
-        hipLaunchKernelGGL(k_diff, dim3(b.ndocs), dim3(64), 0, s, b.arena, b.chunks, b.docs, b.bounds, b.ws_off, b.ws,
-                           b.lds_bytes, b.results, fd);
+      if (b.any_diff) {
+        // wide replay for batches of fewer documents than wave slots (AM_DIFF_MODE=wide|lane0 overrides)
+        static const int mode = [] {
+          const char* v = std::getenv("AM_DIFF_MODE");
+          return !v ? 0 : std::strcmp(v, "wide") == 0 ? 1 : std::strcmp(v, "lane0") == 0 ? 2 : 0;
+        }();
+        const bool wide = mode == 1 || (mode == 0 && b.ndocs < 1024);
+        if (wide)
+          hipLaunchKernelGGL(k_diff<true>, dim3(b.ndocs), dim3(64), 0, s, b.arena, b.chunks, b.docs, b.bounds, b.ws_off, b.ws,
+                             b.lds_bytes, b.results, fd);
+        else
+          hipLaunchKernelGGL(k_diff<false>, dim3(b.ndocs), dim3(64), 0, s, b.arena, b.chunks, b.docs, b.bounds, b.ws_off, b.ws,
+                             b.lds_bytes, b.results, fd);
+      }
     }
   }
 }
