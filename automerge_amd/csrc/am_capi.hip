@@ -451,6 +451,20 @@ static bool inflate_stage(am_batch* b, const uint8_t* arena, uint64_t arena_len,
   return true;
 }
 
+// LDS budget of one k_doc workgroup (AM_LDS_BUDGET; AM_LDS_BUDGET_KB overrides it, for A/B runs).
+// A batch that wants patches keeps 40 KB: a document between 40 and 64 KB of hot set then merges in
+// global mode and replays its applyChanges patch in k_diff at 8 waves per SIMD (C5 pairs, 65,536
+// per batch: 232 ms) instead of in LDS mode at 2 workgroups per CU (361 ms; 44 ms against 74 ms
+// without the patch)
+static uint32_t lds_budget(bool any_diff) {
+  static const uint32_t v = [] {
+    const char* e = std::getenv("AM_LDS_BUDGET_KB");
+    const unsigned long k = e ? std::strtoul(e, nullptr, 10) : 0ul;
+    return k >= 8 && k <= 160 ? (uint32_t)(k * 1024) : 0u;
+  }();
+  return v ? v : any_diff ? 40u * 1024 : (uint32_t)AM_LDS_BUDGET;
+}
+
 static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, const am_chunk_desc* chunks, uint32_t nchunks,
                        const am_doc_desc* docs, uint32_t ndocs, const am_known_hash* known, uint32_t nknown) {
   am_engine* e = b->eng;
@@ -485,7 +499,7 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   b->ws_need = total;
   // dynamic LDS of the document workgroups: the largest hot working set, capped by the budget
   uint64_t lds = (max_hot + 15) & ~(uint64_t)15;
-  if (lds > AM_LDS_BUDGET) lds = AM_LDS_BUDGET;
+  if (lds > lds_budget(b->any_diff)) lds = lds_budget(b->any_diff);
   b->lds_bytes = (uint32_t)lds;
   b->max_hot_v = max_hot;
   // k_doc_fast (am_doc_fast.h) for the documents in its envelope; AM_FAST=0 turns it off
@@ -938,7 +952,7 @@ extern "C" am_pipe* am_pipe_create(am_engine* eng, const am_pipe_caps* caps, am_
       if (hipEventCreate(e) != hipSuccess) return fail(p, "automerge_amd: cannot create a HIP event");
     if (hsa_signal_create(0, 0, nullptr, &sl->home) != HSA_STATUS_SUCCESS) sl->home.handle = 0;
     if (hsa_signal_create(0, 0, nullptr, &sl->insig) != HSA_STATUS_SUCCESS) sl->insig.handle = 0;
-    b.lds_bytes = AM_LDS_BUDGET;       // k_doc takes what k_doc_fast leaves, in either mode
+    b.lds_bytes = lds_budget(false);   // k_doc takes what k_doc_fast leaves, in either mode (set per batch)
     b.max_hot_v = ~0ull;
     b.fast_lds = c.fast_lds;
   }
@@ -1211,6 +1225,7 @@ static int pipe_submit(am_pipe* p, const uint8_t* arena, uint64_t arena_len, con
   b.nchunks = nchunks;
   b.ndocs = ndocs;
   b.any_diff = any_diff;
+  b.lds_bytes = lds_budget(any_diff);
   sl->packed = packed;
   sl->arena_len = arena_len;
   // inputs

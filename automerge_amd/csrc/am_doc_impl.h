@@ -2075,17 +2075,19 @@ __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restric
       patch_scan(src, po, w, pmax);
       wire_out(po, pmax, wsg + L.pwire, L.pwire_cap);
     }
-    // P8: the patch applyChanges returns (am_diff.h), one lane, after the merge. LDS-mode documents
-    // replay it here; a global-mode document leaves its counts for k_diff, a one-wave-per-document
+    // P8: the patch applyChanges returns (am_diff.h), after the merge. LDS-mode documents replay it
+    // here (the wide replay); a global-mode document leaves its counts for k_diff, a one-wave-per-document
     // launch after this one (the replay is one lane's chain of dependent global loads: at one
     // lane per 4-wave workgroup too few of them were in flight)
-    if (s.b.P == 2 && t == 0) {
+    if (s.b.P == 2) {
       if constexpr (kHotLds) {
+        // the workgroup is one wave: every lane runs the wide replay over the LDS-resident rows
+        static_assert(!kHotLds || kDocT == 64, "the LDS-mode P8 replay is one wave");
         DiffSrc src{rows, ents, sr, succ_cnt, outent, reinterpret_cast<const int32_t*>(wsg + L.etime),
                     reinterpret_cast<const uint32_t*>(wsg + L.passend), s.npass, s.nb, s.nrows, NOUT, NSUCC,
                     s.nb_act < s.nb ? 0u : s.nb, actors, s.nactors, chg, NC, A};
-        p8_run(src, p8_args(wsg, L, s.b, dd, chunks, arena));
-      } else {
+        p8_run<true>(src, p8_args(wsg, L, s.b, dd, chunks, arena));
+      } else if (t == 0) {
         uint32_t* job = reinterpret_cast<uint32_t*>(wsg + L.djob);
         job[0] = s.npass; job[1] = s.nb; job[2] = s.nrows; job[3] = NOUT;
         job[4] = NSUCC; job[5] = s.nb_act < s.nb ? 0u : s.nb; job[6] = s.nactors; job[7] = NC;

@@ -18,8 +18,10 @@
 #define AM_HD __host__ __device__
 #endif
 
-// LDS budget of one document workgroup (bytes of dynamic shared memory)
-#define AM_LDS_BUDGET (40 * 1024)
+// LDS budget of one document workgroup (bytes of dynamic shared memory). 64 KB: a C5 pair merged
+// (~100 rows, a 40-64 KB hot set) runs in LDS mode, 1.7x faster than global mode (2 workgroups
+// per CU against 4 four-wave ones; gfx950 has 160 KB of LDS per CU)
+#define AM_LDS_BUDGET (64 * 1024)
 
 struct DocBounds {
   uint32_t R;   // op rows (base + every change in the list)

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--docs", type=int, default=65536)
     ap.add_argument("--text", type=int, default=0, help="C3 text histories of this many changes instead of C4")
     ap.add_argument("--patch", action="store_true", help="stage with AM_DOC_WANT_DIFF (the applyChanges patch)")
+    ap.add_argument("--c5", action="store_true", help="C5 pairs merged: base + both sides' 10 changes (~100 rows)")
     args = ap.parse_args()
     import workload
     from automerge_amd import _native
@@ -32,7 +33,10 @@ def main():
     lib = _native.lib
     f = lib.amx_phase_cycles
     f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-    if args.text:
+    if args.c5:
+        arena, chunks, docs, ops = workload.c5(0, args.docs)
+        docs = docs.copy()
+    elif args.text:
         arena, chunks, docs, ops = workload.text(0, args.docs, args.text, 100, 10)
     else:
         arena, chunks, docs, ops = workload.c4(0, args.docs)
