@@ -274,11 +274,33 @@ std::vector<uint8_t> make_chunk(const uint8_t checksum[4], uint8_t type, const s
 // =============================================================================================
 // engine / batch
 // =============================================================================================
-// device arenas the batched per-handle calls compact their outputs into (k_pipe_compact)
+// pinned host memory (hipHostMalloc), grow-only (by at least half again)
+template <class T>
+struct PinBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t n) {
+    if (n <= cap && p) return true;
+    const size_t want = std::max<size_t>(n ? n : 1, cap + cap / 2);
+    if (p) { (void)hipHostFree(p); p = nullptr; cap = 0; }
+    if (hipHostMalloc(reinterpret_cast<void**>(&p), want * sizeof(T), hipHostMallocDefault) != hipSuccess) {
+      p = nullptr;
+      return false;
+    }
+    cap = want;
+    return true;
+  }
+  ~PinBuf() { if (p) (void)hipHostFree(p); }
+};
+// device arenas the batched per-handle calls compact their outputs into (k_pipe_compact), and the
+// pinned host buffers their input arena is packed into and their outputs come home in (no
+// zero-filled std::vector per call, DMA-speed copies)
 struct CollectBufs {
   DevBuf<uint64_t> olen, ooff, plen, poff, tmp, totals;
   DevBuf<am_doc_summary> summ;
   DevBuf<uint8_t> out, pat, hashes;
+  PinBuf<uint8_t> h_arena, h_out, h_pat;
+  PinBuf<am_doc_summary> h_summ;
 };
 struct am_engine {
   int device = 0;
@@ -1584,7 +1606,7 @@ bool chunk_heads(const std::vector<uint8_t>& chunk, std::vector<std::array<uint8
 
 // Every document's merged chunk and patch log of the last run of batch b, densely in two host
 // arenas (k_pipe_lens / k_pipe_compact: a sizing pass, then the copies; one D2H each).
-bool batch_collect(am_batch* b, std::vector<am_doc_summary>& summ, std::vector<uint8_t>& out, std::vector<uint8_t>& pat) {
+bool batch_collect(am_batch* b, const am_doc_summary*& summ, const uint8_t*& out, const uint8_t*& pat) {
   am_engine* e = b->eng;
   if (!e->coll) e->coll = new CollectBufs();
   CollectBufs& c = *e->coll;
@@ -1599,14 +1621,15 @@ bool batch_collect(am_batch* b, std::vector<am_doc_summary>& summ, std::vector<u
   if (hipMemcpyAsync(tot, c.totals.p, sizeof tot, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
     return false;
   if (!c.out.ensure(tot[0] + 16) || !c.pat.ensure(tot[1] + 16)) return false;
+  if (!c.h_summ.ensure(nd + 1) || !c.h_out.ensure(tot[0] + 16) || !c.h_pat.ensure(tot[1] + 16)) return false;
   am_launch_pipe_compact(d, c.olen.p, c.ooff.p, c.plen.p, c.poff.p, c.tmp.p, c.totals.p, c.out.p, tot[0], c.pat.p, tot[1],
                          c.summ.p, s);
-  summ.resize(nd);
-  out.resize(tot[0]);
-  pat.resize(tot[1]);
-  if (nd && hipMemcpyAsync(summ.data(), c.summ.p, sizeof(am_doc_summary) * nd, hipMemcpyDeviceToHost, s) != hipSuccess) return false;
-  if (tot[0] && hipMemcpyAsync(out.data(), c.out.p, tot[0], hipMemcpyDeviceToHost, s) != hipSuccess) return false;
-  if (tot[1] && hipMemcpyAsync(pat.data(), c.pat.p, tot[1], hipMemcpyDeviceToHost, s) != hipSuccess) return false;
+  if (nd && hipMemcpyAsync(c.h_summ.p, c.summ.p, sizeof(am_doc_summary) * nd, hipMemcpyDeviceToHost, s) != hipSuccess) return false;
+  if (tot[0] && hipMemcpyAsync(c.h_out.p, c.out.p, tot[0], hipMemcpyDeviceToHost, s) != hipSuccess) return false;
+  if (tot[1] && hipMemcpyAsync(c.h_pat.p, c.pat.p, tot[1], hipMemcpyDeviceToHost, s) != hipSuccess) return false;
+  summ = c.h_summ.p;
+  out = c.h_out.p;
+  pat = c.h_pat.p;
   return hipStreamSynchronize(s) == hipSuccess && hipGetLastError() == hipSuccess;
 }
 
@@ -1677,7 +1700,10 @@ bool run_many(am_engine* e, const std::vector<ManyJob>& jobs, std::vector<ManyOu
     nmeta += m;
   }
   const uint32_t nchunks = c0[n] + nmeta;
-  std::vector<uint8_t> arena(moff[n]);
+  if (!e->coll) e->coll = new CollectBufs();
+  std::vector<uint8_t> arena_v;  // pageable fallback when pinned memory is short
+  uint8_t* arena = e->coll->h_arena.ensure(moff[n] + 16) ? e->coll->h_arena.p : (arena_v.resize(moff[n] + 16), arena_v.data());
+  const uint64_t arena_len = moff[n];
   std::vector<am_chunk_desc> cds(nchunks);
   std::vector<am_known_hash> known(kb[n]);
   std::vector<uint32_t> mchunk(n, 0);
@@ -1692,7 +1718,7 @@ bool run_many(am_engine* e, const std::vector<ManyJob>& jobs, std::vector<ManyOu
     if (j.base && !j.base->empty()) {
       dd.base_chunk = (int64_t)c;
       cds[c++] = {o, (uint32_t)j.base->size(), j.base_verified ? 1u : 0u};
-      std::memcpy(arena.data() + o, j.base->data(), j.base->size());
+      std::memcpy(arena + o, j.base->data(), j.base->size());
       o += j.base->size();
     }
     dd.chg_begin = c;
@@ -1700,7 +1726,7 @@ bool run_many(am_engine* e, const std::vector<ManyJob>& jobs, std::vector<ManyOu
     if (j.chg)
       for (auto& ch : *j.chg) {
         cds[c++] = {o, (uint32_t)ch.size(), 0};
-        if (!ch.empty()) std::memcpy(arena.data() + o, ch.data(), ch.size());
+        if (!ch.empty()) std::memcpy(arena + o, ch.data(), ch.size());
         o += ch.size();
       }
     dd.known_begin = kb[i];
@@ -1713,7 +1739,7 @@ bool run_many(am_engine* e, const std::vector<ManyJob>& jobs, std::vector<ManyOu
       if (moff[i + 1] > moff[i]) {
         dd.meta_chunk = mchunk[i] + 1;
         cds[mchunk[i]] = {moff[i], (uint32_t)j.meta->size(), AM_CHUNK_RAW};
-        std::memcpy(arena.data() + moff[i], j.meta->data(), j.meta->size());
+        std::memcpy(arena + moff[i], j.meta->data(), j.meta->size());
       }
     }
     dds[i] = dd;
@@ -1721,7 +1747,7 @@ bool run_many(am_engine* e, const std::vector<ManyJob>& jobs, std::vector<ManyOu
   clk.mark("pack");
   am_batch* b = scratch_batch(e);
   am_error ce;
-  if (am_batch_stage(b, arena.data(), arena.size(), cds.data(), nchunks, dds.data(), (uint32_t)n, known.data(),
+  if (am_batch_stage(b, arena, arena_len, cds.data(), nchunks, dds.data(), (uint32_t)n, known.data(),
                      (uint32_t)known.size(), &ce) ||
       am_batch_run(b) || am_batch_sync(b, &ce)) {
     err = {AM_U_CAPACITY, false, std::string("automerge_amd: GPU pipeline failed: ") + ce.message};
@@ -1731,9 +1757,8 @@ bool run_many(am_engine* e, const std::vector<ManyJob>& jobs, std::vector<ManyOu
   std::vector<am_doc_result> rr(n);
   std::vector<uint8_t> hs(32ull * nchunks);
   std::vector<int32_t> cst(nchunks);
-  std::vector<am_doc_summary> summ;
-  std::vector<uint8_t> out, pat;
-  if (!e->coll) e->coll = new CollectBufs();
+  const am_doc_summary* summ = nullptr;
+  const uint8_t *out = nullptr, *pat = nullptr;
   bool ok = am_batch_results(b, rr.data()) == 0 && e->coll->hashes.ensure(32ull * nchunks + 16);
   if (ok && nchunks) {
     am_launch_chunk_hashes(b->info.p, nchunks, e->coll->hashes.p, e->stream);
@@ -1763,8 +1788,8 @@ bool run_many(am_engine* e, const std::vector<ManyJob>& jobs, std::vector<ManyOu
     for (uint32_t k = 0; k < cn; k++) std::memcpy(res.hashes[k].data(), hs.data() + 32ull * (cb + k), 32);
     if (rr[i].status) {
       std::string actor;
-      if (rr[i].arg_actor_len && rr[i].arg_actor_off + rr[i].arg_actor_len <= arena.size())
-        actor = hexs(arena.data() + rr[i].arg_actor_off, rr[i].arg_actor_len);
+      if (rr[i].arg_actor_len && rr[i].arg_actor_off + rr[i].arg_actor_len <= arena_len)
+        actor = hexs(arena + rr[i].arg_actor_off, rr[i].arg_actor_len);
       o.err = {rr[i].status, false, message_for(rr[i].status, rr[i].arg0, rr[i].arg1, actor)};
       return;
     }
@@ -1773,13 +1798,13 @@ bool run_many(am_engine* e, const std::vector<ManyJob>& jobs, std::vector<ManyOu
       o.err = {AM_U_CAPACITY, false, "automerge_amd: output compaction failed"};
       return;
     }
-    res.out.assign(out.begin() + sm.out_off, out.begin() + sm.out_off + sm.out_len);
+    res.out.assign(out + sm.out_off, out + sm.out_off + sm.out_len);
     if (!chunk_heads(res.out, res.heads)) {
       o.err = {AM_U_VALUE, false, "automerge_amd: corrupt merged document"};
       return;
     }
     if (jobs[i].patch_mode) {
-      res.patch.assign(pat.begin() + sm.patch_off, pat.begin() + sm.patch_off + sm.patch_len);
+      res.patch.assign(pat + sm.patch_off, pat + sm.patch_off + sm.patch_len);
       split_meta(res);
     }
     o.ok = true;
@@ -2638,8 +2663,8 @@ static int am_doc_apply_changes_batch_impl(size_t n, am_doc* const* docs, const 
       call_info(d, info ? info + c.i : nullptr);
     });
     clk.mark("commit");
-    am_par_for(outs.size(), [&](size_t k) { outs[k] = ManyOut(); });
-    if (graph.empty()) am_par_for(calls.size(), [&](size_t k) { calls[k] = Call(); });
+    am_reclaim(outs);
+    if (graph.empty()) am_reclaim(calls);
     calls.clear();
     if (!graph.empty()) {
       std::vector<am_doc*> gd;

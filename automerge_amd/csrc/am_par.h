@@ -6,9 +6,13 @@
 
 #include <algorithm>
 #include <atomic>
-#include <thread>
+#include <condition_variable>
+#include <deque>
 #include <exception>
+#include <functional>
+#include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 inline unsigned am_host_threads() {
@@ -49,4 +53,54 @@ void am_par_for(size_t n, F f) {
   work();
   for (auto& x : th) x.join();
   if (first) std::rethrow_exception(first);
+}
+
+// Deferred reclamation: the per-document buffers a batched call leaves (millions of small vectors
+// for 200k handles: 140-400 ms of frees on the workers, measured) are destroyed on one background
+// thread instead of on the caller's critical path. AM_RECLAIM=0 destroys them in place, on the
+// workers, as before. The thread is started on first use (never before a fork of the caller's).
+class AmReclaimer {
+ public:
+  static AmReclaimer& get() {
+    static AmReclaimer* r = new AmReclaimer();  // never destroyed: the thread may outlive main()
+    return *r;
+  }
+  void push(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  AmReclaimer() { std::thread([this] { run(); }).detach(); }
+  void run() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return !q_.empty(); });
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+};
+// hands the vector's elements to the reclaimer (v is left empty)
+template <class T>
+void am_reclaim(std::vector<T>& v) {
+  static const bool on = [] { const char* e = getenv("AM_RECLAIM"); return !(e && e[0] == '0'); }();
+  if (!on) {
+    am_par_for(v.size(), [&](size_t i) { v[i] = T(); });
+    std::vector<T>().swap(v);
+    return;
+  }
+  auto p = std::make_shared<std::vector<T>>(std::move(v));
+  v.clear();
+  AmReclaimer::get().push([p]() mutable { p.reset(); });
 }

@@ -606,8 +606,7 @@ extern "C" int am_sync_generate(size_t n, am_doc* const* docs, const uint8_t* co
     }
   }
   clk.mark("out");
-  am_par_for(n, [&](size_t i) { gs[i] = Gen(); });  // the per-document buffers, freed on the workers
-  std::vector<Gen>().swap(gs);
+  am_reclaim(gs);  // the per-document buffers, freed off the critical path
   clk.mark("free");
   clk.print("generate", n);
   return nfail;
@@ -837,8 +836,7 @@ extern "C" int am_sync_receive_batch(size_t n, am_doc* const* docs, const uint8_
     nfail += code != 0;
   }
   clk.mark("out");
-  am_par_for(n, [&](size_t i) { rs[i] = R(); });
-  std::vector<R>().swap(rs);
+  am_reclaim(rs);
   clk.mark("free");
   clk.print("receive", n);
   return nfail;

@@ -9,7 +9,7 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d $OUT/$c -o $c -- \
-    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-pcie --check 0 > $OUT/$c.log 2>&1 || { echo "$c pass failed"; tail -5 $OUT/$c.log; exit 1; }
+    python3 $R/bench.py --steps 2 --warmup 1 --mode resident --no-cpu-baseline --check 0 > $OUT/$c.log 2>&1 || { echo "$c pass failed"; tail -5 $OUT/$c.log; exit 1; }
   echo "$c ok"
 done
 cd $R && python3 tools/traffic.py $OUT $OUT/traffic_k_doc.json
