@@ -96,6 +96,7 @@ _sigs = {
     "am_batch_doc_heads": (C.c_int, [P, C.c_uint32, P, C.c_uint32, C.POINTER(C.c_uint32)]),
     "am_batch_stage_times": (C.c_int, [P, C.POINTER(C.c_float)]),
     "am_batch_workspace_bytes": (C.c_uint64, [P]),
+    "am_batch_workspace_plan": (C.c_uint64, [P]),
     "am_batch_kernel_info": (C.c_int, [P, P]),
     "am_batch_doc_plan": (C.c_int, [P, C.c_uint32, P]),
     "am_batch_fast_slices": (C.c_int, [P, P]),

@@ -182,6 +182,11 @@ class Batch:
     def workspace_bytes(self):
         return N.lib.am_batch_workspace_bytes(self._b)
 
+    def workspace_plan(self):
+        """The scanned per-document plans (compact ones for k_doc_fast's documents), without the
+        overflow reserve workspace_bytes() includes."""
+        return N.lib.am_batch_workspace_plan(self._b)
+
     def kernel_info(self):
         """{k_doc LDS bytes, k_doc_fast LDS bytes per document, largest k_doc hot set} of the staged batch."""
         out = np.zeros(3, np.uint64)

@@ -329,13 +329,15 @@ struct am_batch {
   uint32_t fast_lds = 0;
   bool fast_only = false;
   bool any_diff = false;
+  bool compact = false;       // k_doc_fast's documents get the compact workspace plan (ws_layout)
   uint32_t lds_bytes = 0;
   uint64_t max_hot_v = 0;
   DevBuf<uint8_t> ws;
   DevBuf<am_doc_result> results;
   DevBuf<int32_t> chg_state;
   uint32_t nchunks = 0, ndocs = 0;
-  uint64_t ws_need = 0;
+  uint64_t ws_need = 0;       // workspace held: the scanned plans + the overflow reserve
+  uint64_t ws_plan = 0;       // the scanned plans alone (compact plans for k_doc_fast's documents)
   bool timed = false;
   uint32_t inflated = 0;      // change chunks inflated on the GPU by the last stage
   float inflate_ms = 0.f;     // their two inflate passes (HIP events)
@@ -346,6 +348,7 @@ struct am_batch {
     b.arena = arena.p; b.chunks = chunks.p; b.docs = docs.p; b.known = known.p; b.info = info.p; b.hdr = hdr.p; b.bounds = bounds.p;
     b.ws_bytes = ws_bytes.p; b.ws_off = ws_off.p; b.scan_tmp = scan_tmp.p; b.ws_total = ws_total.p; b.max_hot = max_hot.p; b.lds_bytes = lds_bytes; b.max_hot_host = max_hot_v; b.ws = ws.p;
     b.fast_lds = fast_lds; b.fast_done = fast_done.p; b.fast_only = fast_only; b.any_diff = any_diff; b.rest = rest.p;
+    b.compact = compact;
     b.ws_cap = ws.cap; b.results = results.p; b.chg_state = chg_state.p; b.nchunks = nchunks; b.ndocs = ndocs;
     return b;
   }
@@ -478,6 +481,11 @@ static bool inflate_stage(am_batch* b, const uint8_t* arena, uint64_t arena_len,
 // global mode and replays its applyChanges patch in k_diff at 8 waves per SIMD (C5 pairs, 65,536
 // per batch: 232 ms) instead of in LDS mode at 2 workgroups per CU (361 ms; 44 ms against 74 ms
 // without the patch)
+// compact workspace plans for k_doc_fast's documents (AM_WS_COMPACT=0: every document gets k_doc's)
+static bool ws_compact_on() {
+  static const bool v = [] { const char* e = std::getenv("AM_WS_COMPACT"); return !(e && e[0] == '0'); }();
+  return v;
+}
 static uint32_t lds_budget(bool any_diff) {
   static const uint32_t v = [] {
     const char* e = std::getenv("AM_LDS_BUDGET_KB");
@@ -495,7 +503,7 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   // 64 bytes of slack: k_doc_fast stages whole 16-byte words of a document's span
   if (!b->arena.ensure(arena_len + 64) || !b->chunks.ensure(nchunks) || !b->docs.ensure(ndocs) || !b->known.ensure(nknown) ||
       !b->info.ensure(nchunks) || !b->hdr.ensure(nchunks) || !b->bounds.ensure(ndocs) || !b->ws_bytes.ensure(ndocs) || !b->ws_off.ensure(ndocs) ||
-      !b->scan_tmp.ensure(am_scan_tmp_elems(ndocs)) || !b->ws_total.ensure(1) || !b->max_hot.ensure(2) ||
+      !b->scan_tmp.ensure(am_scan_tmp_elems(ndocs)) || !b->ws_total.ensure(1) || !b->max_hot.ensure(4) ||
       !b->fast_done.ensure(ndocs) || !b->rest.ensure(ndocs + 1) || !b->results.ensure(ndocs) ||
       !b->chg_state.ensure(nchunks))
     return false;
@@ -508,25 +516,31 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   b->any_diff = false;
   for (uint32_t d = 0; d < ndocs && !b->any_diff; d++) b->any_diff = (docs[d].flags & (AM_DOC_WANT_DIFF | AM_DOC_WANT_PATCH)) != 0;
   if (!inflate_stage(b, arena, arena_len, chunks, nchunks, docs, ndocs)) return false;
+  // k_doc_fast (am_doc_fast.h) for the documents in its envelope; AM_FAST=0 turns it off
+  const char* fe = std::getenv("AM_FAST");
+  const bool fast_on = !(fe && fe[0] == '0');
+  b->compact = fast_on && ws_compact_on();
   // sizing pass: chunk counts -> per-document workspace bounds -> total
   BatchDev d = b->dev();
   am_launch_chunks(d, s);
   am_launch_bounds(d, s);
-  uint64_t total = 0, max_hot = 0, max_fast = 0;
+  uint64_t total = 0, max_hot = 0, max_fast = 0, saved = 0;
   if (ndocs) HIPCHECK(hipMemcpyAsync(&total, b->ws_total.p, sizeof total, hipMemcpyDeviceToHost, s));
   if (ndocs) HIPCHECK(hipMemcpyAsync(&max_hot, b->max_hot.p, sizeof max_hot, hipMemcpyDeviceToHost, s));
   if (ndocs) HIPCHECK(hipMemcpyAsync(&max_fast, b->max_hot.p + 1, sizeof max_fast, hipMemcpyDeviceToHost, s));
+  if (ndocs) HIPCHECK(hipMemcpyAsync(&saved, b->max_hot.p + 2, sizeof saved, hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
   HIPCHECK(hipGetLastError());
+  // a batch reserves the whole plan of every compact document as overflow, so none of them can
+  // run out of room if the fast kernel gives up on all of them (the pipe reserves a fraction)
+  b->ws_plan = total;
+  total += saved;
   b->ws_need = total;
   // dynamic LDS of the document workgroups: the largest hot working set, capped by the budget
   uint64_t lds = (max_hot + 15) & ~(uint64_t)15;
   if (lds > lds_budget(b->any_diff)) lds = lds_budget(b->any_diff);
   b->lds_bytes = (uint32_t)lds;
   b->max_hot_v = max_hot;
-  // k_doc_fast (am_doc_fast.h) for the documents in its envelope; AM_FAST=0 turns it off
-  const char* fe = std::getenv("AM_FAST");
-  const bool fast_on = !(fe && fe[0] == '0');
   b->fast_lds = fast_on ? (uint32_t)((max_fast + 15) & ~(uint64_t)15) : 0u;
   b->fast_only = false;
   if (!b->ws.ensure(total + 16)) return false;
@@ -723,6 +737,7 @@ extern "C" int am_batch_fast_flags(am_batch* b, uint8_t* flags) {
 }
 
 extern "C" uint64_t am_batch_workspace_bytes(am_batch* b) { return b->ws_need; }
+extern "C" uint64_t am_batch_workspace_plan(am_batch* b) { return b->ws_plan; }
 
 // pako.inflateRaw over n independent buffers on the GPU (the kernels of the batch stage). outs[i]
 // (malloc'd, am_free) / out_lens[i]; ok[i] = 0 when buffer i is not a valid raw DEFLATE stream.
@@ -962,7 +977,7 @@ extern "C" am_pipe* am_pipe_create(am_engine* eng, const am_pipe_caps* caps, am_
         b.arena.ensure(c.arena_bytes + 64) && b.chunks.ensure(c.chunks) && b.docs.ensure(c.docs) && b.known.ensure(1) &&
         b.info.ensure(c.chunks) && b.hdr.ensure(c.chunks) && b.bounds.ensure(c.docs) && b.ws_bytes.ensure(c.docs) &&
         b.ws_off.ensure(c.docs) && b.scan_tmp.ensure(am_scan_tmp_elems(c.docs)) && b.ws_total.ensure(1) &&
-        b.max_hot.ensure(2) && b.fast_done.ensure(c.docs) && b.rest.ensure(c.docs + 1) && b.results.ensure(c.docs) &&
+        b.max_hot.ensure(4) && b.fast_done.ensure(c.docs) && b.rest.ensure(c.docs + 1) && b.results.ensure(c.docs) &&
         b.chg_state.ensure(c.chunks) &&
         b.ws.ensure(c.ws_bytes + 16) && sl->olen.ensure(c.docs) && sl->ooff.ensure(c.docs) && sl->plen.ensure(c.docs) &&
         sl->poff.ensure(c.docs) && sl->tmp.ensure(am_scan_tmp_elems(c.docs)) && sl->totals.ensure(2) &&
@@ -975,6 +990,7 @@ extern "C" am_pipe* am_pipe_create(am_engine* eng, const am_pipe_caps* caps, am_
     if (hsa_signal_create(0, 0, nullptr, &sl->home) != HSA_STATUS_SUCCESS) sl->home.handle = 0;
     if (hsa_signal_create(0, 0, nullptr, &sl->insig) != HSA_STATUS_SUCCESS) sl->insig.handle = 0;
     b.lds_bytes = lds_budget(false);   // k_doc takes what k_doc_fast leaves, in either mode (set per batch)
+    b.compact = c.fast_lds != 0 && ws_compact_on();  // what the fast kernel gives up on takes the overflow
     b.max_hot_v = ~0ull;
     b.fast_lds = c.fast_lds;
   }

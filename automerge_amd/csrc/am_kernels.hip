@@ -835,9 +835,10 @@ void am_fast_slices_host(const DocBounds* db, const am_doc_desc* dd, uint32_t n,
 __global__ void __launch_bounds__(256) k_bounds(const uint8_t* __restrict__ arena, const am_doc_desc* __restrict__ docs, uint32_t ndocs,
                                                 const am_chunk_desc* __restrict__ chunks, const ChunkInfo* __restrict__ info,
                                                 DocBounds* __restrict__ bounds, uint64_t* __restrict__ ws_bytes,
-                                                uint64_t* __restrict__ max_hot) {
+                                                uint64_t* __restrict__ max_hot, bool compact) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t h = 0, f = 0;  // k_doc hot set; k_doc_fast LDS slice (0: outside its envelope)
+  uint64_t saved = 0;     // the whole plan of a document given the compact one (its overflow reserve)
   if (d < ndocs) {
   am_doc_desc dd = docs[d];
   DocBounds b;
@@ -883,11 +884,17 @@ __global__ void __launch_bounds__(256) k_bounds(const uint8_t* __restrict__ aren
   b.U = ((dd.flags & AM_DOC_FIX_UTF8) ? 1u : 0u) | ((dd.flags & AM_DOC_PATCH_ROOM) ? 2u : 0u);
   b.UC = (uint32_t)UC; b.UV = (uint32_t)UV;
   WsLayout L = ws_layout(b);
-  bounds[d] = b;
-  ws_bytes[d] = L.total;
   // a scattered document needs the global-mode launch: report a hot set above any LDS budget
   h = doc_scattered(b) ? (1ull << 40) : L.hot_total;
   if (fast_eligible(b, dd)) f = fast_layout(b, dd.known_count).total;
+  uint64_t total = L.total;
+  if (compact && f) {  // k_doc_fast's document: its compact plan (k_rest re-plans it if the kernel gives up)
+    b.U |= 4u;
+    total = ws_layout(b).total;
+    saved = L.total;
+  }
+  bounds[d] = b;
+  ws_bytes[d] = total;
   }
   // max_hot[0]: largest k_doc hot working set; max_hot[1]: largest k_doc_fast LDS slice -- one
   // atomic per wave
@@ -896,10 +903,12 @@ __global__ void __launch_bounds__(256) k_bounds(const uint8_t* __restrict__ aren
     const uint64_t h2 = __shfl_xor(h, o, 64), f2 = __shfl_xor(f, o, 64);
     h = h2 > h ? h2 : h;
     f = f2 > f ? f2 : f;
+    saved += __shfl_xor(saved, o, 64);
   }
   if ((threadIdx.x & 63) == 0) {
     if (h) atomicMax(reinterpret_cast<unsigned long long*>(max_hot), (unsigned long long)h);
     if (f) atomicMax(reinterpret_cast<unsigned long long*>(max_hot + 1), (unsigned long long)f);
+    if (saved) atomicAdd(reinterpret_cast<unsigned long long*>(max_hot + 2), (unsigned long long)saved);
   }
 }
 
@@ -1017,18 +1026,30 @@ void am_launch_history_compact(const HistResult* res, const HistDesc* hd, uint32
 }
 void am_launch_bounds(const BatchDev& b, hipStream_t s) {
   if (!b.ndocs) return;
-  (void)hipMemsetAsync(b.max_hot, 0, 2 * sizeof(uint64_t), s);
+  (void)hipMemsetAsync(b.max_hot, 0, 4 * sizeof(uint64_t), s);
   hipLaunchKernelGGL(k_bounds, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, b.arena, b.docs, b.ndocs, b.chunks, b.info, b.bounds,
-                     b.ws_bytes, b.max_hot);
+                     b.ws_bytes, b.max_hot, b.compact);
   uint32_t nblk = (b.ndocs + SCAN_T - 1) / SCAN_T;
   hipLaunchKernelGGL(k_scan_blocks, dim3(nblk), dim3(SCAN_T), 0, s, b.ws_bytes, b.ws_off, b.scan_tmp, b.ndocs);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, b.scan_tmp, nblk, b.ws_total);
   hipLaunchKernelGGL(k_scan_add, dim3(nblk), dim3(SCAN_T), 0, s, b.ws_off, b.scan_tmp, b.ndocs);
 }
-// the documents k_doc_fast left, as a list for k_doc's loop (rest[0] = count, zeroed beforehand)
-__global__ void __launch_bounds__(256) k_rest(const uint8_t* __restrict__ fast_done, uint32_t ndocs, uint32_t* __restrict__ rest) {
+// the documents k_doc_fast left, as a list for k_doc's loop (rest[0] = count, zeroed beforehand).
+// One that had the compact plan gets the whole plan, bump-allocated in the overflow region after
+// the scanned workspaces ([*ws_total, ws_cap)); past its end k_doc reports AM_U_CAPACITY.
+__global__ void __launch_bounds__(256) k_rest(const uint8_t* __restrict__ fast_done, uint32_t ndocs, uint32_t* __restrict__ rest,
+                                              DocBounds* __restrict__ bounds, uint64_t* __restrict__ ws_off,
+                                              const uint64_t* __restrict__ ws_total, uint64_t* __restrict__ ovf) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x, l = threadIdx.x & 63;
   const bool need = d < ndocs && !fast_done[d];
+  if (need && (bounds[d].U & 4u)) {
+    DocBounds b = bounds[d];
+    b.U &= ~4u;
+    const uint64_t t = ws_layout(b).total;
+    const uint64_t o = atomicAdd(reinterpret_cast<unsigned long long*>(ovf), (unsigned long long)t);
+    bounds[d] = b;
+    ws_off[d] = *ws_total + o;
+  }
   const uint64_t m = __ballot(need);
   uint32_t base = 0;
   if (l == 0 && m) base = atomicAdd(rest, (uint32_t)__popcll(m));
@@ -1070,7 +1091,9 @@ void am_launch_doc(const BatchDev& b, hipStream_t s) {
     uint32_t grid = b.ndocs;
     if (rest) {
       (void)hipMemsetAsync(b.rest, 0, sizeof(uint32_t), s);
-      hipLaunchKernelGGL(k_rest, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, fd, b.ndocs, b.rest);
+      (void)hipMemsetAsync(b.max_hot + 3, 0, sizeof(uint64_t), s);
+      hipLaunchKernelGGL(k_rest, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, fd, b.ndocs, b.rest, b.bounds, b.ws_off,
+                         b.ws_total, b.max_hot + 3);
       grid = b.ndocs < K_DOC_LOOP_WG ? b.ndocs : K_DOC_LOOP_WG;
     }
     hipLaunchKernelGGL(lds_mode::k_doc, dim3(grid), dim3(DOC_T), b.lds_bytes, s, b.arena, b.chunks, b.docs, b.known,

@@ -22,7 +22,8 @@ struct BatchDev {
   uint64_t* ws_off;        // per doc (exclusive scan)
   uint64_t* scan_tmp;      // block sums
   uint64_t* ws_total;      // 1 value
-  uint64_t* max_hot;       // 1 value: largest hot working set of the batch
+  uint64_t* max_hot;       // 4 values: largest hot set, largest fast slice, the whole plans of the compact documents,
+                           // the overflow region's bump counter (k_rest)
   uint32_t lds_bytes;      // dynamic LDS per document workgroup
   uint64_t max_hot_host;   // host copy of *max_hot
   uint32_t fast_lds;       // k_doc_fast LDS slice per document (0: no document in its envelope / disabled)
@@ -30,6 +31,7 @@ struct BatchDev {
   uint32_t* rest;          // [0] = count, [1..]: the documents k_doc_fast left (k_rest)
   bool fast_only;          // every document is in the fast envelope: skip the k_doc launches
   bool any_diff;           // some document asks for its applyChanges patch (k_doc_fast<true>)
+  bool compact;            // k_bounds gives k_doc_fast's documents the compact plan (ws_layout, U bit 2)
   uint8_t* ws;
   uint64_t ws_cap;
   am_doc_result* results;

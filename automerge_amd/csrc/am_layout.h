@@ -36,7 +36,8 @@ struct DocBounds {
   uint32_t ND;  // sum of change deps (plan)
   uint32_t P;   // 1: write the getPatch() log (AM_DOC_WANT_PATCH); 2: the applyChanges patch (AM_DOC_WANT_DIFF)
   uint32_t U;   // bit0: invalid UTF-8 keys / messages are replaced (AM_DOC_FIX_UTF8): room for 3 bytes per input
-                // byte; bit1: 8x applyChanges-patch pools (AM_DOC_PATCH_ROOM)
+                // byte; bit1: 8x applyChanges-patch pools (AM_DOC_PATCH_ROOM); bit2: k_doc_fast's compact
+                // plan (ws_layout below; k_rest re-plans a document the fast kernel gives up on)
   uint32_t UC;  // instances of unknown op columns over the document's chunks (new.js:1387-1425)
   uint32_t UV;  // bound on their values
   uint64_t S;   // key + message string bytes over all rows
@@ -92,6 +93,21 @@ AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   WsLayout L;
   uint64_t o = 0;
   auto take = [&](uint64_t bytes) { uint64_t at = o; o += (bytes + 15) & ~(uint64_t)15; return at; };
+  if (b.U & 4) {
+    // k_doc_fast's plan: the heads, the output image and the patch's wire form -- all the fast
+    // kernel writes to global memory. An image or a patch larger than these caps makes the fast
+    // kernel give up on the document (as any other miss does); k_rest then gives it the whole plan
+    // below in the overflow region after the batch's workspaces.
+    L = WsLayout{};
+    const uint64_t span = b.span_hi - b.span_lo;
+    L.heads = take((uint64_t)b.H * 32);
+    L.out_cap = 64 + 40 * (uint64_t)b.A + 42 * (uint64_t)b.H + 300 + span + 10 * (uint64_t)b.R;
+    L.out = take(L.out_cap);
+    L.pwire_cap = b.P ? 48 + 512 + 2 * b.B + 32 * ((uint64_t)b.R + b.A + b.C + b.H) : 0;
+    L.pwire = b.P ? take(L.pwire_cap) : 0;
+    L.total = o;
+    return L;
+  }
   const uint64_t R = b.R, E = b.E, C = b.C, D = b.D, N = b.N;
   const uint64_t PR = am_pow2(b.R ? b.R : 1), PE = am_pow2(b.E ? b.E : 1);
   L.rows = take(R * AM_SZ_ROW);

@@ -237,7 +237,9 @@ def main():
     # capacities from a representative batch (the largest one), staged the ordinary way
     probe = Batch(device=local)
     probe.stage(*max(parts, key=lambda p: len(p[0])))
-    ws_need = int(probe.workspace_bytes())
+    # the scanned plans (k_doc_fast's documents: compact ones), plus 1/8 + 64 MB of overflow room
+    # for documents the fast kernel gives up on (each then takes k_doc's whole plan there)
+    ws_need = int(probe.workspace_plan())
     kinfo = probe.kernel_info()
     del probe
     arena_cap = max(len(p[0]) for p in parts)
@@ -245,7 +247,8 @@ def main():
     ccap = max(len(p[1]) for p in parts)
     out_cap = ncap * 1024 + (1 << 20)
     patch_cap = ncap * 1024 + (1 << 20) if not args.no_patch else (1 << 20)
-    pl = pipe.Pipeline(arena_cap, ccap, ncap, ws_need + ws_need // 8 + (1 << 20), out_cap, patch_cap,
+    ws_slot = ws_need + ws_need // 8 + (64 << 20)
+    pl = pipe.Pipeline(arena_cap, ccap, ncap, ws_slot, out_cap, patch_cap,
                        kinfo["k_doc_fast_lds_per_doc"], slots=args.slots, device=local)
     nb = len(parts)
     in_b = int(arena.nbytes)
@@ -384,7 +387,7 @@ def main():
     summ_all = np.concatenate(summ_b)
     statuses = summ_all["status"]
     alg_launch = (in_b + out_bytes + patch_bytes) / nb
-    workspace = int(ws_need)
+    workspace = int(ws_slot)  # what one pipeline slot holds (plans + overflow room)
     # per-shard digest: container checksum, length and status of every merged document
     chk = []
     for s_, po in zip(summ_b, outs_b):
@@ -470,7 +473,8 @@ def main():
                      "traffic": tr["traffic_bytes"] if tr else None, "alg_bytes_per_launch": alg_launch, "avg_ms": t_doc,
                      "limiter": "VALU issue of the one-wave-per-document merge (DESIGN.md 4); not HBM"},
         "errors": tot[2], "verified_docs": checked, "input_bytes_rank0": in_b, "output_bytes_rank0": out_bytes,
-        "patch_bytes_rank0": patch_bytes, "workspace_bytes_per_batch": workspace, "gen_s": t_gen,
+        "patch_bytes_rank0": patch_bytes, "workspace_bytes_per_batch": workspace,
+        "workspace_bytes_per_doc": workspace / max(1, ncap), "gen_s": t_gen,
         "docs_per_sec": tot[0] / (elapsed / args.steps), "digest": tot[4],
         "cpu_baseline": cpu, "cpu_reference_node": cpu_reference(),
     }

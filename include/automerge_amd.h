@@ -230,8 +230,12 @@ int64_t am_batch_ws_canary(am_batch *b, uint64_t n);
 int am_batch_doc_layout(am_batch *b, uint32_t doc, void *bounds_out, uint64_t *lay_out, uint32_t cap);
 /* Diagnostics: the raw 48-byte header of document doc's patch-log slot. */
 int am_batch_doc_patch_raw(am_batch *b, uint32_t doc, uint8_t *dst48);
-/* Device pointer + size of the staged arena / merged outputs (for bench byte accounting). */
+/* Device workspace the staged batch holds (for bench byte accounting): the scanned per-document
+ * plans plus the overflow reserve (the whole plan of every document given k_doc_fast's compact plan,
+ * in case the fast kernel gives up on it). */
 uint64_t am_batch_workspace_bytes(am_batch *b);
+/* The scanned per-document plans alone: what a pipeline slot needs before its overflow headroom. */
+uint64_t am_batch_workspace_plan(am_batch *b);
 /* Launch shape of the staged batch's document kernels: out3[0] = k_doc dynamic LDS bytes,
  * out3[1] = k_doc_fast LDS slice per document (0: none in its envelope), out3[2] = largest k_doc
  * hot working set. Not part of the reference interface (bench/profiling only). */
@@ -249,8 +253,9 @@ int am_batch_fast_slices(am_batch *b, uint32_t *out);
  * documents and patch logs (documents staged with AM_DOC_WANT_DIFF) come back densely packed in
  * 16-byte slots, described by one am_doc_summary per document. Host buffers should come from
  * am_host_alloc (pinned) for the copies to be asynchronous.
- *   caps: per-batch capacities. ws_bytes: device workspace per batch (am_batch_workspace_bytes of a
- *   representative batch, with headroom); fast_lds: k_doc_fast LDS slice per document
+ *   caps: per-batch capacities. ws_bytes: device workspace per batch (am_batch_workspace_plan of a
+ *   representative batch, with headroom: the headroom past a batch's plans is the overflow region
+ *   where a document the fast kernel gives up on gets k_doc's whole plan); fast_lds: k_doc_fast LDS slice per document
  *   (am_batch_kernel_info out3[1]; 0 disables the small-document kernel). Documents that exceed a
  *   capacity report AM_U_CAPACITY in their summary and can be rerun through am_batch_*.
  * Change chunks must be uncompressed (type 1): DEFLATEd ones go through am_batch_stage. */

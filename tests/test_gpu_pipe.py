@@ -88,8 +88,10 @@ def test_pipeline_capacities():
     tight.drain(1)
     st = sm["status"]
     assert (st == 0).sum() > 50 and (st == 106).sum() > 50 and set(np.unique(st)) <= {0, 106}
-    # too little workspace: the documents beyond it report AM_U_CAPACITY, the others merge
-    short = pipe.Pipeline(len(a), len(c), len(d), ws // 2, 1 << 20, 1 << 20, kinfo["k_doc_fast_lds_per_doc"], slots=2)
+    # too little workspace (half the scanned plans, no overflow room): the documents beyond it report
+    # AM_U_CAPACITY, the others merge
+    short = pipe.Pipeline(len(a), len(c), len(d), int(ref.workspace_plan()) // 2, 1 << 20, 1 << 20,
+                          kinfo["k_doc_fast_lds_per_doc"], slots=2)
     short.submit(pa.arr, pc.arr, pd.arr, sm, po.u8, pp.u8)
     short.drain(1)
     st = sm["status"]
