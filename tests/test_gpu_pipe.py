@@ -140,3 +140,42 @@ def test_packed_descriptors_that_lie():
     st = sm["status"]
     assert (st[:100] == 0).all()
     assert (st[100:] != 0).all()
+
+
+def test_pipeline_fast_kernel_fallback_uses_the_overflow():
+    """Documents k_doc_fast gives up on (here: a change whose checksum is wrong) lose their compact
+    workspace plan: k_rest re-plans them in the overflow room past the batch's plans, where k_doc
+    reports their error exactly as the batch path does. Without overflow room they report
+    AM_U_CAPACITY; every other document merges either way."""
+    from automerge_amd import pipe
+    from automerge_amd.batch import WANT_DIFF, Batch
+    (a, c, d), _ = _parts("c4", 0, 300, 300, WANT_DIFF)
+    a = a.copy()
+    bad = [5, 77, 150, 299]
+    for i in bad:  # the last byte of the document's second change: its SHA-256 no longer matches
+        ch = c[int(d[i]["chg_begin"]) + 1]
+        a[int(ch["off"]) + int(ch["len"]) - 1] ^= 0x5A
+    ref = Batch()
+    ref.stage(a, c, d)
+    ref.run()
+    ref.sync()
+    rr = ref.results()
+    assert all(int(rr[i]["status"]) != 0 for i in bad) and (rr["status"] != 0).sum() == len(bad)
+    kinfo = ref.kernel_info()
+    plan = int(ref.workspace_plan())
+    assert plan < int(ref.workspace_bytes())  # the compact plans leave room for the overflow reserve
+    pa, pc, pd = pipe.pinned_copy(a), pipe.pinned_copy(c), pipe.pinned_copy(d)
+    for room, want_bad in ((plan // 8 + (8 << 20), None), (0, 106)):
+        pl = pipe.Pipeline(len(a), len(c), len(d), plan + room, 1 << 20, 4 << 20, kinfo["k_doc_fast_lds_per_doc"], slots=2)
+        s = pipe.Pinned(len(d) * pipe.SUMMARY_DT.itemsize)
+        po, pp = pipe.Pinned(1 << 20), pipe.Pinned(4 << 20)
+        sm = s.view(pipe.SUMMARY_DT, len(d))
+        pl.submit(pa.arr, pc.arr, pd.arr, sm, po.u8, pp.u8)
+        pl.drain(1)
+        for j in range(len(d)):
+            if j in bad:
+                assert int(sm[j]["status"]) == (int(rr[j]["status"]) if want_bad is None else want_bad), j
+                continue
+            assert int(sm[j]["status"]) == 0, j
+            o = bytes(po.u8[int(sm[j]["out_off"]):int(sm[j]["out_off"]) + int(sm[j]["out_len"])])
+            assert o == ref.doc_output(j, rr[j]), j
