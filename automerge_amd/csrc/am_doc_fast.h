@@ -1465,9 +1465,10 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
   const am_doc_desc dd = docs[doc];
   const DocBounds b = bounds[doc];
   if (!fast_eligible(b, dd)) return;
+  if (!(b.U & 4u)) return;  // not given the compact plan (AM_WS_COMPACT=0): k_doc merges it
   const FastLayout F = fast_layout(b, dd.known_count);
   if (F.total > lds_per_doc || F.total <= lds_floor) return;  // another launch's slice class (or k_doc's)
-  const WsLayout L = ws_layout(b);
+  const WsFast L = ws_fast(b);
   const uint64_t wso = ws_off[doc];
   if (wso + L.total > ws_cap) return;  // capacity error: reported by k_doc
   uint8_t* const wsg = ws_base + wso;
@@ -2382,21 +2383,22 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
     const bool t31 = __all(!act || v_time == AM_NULL64 || (v_time >= 0 && v_time <= 0x7fffffff));
     const bool seg = NC <= 16 && F.ob_cap >= cur + 8 * kRowCap + 64;
     const uint32_t tbase = F.ob_cap - 8 * kRowCap;
-    uint32_t seglen[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // rows: U {actor, depsNum, extraLen}, D {seq, maxOp, time}
+    // encoded lengths of the staged rows U {actor, depsNum, extraLen} (lu) and D {seq, maxOp, time}
+    // (ld), at lanes 0 / 16 / 32 of each (read back by readlane: an indexed local array of them was
+    // private memory, 40 B per lane of scratch traffic)
+    uint32_t lu = 0, ld = 0;
     if (seg) {
       const uint32_t g = l >> 4, p = l & 15;
       const int32_t a = __shfl((int32_t)v_act, (int)p, 64), nd = __shfl((int32_t)v_nd, (int)p, 64);
       const int32_t xl = __shfl((int32_t)v_xlen, (int)p, 64);
       const bool xn = __shfl((int32_t)(v_xlen == AM_NULL64), (int)p, 64) != 0;
-      const uint32_t lu = enc32r<EK_U>(g < 3 ? NC : 0u, g == 0 ? a : g == 1 ? nd : xl, g == 2 && xn, OB + tbase + g * kRowCap,
+      lu = enc32r<EK_U>(g < 3 ? NC : 0u, g == 0 ? a : g == 1 ? nd : xl, g == 2 && xn, OB + tbase + g * kRowCap,
                                        kRowCap, bad);
       const int32_t sq = __shfl((int32_t)v_seq, (int)p, 64), mx = __shfl((int32_t)v_max, (int)p, 64);
       const int32_t tm = __shfl((int32_t)v_time, (int)p, 64);
       const bool tn = __shfl((int32_t)(v_time == AM_NULL64), (int)p, 64) != 0;
-      const uint32_t ld = enc32r<EK_D>(g < (t31 ? 3u : 2u) ? NC : 0u, g == 0 ? sq : g == 1 ? mx : tm, g == 2 && tn,
+      ld = enc32r<EK_D>(g < (t31 ? 3u : 2u) ? NC : 0u, g == 0 ? sq : g == 1 ? mx : tm, g == 2 && tn,
                                        OB + tbase + (4 + g) * kRowCap, kRowCap, bad);
-#pragma unroll
-      for (int r = 0; r < 4; r++) { seglen[r] = wave::bcast(lu, 16 * r); seglen[4 + r] = wave::bcast(ld, 16 * r); }
     }
     const uint32_t cap_end = seg ? tbase : F.ob_cap;
 #pragma unroll 1
@@ -2405,7 +2407,7 @@ __global__ void __launch_bounds__(64 * FD_DOCS_PER_WG) FD_WAVES_ATTR
       const int srow = !seg ? -1 : col == DC_ACTOR ? 0 : col == DC_DEPS_NUM ? 1 : col == DC_EXTRA_LEN ? 2 : col == DC_SEQ ? 4
                                  : col == DC_MAXOP ? 5 : (col == DC_TIME && t31) ? 6 : -1;
       if (srow >= 0) {
-        len = seglen[srow];
+        len = srow < 4 ? wave::bcast(lu, 16 * srow) : wave::bcast(ld, 16 * (srow - 4));
         if (len == ~0u || cur + len > cap_end) { bad = true; break; }
         const uint8_t* src = OB + tbase + srow * kRowCap;
         for (uint32_t q = l; q < len; q += 64) OB[cur + q] = src[q];

@@ -89,23 +89,38 @@ AM_HD inline uint32_t am_pow2(uint32_t n) {
 #define AM_SZ_ACTORREF 16
 #define AM_SZ_CHGHDR 224
 
+// k_doc_fast's plan (DocBounds.U bit 2): the heads, the output image and the patch's wire form --
+// all the fast kernel writes to global memory. An image or a patch larger than these caps makes the
+// fast kernel give up on the document (as any other miss does); k_rest then gives it the whole plan
+// (ws_layout below) in the overflow region after the batch's workspaces. Its own small struct: the
+// fast kernel reads only these, and the whole WsLayout there costs private (scratch) memory.
+struct WsFast {
+  uint64_t heads, out, out_cap, pwire, pwire_cap, total;
+};
+AM_HD inline WsFast ws_fast(const DocBounds& b) {
+  WsFast F;
+  const uint64_t span = b.span_hi - b.span_lo;
+  auto r16 = [](uint64_t v) { return (v + 15) & ~(uint64_t)15; };
+  F.heads = 0;
+  F.out_cap = 64 + 40 * (uint64_t)b.A + 42 * (uint64_t)b.H + 300 + span + 10 * (uint64_t)b.R;
+  F.out = r16((uint64_t)b.H * 32);
+  F.pwire_cap = b.P ? 48 + 512 + 2 * b.B + 32 * ((uint64_t)b.R + b.A + b.C + b.H) : 0;
+  F.pwire = F.out + r16(F.out_cap);
+  F.total = F.pwire + (b.P ? r16(F.pwire_cap) : 0);
+  return F;
+}
+
 AM_HD inline WsLayout ws_layout(const DocBounds& b) {
   WsLayout L;
   uint64_t o = 0;
   auto take = [&](uint64_t bytes) { uint64_t at = o; o += (bytes + 15) & ~(uint64_t)15; return at; };
   if (b.U & 4) {
-    // k_doc_fast's plan: the heads, the output image and the patch's wire form -- all the fast
-    // kernel writes to global memory. An image or a patch larger than these caps makes the fast
-    // kernel give up on the document (as any other miss does); k_rest then gives it the whole plan
-    // below in the overflow region after the batch's workspaces.
+    const WsFast F = ws_fast(b);
     L = WsLayout{};
-    const uint64_t span = b.span_hi - b.span_lo;
-    L.heads = take((uint64_t)b.H * 32);
-    L.out_cap = 64 + 40 * (uint64_t)b.A + 42 * (uint64_t)b.H + 300 + span + 10 * (uint64_t)b.R;
-    L.out = take(L.out_cap);
-    L.pwire_cap = b.P ? 48 + 512 + 2 * b.B + 32 * ((uint64_t)b.R + b.A + b.C + b.H) : 0;
-    L.pwire = b.P ? take(L.pwire_cap) : 0;
-    L.total = o;
+    L.heads = F.heads;
+    L.out = F.out; L.out_cap = F.out_cap;
+    L.pwire = b.P ? F.pwire : 0; L.pwire_cap = F.pwire_cap;
+    L.total = F.total;
     return L;
   }
   const uint64_t R = b.R, E = b.E, C = b.C, D = b.D, N = b.N;

@@ -7,6 +7,8 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r5final
 mkdir -p $O
 cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; exit 1; }
+echo "tests ok"
 timeout -k 10 400 python3 -u bench.py > $O/bench_a.json 2> $O/bench_a.err || { echo "bench failed"; exit 1; }
 echo "bench a ok"
 cd /tmp && export TMPDIR=/tmp
@@ -22,6 +24,8 @@ timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WA
   --output-format csv -d $O/sq -o sq -- python3 $R/bench.py --mode resident --steps 2 --warmup 1 --no-cpu-baseline --check 0 > $O/sq.log 2>&1 || { echo "sq pass failed"; exit 1; }
 echo "sq ok"
 cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; exit 1; }
+echo "tests ok"
 python3 tools/traffic.py $O profiles/traffic_k_doc.json > $O/traffic.log 2>&1 || { echo "traffic.py failed"; exit 1; }
 cp profiles/traffic_k_doc.json $O/traffic_k_doc.json
 timeout -k 10 400 python3 -u bench.py > $O/bench_b.json 2> $O/bench_b.err || { echo "bench b failed"; exit 1; }
