@@ -2134,14 +2134,14 @@ static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* le
   fill_known();
   OneResult res;
   std::vector<uint8_t> arena;
-  if (!run_one(d->eng, d->state.empty() ? nullptr : &d->state, false, staged, known, d->have_hash_graph, res, arena, e, pmode,
+  if (!run_one(d->eng, d->state.empty() ? nullptr : &d->state, true, staged, known, d->have_hash_graph, res, arena, e, pmode,
                0, meta)) {
     // a loaded document without its hash graph: compute it and run again (new.js:1826-1832)
     if (e.code != AM_U_HASH_GRAPH || d->have_hash_graph) { to_c(e, err); return 1; }
     if (am_doc_compute_hash_graph(d, err)) return 1;
     fill_known();
     e = Err{};
-    if (!run_one(d->eng, &d->state, false, staged, known, true, res, arena, e, pmode, 0, meta)) {
+    if (!run_one(d->eng, &d->state, true, staged, known, true, res, arena, e, pmode, 0, meta)) {
       to_c(e, err);
       return 1;
     }
@@ -2151,7 +2151,7 @@ static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* le
   if (track && res.patch.size() >= sizeof(PatchHdr2)) {
     PatchHdr2 ph;
     std::memcpy(&ph, res.patch.data(), sizeof ph);
-    if (ph.status == AM_U_CAPACITY && !run_one(d->eng, d->state.empty() ? nullptr : &d->state, false, staged, known,
+    if (ph.status == AM_U_CAPACITY && !run_one(d->eng, d->state.empty() ? nullptr : &d->state, true, staged, known,
                                                d->have_hash_graph, res, arena, e, 2, AM_DOC_PATCH_ROOM, meta)) {
       to_c(e, err);
       return 1;
@@ -2371,7 +2371,7 @@ extern "C" int am_doc_get_patch(am_doc* d, uint8_t** out, size_t* len, am_error*
     OneResult res;
     std::vector<uint8_t> arena;
     Err e;
-    if (!run_one(d->eng, &d->state, false, {}, {}, d->have_hash_graph, res, arena, e, true)) { to_c(e, err); return 1; }
+    if (!run_one(d->eng, &d->state, true, {}, {}, d->have_hash_graph, res, arena, e, true)) { to_c(e, err); return 1; }
     log.swap(res.patch);
   }
   Err pe;
@@ -2628,6 +2628,7 @@ static int am_doc_apply_changes_batch_impl(size_t n, am_doc* const* docs, const 
       am_doc* d = docs[calls[k].i];
       ManyJob& j = jobs[k];
       j.base = d->state.empty() ? nullptr : &d->state;
+      j.base_verified = true;  // the handle's state is the engine's own checksummed output
       j.chg = &calls[k].orig;
       j.known = &calls[k].known;
       j.have_graph = d->have_hash_graph;
@@ -2738,6 +2739,7 @@ static int am_doc_get_patch_batch_impl(size_t n, am_doc* const* docs, uint8_t** 
     if (docs[i]->state.empty() || docs[i]->eng != eng) { single.push_back(i); continue; }
     ManyJob j;
     j.base = &docs[i]->state;
+    j.base_verified = true;
     j.have_graph = docs[i]->have_hash_graph;
     j.patch_mode = 1;
     jobs.push_back(j);
