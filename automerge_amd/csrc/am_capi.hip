@@ -338,6 +338,7 @@ struct am_batch {
   uint32_t nchunks = 0, ndocs = 0;
   uint64_t ws_need = 0;       // workspace held: the scanned plans + the overflow reserve
   uint64_t ws_plan = 0;       // the scanned plans alone (compact plans for k_doc_fast's documents)
+  bool fresh = false;         // staged and not run since: the sizing pass's chunk info and plans stand
   bool timed = false;
   uint32_t inflated = 0;      // change chunks inflated on the GPU by the last stage
   float inflate_ms = 0.f;     // their two inflate passes (HIP events)
@@ -544,6 +545,7 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   b->fast_lds = fast_on ? (uint32_t)((max_fast + 15) & ~(uint64_t)15) : 0u;
   b->fast_only = false;
   if (!b->ws.ensure(total + 16)) return false;
+  b->fresh = true;
   return true;
 }
 
@@ -588,11 +590,15 @@ extern "C" int am_batch_run(am_batch* b) {
                                       (unsigned long long)b->ws_need);
     return r == hipSuccess;
   };
+  // the first run after a stage reuses the sizing pass's k_chunks / k_bounds results (nothing has
+  // changed them; a run's k_rest re-plans bounds, so later runs redo both)
+  const bool fresh = b->fresh;
+  b->fresh = false;
   (void)hipEventRecord(e->ev[0], s);
-  am_launch_chunks(d, s);
+  if (!fresh) am_launch_chunks(d, s);
   if (!check("k_chunks")) return 1;
   (void)hipEventRecord(e->ev[1], s);
-  am_launch_bounds(d, s);
+  if (!fresh) am_launch_bounds(d, s);
   if (!check("k_bounds")) return 1;
   (void)hipEventRecord(e->ev[2], s);
   am_launch_doc(d, s);

@@ -1,5 +1,6 @@
 #!/bin/bash
 set -o pipefail
-O=gpurun_out/r5
-mkdir -p $O
-AM_LIB_PATH=$PWD/tools/dcheck/libam_dcheck.so AM_DEBUG_WS_CANARY=4194304 timeout -k 10 200 python -u tools/mid_canary.py --docs 2048,2055,2141,2147,2237,2344,0,1 --flags diff > $O/dcheck.log 2>&1 || exit 1
+bash tools/gpu_r5final.sh || exit 1
+timeout -k 10 600 python -u tools/bench_local.py --calls 10 > gpurun_out/r5final/local.json 2> gpurun_out/r5final/local.err || exit 1
+timeout -k 10 300 python -u tools/bench_mid.py --docs 8192 --steps 2 --check 8 --flags diff > gpurun_out/r5final/mid_diff.json 2> gpurun_out/r5final/mid_diff.err || exit 1
+echo "extra ok"
