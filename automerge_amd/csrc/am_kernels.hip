@@ -810,10 +810,12 @@ constexpr uint32_t kDocT = DOC_T_GLB;
 }  // namespace glb_mode
 // P8 of the global-mode documents (glb_mode::k_diff_one): one wave per document. Wide: all lanes run
 // the replay (scans and searches spread over them: few, large documents); else lane 0 alone (many
-// documents: the waves themselves fill the machine). The chain is dependent loads, so resident waves
-// decide its speed: registers capped for AM_DIFF_WAVES waves per SIMD
+// documents: the waves themselves fill the machine). The chain is dependent loads: resident waves hide
+// their latency, but a register cap that spills puts scratch round trips into the chain itself.
+// Measured (C5 pairs merged with their patch, 65,536 per batch / mid documents, 8,192): 8 waves per
+// SIMD 236 ms / 29.3M ops/s, 6: 234 / 29.7M, 4: 207 / 34.8M, 3: 232 / 30.8M, 2: 278 / 26.3M
 #ifndef AM_DIFF_WAVES
-#define AM_DIFF_WAVES 8
+#define AM_DIFF_WAVES 4
 #endif
 template <bool Wide>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(AM_DIFF_WAVES, 8))) k_diff(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,

@@ -2,5 +2,8 @@
 set -o pipefail
 O=gpurun_out/r5
 mkdir -p $O
-AM_DEBUG_WS_CANARY=64 AM_LIB_PATH=tools/dcheck/libam_dcheck.so timeout -k 10 300 python -u tools/patch_probe.py --runs 1 > $O/pprobe.log 2>&1
-AM_DEBUG_WS_CANARY=64 AM_LIB_PATH=tools/dcheck/libam_dcheck.so timeout -k 10 300 python -u tools/mid_probe.py --docs 2048 --flags diff > $O/mprobe.log 2>&1 || exit 1
+for lib in tools/clock/libam_w4.so tools/clock/libam_w3.so tools/clock/libam_w2.so; do
+  if [ $lib = default ]; then unset AM_LIB_PATH; else export AM_LIB_PATH=$lib; fi
+  timeout -k 10 300 python -u tools/c5_merge_probe.py >> $O/c5_waves.log 2>&1 || exit 1
+  timeout -k 10 300 python -u tools/bench_mid.py --docs 8192 --steps 2 --check 0 --flags diff >> $O/mid_waves.log 2>&1 || exit 1
+done
