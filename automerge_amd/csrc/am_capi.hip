@@ -2441,7 +2441,8 @@ static void hash_graphs(const std::vector<am_doc*>& ds, std::vector<Err>& E) {
     for (size_t k = g0; k < g1; k++) { ptr.push_back(ds[k]->state.data()); len.push_back(ds[k]->state.size()); }
     std::vector<am_history> h(g1 - g0);
     am_document_changes_batch(ds[g0]->eng, ptr.data(), len.data(), g1 - g0, h.data());
-    for (size_t k = g0; k < g1; k++) {
+    am_par_for(g1 - g0, [&](size_t kk) {  // each handle its own, on the host workers
+      const size_t k = g0 + kk;
       am_doc* d = ds[k];
       am_history& x = h[k - g0];
       if (x.err.code) {
@@ -2461,7 +2462,7 @@ static void hash_graphs(const std::vector<am_doc*>& ds, std::vector<Err>& E) {
       std::free(x.changes);
       std::free(x.offs);
       std::free(x.hashes32);
-    }
+    });
   }
 }
 

@@ -21,6 +21,7 @@
 #include "../../include/automerge_amd.h"
 #include "am_change_enc.h"
 #include "am_launch.h"
+#include "am_par.h"
 
 namespace {
 
@@ -359,16 +360,20 @@ extern "C" int am_document_changes_batch(am_engine* eng, const uint8_t* const* d
     }
     live.swap(again);
   }
-  int rc = 0;
-  for (size_t i = 0; i < n; i++) {
-    if (out[i].err.code) { rc = 1; continue; }
+  // per document on the host workers: each writes only its own out[i] (the change re-encode and
+  // DEFLATE of large changes are the bulk of it)
+  std::atomic<int> rc_any{0};
+  am_par_for(n, [&](size_t i) {
+    int rc = 0;
+    struct Flag { std::atomic<int>& a; int& v; ~Flag() { if (v) a.store(1, std::memory_order_relaxed); } } flag{rc_any, rc};
+    if (out[i].err.code) { rc = 1; return; }
     const DocRun& r = runs[i];
     if (r.r.status != HE_OK) {
       uint32_t code;
       const std::string m = history_message(r, src[i].first, src[i].second, code);
       set_err(&out[i].err, code ? code : AM_U_VALUE, m);
       rc = 1;
-      continue;
+      return;
     }
     std::vector<Bytes> chs;
     size_t total = 0;
@@ -376,7 +381,7 @@ extern "C" int am_document_changes_batch(am_engine* eng, const uint8_t* const* d
       chs.push_back(deflate_change(Bytes(r.bytes + c.off, r.bytes + c.off + c.len)));
       total += chs.back().size();
     }
-    if (out[i].err.code) { rc = 1; continue; }
+    if (out[i].err.code) { rc = 1; return; }
     out[i].changes = (uint8_t*)std::malloc(total ? total : 1);
     out[i].offs = (uint64_t*)std::malloc(sizeof(uint64_t) * (chs.size() + 1));
     out[i].hashes32 = (uint8_t*)std::malloc(32 * (chs.size() ? chs.size() : 1));
@@ -385,7 +390,7 @@ extern "C" int am_document_changes_batch(am_engine* eng, const uint8_t* const* d
       out[i].changes = nullptr; out[i].offs = nullptr; out[i].hashes32 = nullptr;
       set_err(&out[i].err, AM_U_CAPACITY, "automerge_amd: out of host memory");
       rc = 1;
-      continue;
+      return;
     }
     size_t o = 0;
     for (size_t k = 0; k < chs.size(); k++) {
@@ -396,8 +401,8 @@ extern "C" int am_document_changes_batch(am_engine* eng, const uint8_t* const* d
     }
     out[i].offs[chs.size()] = o;
     out[i].nchanges = chs.size();
-  }
-  return rc;
+  });
+  return rc_any.load();
 }
 
 extern "C" int am_document_changes(am_engine* eng, const uint8_t* doc, size_t len, uint8_t** out, uint64_t** offs, uint8_t** hashes32,
