@@ -477,23 +477,22 @@ static bool inflate_stage(am_batch* b, const uint8_t* arena, uint64_t arena_len,
   return true;
 }
 
-// LDS budget of one k_doc workgroup (AM_LDS_BUDGET; AM_LDS_BUDGET_KB overrides it, for A/B runs).
-// A batch that wants patches keeps 40 KB: a document between 40 and 64 KB of hot set then merges in
-// global mode and replays its applyChanges patch in k_diff at 8 waves per SIMD (C5 pairs, 65,536
-// per batch: 232 ms) instead of in LDS mode at 2 workgroups per CU (361 ms; 44 ms against 74 ms
-// without the patch)
 // compact workspace plans for k_doc_fast's documents (AM_WS_COMPACT=0: every document gets k_doc's)
 static bool ws_compact_on() {
   static const bool v = [] { const char* e = std::getenv("AM_WS_COMPACT"); return !(e && e[0] == '0'); }();
   return v;
 }
+// LDS budget of one k_doc workgroup (AM_LDS_BUDGET; AM_LDS_BUDGET_KB overrides it, for A/B runs).
+// The applyChanges patch of every document replays in k_diff, whichever mode merged it, so a batch
+// that wants patches takes the same budget (any_diff kept for A/B builds)
 static uint32_t lds_budget(bool any_diff) {
+  (void)any_diff;
   static const uint32_t v = [] {
     const char* e = std::getenv("AM_LDS_BUDGET_KB");
     const unsigned long k = e ? std::strtoul(e, nullptr, 10) : 0ul;
     return k >= 8 && k <= 160 ? (uint32_t)(k * 1024) : 0u;
   }();
-  return v ? v : any_diff ? 40u * 1024 : (uint32_t)AM_LDS_BUDGET;
+  return v ? v : (uint32_t)AM_LDS_BUDGET;
 }
 
 static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, const am_chunk_desc* chunks, uint32_t nchunks,

@@ -1245,9 +1245,9 @@ __device__ static void p8_run(const DiffSrc& src, const P8Args a, PatchOut* po_ 
   }
 }
 
-// k_diff (global mode): P8 of every global-mode document k_doc merged with AM_DOC_WANT_DIFF, one
-// wave per document (the wide replay: all 64 lanes, see am_diff.h), from the rows k_doc left in the
-// document's workspace and the counts it recorded at L.djob
+// k_diff: P8 of every document k_doc merged with AM_DOC_WANT_DIFF (either mode), one wave per
+// document, from the rows k_doc left in the document's workspace (an LDS-mode document's mirrored
+// hot set) and the counts it recorded at L.djob
 template <bool Wide>
 __device__ static void k_diff_one(uint32_t doc, const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
                                   const am_doc_desc* __restrict__ docs, const DocBounds* __restrict__ bounds,
@@ -1258,7 +1258,6 @@ __device__ static void k_diff_one(uint32_t doc, const uint8_t* __restrict__ aren
   const DocBounds b = bounds[doc];
   if (b.P != 2) return;
   const WsLayout L = ws_layout(b);
-  if (L.hot_total <= lds_bytes && !doc_scattered(b)) return;  // an LDS-mode document: replayed in k_doc
   if (results[doc].status) return;
   uint8_t* const wsg = ws_base + ws_off[doc];
   const uint32_t* job = reinterpret_cast<const uint32_t*>(wsg + L.djob);
@@ -2075,19 +2074,19 @@ __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restric
       patch_scan(src, po, w, pmax);
       wire_out(po, pmax, wsg + L.pwire, L.pwire_cap);
     }
-    // P8: the patch applyChanges returns (am_diff.h), after the merge. LDS-mode documents replay it
-    // here (the wide replay); a global-mode document leaves its counts for k_diff, a one-wave-per-document
-    // launch after this one (the replay is one lane's chain of dependent global loads: at one
-    // lane per 4-wave workgroup too few of them were in flight)
+    // P8: the patch applyChanges returns (am_diff.h), after the merge, in k_diff: a launch of one
+    // wave per document after this one (the replay is a chain of dependent loads; at one lane per
+    // k_doc workgroup -- LDS mode: two to four per CU -- too few of them are in flight). This
+    // workgroup leaves the counts at L.djob; an LDS-mode document first mirrors its hot set (the
+    // rows, entries, sort records, actors, change rows and staged input the replay reads) into its
+    // global workspace, where a global-mode document keeps it anyway.
     if (s.b.P == 2) {
       if constexpr (kHotLds) {
-        // the workgroup is one wave: every lane runs the wide replay over the LDS-resident rows
-        static_assert(!kHotLds || kDocT == 64, "the LDS-mode P8 replay is one wave");
-        DiffSrc src{rows, ents, sr, succ_cnt, outent, reinterpret_cast<const int32_t*>(wsg + L.etime),
-                    reinterpret_cast<const uint32_t*>(wsg + L.passend), s.npass, s.nb, s.nrows, NOUT, NSUCC,
-                    s.nb_act < s.nb ? 0u : s.nb, actors, s.nactors, chg, NC, A};
-        p8_run<true>(src, p8_args(wsg, L, s.b, dd, chunks, arena));
-      } else if (t == 0) {
+        const uint4* src = hp<const uint4>(s, 0);
+        uint4* dst = reinterpret_cast<uint4*>(wsg);
+        for (uint32_t q = t; q < (uint32_t)(L.hot_total / 16); q += T) dst[q] = src[q];
+      }
+      if (t == 0) {
         uint32_t* job = reinterpret_cast<uint32_t*>(wsg + L.djob);
         job[0] = s.npass; job[1] = s.nb; job[2] = s.nrows; job[3] = NOUT;
         job[4] = NSUCC; job[5] = s.nb_act < s.nb ? 0u : s.nb; job[6] = s.nactors; job[7] = NC;

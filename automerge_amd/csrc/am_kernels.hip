@@ -1100,9 +1100,10 @@ void am_launch_doc(const BatchDev& b, hipStream_t s) {
     }
     hipLaunchKernelGGL(lds_mode::k_doc, dim3(grid), dim3(DOC_T), b.lds_bytes, s, b.arena, b.chunks, b.docs, b.known,
                        b.info, b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd, rest);
-    if (b.max_hot_host > b.lds_bytes) {
+    if (b.max_hot_host > b.lds_bytes)
       hipLaunchKernelGGL(glb_mode::k_doc, dim3(b.ndocs), dim3(DOC_T_GLB), 0, s, b.arena, b.chunks, b.docs, b.known, b.info,
                          b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd, nullptr);
+    {
       if (b.any_diff) {
         // wide replay for batches of fewer documents than wave slots (AM_DIFF_MODE=wide|lane0 overrides)
         static const int mode = [] {
