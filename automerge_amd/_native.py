@@ -104,6 +104,7 @@ _sigs = {
     "am_batch_fast_flags": (C.c_int, [P, P]),
     "am_engine_stats": (C.c_int, [P, P]),
     "am_batch_ws_canary": (C.c_int64, [P, C.c_uint64]),
+    "am_pipe_ws_canary": (C.c_int64, [P]),
     "am_batch_doc_layout": (C.c_int, [P, C.c_uint32, P, P, C.c_uint32]),
     "am_batch_doc_patch_raw": (C.c_int, [P, C.c_uint32, P]),
     "am_doc_init": (P, [P]),

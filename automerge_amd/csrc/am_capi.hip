@@ -105,6 +105,7 @@ std::string message_for(uint32_t code, int64_t a0, int64_t a1, const std::string
     case AM_U_DEL_SHAPE: return "automerge_amd: unsupported: del operation without pred or with insert";
     case AM_U_VALUE: return "automerge_amd: unsupported value shape in the input columns";
     case AM_U_CAPACITY: return "automerge_amd: workspace capacity exceeded";
+    case AM_U_INC_VALUE: return "automerge_amd: unsupported: a non-integer counter increment in the patch";
     default: return fmt("automerge_amd: error %u", code);
   }
 }
@@ -274,6 +275,17 @@ std::vector<uint8_t> make_chunk(const uint8_t checksum[4], uint8_t type, const s
 // =============================================================================================
 // engine / batch
 // =============================================================================================
+// Pinned host memory follows the caller's NUMA policy (hipHostMallocNumaUser): a rank that bound
+// itself to its GPU's NUMA node before its first GPU call (bench.py) gets its staging arenas on that
+// node, the host-link copies then stay on the socket the GPU hangs off. AM_PINNED_NUMA=0: the
+// runtime's default placement.
+static unsigned pinned_flags() {
+  static const unsigned f = [] {
+    const char* v = std::getenv("AM_PINNED_NUMA");
+    return (v && v[0] == '0') ? (unsigned)hipHostMallocDefault : (unsigned)hipHostMallocNumaUser;
+  }();
+  return f;
+}
 // pinned host memory (hipHostMalloc), grow-only (by at least half again)
 template <class T>
 struct PinBuf {
@@ -283,7 +295,7 @@ struct PinBuf {
     if (n <= cap && p) return true;
     const size_t want = std::max<size_t>(n ? n : 1, cap + cap / 2);
     if (p) { (void)hipHostFree(p); p = nullptr; cap = 0; }
-    if (hipHostMalloc(reinterpret_cast<void**>(&p), want * sizeof(T), hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc(reinterpret_cast<void**>(&p), want * sizeof(T), pinned_flags()) != hipSuccess) {
       p = nullptr;
       return false;
     }
@@ -338,6 +350,9 @@ struct am_batch {
   uint32_t nchunks = 0, ndocs = 0;
   uint64_t ws_need = 0;       // workspace held: the scanned plans + the overflow reserve
   uint64_t ws_plan = 0;       // the scanned plans alone (compact plans for k_doc_fast's documents)
+  uint32_t fast_cap = 0xffffffffu;  // compact plans only for fast slices up to this (a pipeline: its fast_lds)
+  uint64_t ws_limit = 0;      // diagnostics (a pipeline under AM_DEBUG_WS_CANARY): the kernels' workspace size,
+                              // canary bytes after it
   bool fresh = false;         // staged and not run since: the sizing pass's chunk info and plans stand
   bool timed = false;
   uint32_t inflated = 0;      // change chunks inflated on the GPU by the last stage
@@ -349,8 +364,8 @@ struct am_batch {
     b.arena = arena.p; b.chunks = chunks.p; b.docs = docs.p; b.known = known.p; b.info = info.p; b.hdr = hdr.p; b.bounds = bounds.p;
     b.ws_bytes = ws_bytes.p; b.ws_off = ws_off.p; b.scan_tmp = scan_tmp.p; b.ws_total = ws_total.p; b.max_hot = max_hot.p; b.lds_bytes = lds_bytes; b.max_hot_host = max_hot_v; b.ws = ws.p;
     b.fast_lds = fast_lds; b.fast_done = fast_done.p; b.fast_only = fast_only; b.any_diff = any_diff; b.rest = rest.p;
-    b.compact = compact;
-    b.ws_cap = ws.cap; b.results = results.p; b.chg_state = chg_state.p; b.nchunks = nchunks; b.ndocs = ndocs;
+    b.compact = compact; b.fast_cap = fast_cap;
+    b.ws_cap = ws_limit ? ws_limit : ws.cap; b.results = results.p; b.chg_state = chg_state.p; b.nchunks = nchunks; b.ndocs = ndocs;
     return b;
   }
 };
@@ -575,7 +590,8 @@ extern "C" int am_batch_run(am_batch* b) {
   }
   // AM_DEBUG_WS_CANARY=<bytes>: the workspace is filled with 0xA5 and followed by that many canary
   // bytes; am_batch_ws_canary reports the first one a kernel wrote
-  static const uint64_t canary = [] { const char* v = std::getenv("AM_DEBUG_WS_CANARY"); return v ? std::strtoull(v, nullptr, 10) : 0ull; }();
+  // (read per run: a test process turns it on for some batches only)
+  const uint64_t canary = [] { const char* v = std::getenv("AM_DEBUG_WS_CANARY"); return v ? std::strtoull(v, nullptr, 10) : 0ull; }();
   if (canary) {
     if (!b->ws.ensure(b->ws_need + canary + 16)) return 1;
     (void)hipMemsetAsync(b->ws.p, 0xA5, b->ws_need + canary, s);
@@ -877,7 +893,7 @@ extern "C" int am_batch_fast_slices(am_batch* b, uint32_t* out) {
 // =============================================================================================
 extern "C" void* am_host_alloc(size_t n) {
   void* p = nullptr;
-  if (hipHostMalloc(&p, n ? n : 1, hipHostMallocDefault) != hipSuccess) return nullptr;
+  if (hipHostMalloc(&p, n ? n : 1, pinned_flags()) != hipSuccess) return nullptr;
   return p;
 }
 extern "C" void am_host_free(void* p) {
@@ -926,6 +942,7 @@ struct am_pipe {
   PipeSlot* pending = nullptr;                 // inputs queued, compute chain not yet (pipe_submit)
   PipeSlot* launched = nullptr;                // the slot whose chain was queued last
   hsa_agent_t gpu{}, host{};
+  uint64_t canary = 0;                         // AM_DEBUG_WS_CANARY bytes after every slot's workspace
 };
 
 static bool sdma_wait(hsa_signal_t sig);
@@ -970,6 +987,7 @@ extern "C" am_pipe* am_pipe_create(am_engine* eng, const am_pipe_caps* caps, am_
   am_pipe* p = new am_pipe();
   p->eng = eng;
   p->caps = *caps;
+  if (const char* v = std::getenv("AM_DEBUG_WS_CANARY")) p->canary = std::strtoull(v, nullptr, 10);
   for (hipStream_t* s : {&p->s_in, &p->s_c, &p->s_out})
     if (hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess) return fail(p, "automerge_amd: cannot create a HIP stream");
   const am_pipe_caps& c = *caps;
@@ -998,9 +1016,28 @@ extern "C" am_pipe* am_pipe_create(am_engine* eng, const am_pipe_caps* caps, am_
     b.compact = c.fast_lds != 0 && ws_compact_on();  // what the fast kernel gives up on takes the overflow
     b.max_hot_v = ~0ull;
     b.fast_lds = c.fast_lds;
+    b.fast_cap = c.fast_lds;  // a slice above the pipe's fixed one keeps k_doc's whole plan in the scan
+    if (p->canary) {  // AM_DEBUG_WS_CANARY: every slot's workspace is followed by canary bytes
+      if (!b.ws.ensure(c.ws_bytes + 16 + p->canary) || hipMemset(b.ws.p, 0xA5, b.ws.cap) != hipSuccess)
+        return fail(p, "automerge_amd: device allocation failed (workspace canary)");
+      b.ws_limit = c.ws_bytes + 16;
+    }
   }
   if (err) err->code = 0;
   return p;
+}
+
+// Diagnostics (a pipeline created under AM_DEBUG_WS_CANARY=<n>): offset past the workspace end of the
+// first canary byte a kernel changed in any slot, -1 when none (call after am_pipe_drain)
+extern "C" int64_t am_pipe_ws_canary(am_pipe* p) {
+  if (!p || !p->canary || !set_device(p->eng)) return -2;
+  std::vector<uint8_t> h(p->canary);
+  for (PipeSlot* sl : p->slots) {
+    if (hipMemcpy(h.data(), sl->b.ws.p + sl->b.ws_limit, p->canary, hipMemcpyDeviceToHost) != hipSuccess) return -2;
+    for (uint64_t i = 0; i < p->canary; i++)
+      if (h[i] != 0xA5) return (int64_t)i;
+  }
+  return -1;
 }
 
 // the D2H copies of a batch whose kernels have been enqueued: waits for its compute chain, then
@@ -2098,6 +2135,8 @@ static bool patch_log_error(const std::vector<uint8_t>& log, Err& e) {
     e.msg = fmt("Invalid length for floating point number: %lld", (long long)h.arg0);
   } else if (h.status == AM_E_UNKNOWN_COUNTER) {
     e.msg = fmt("increment operation %lld@%s for unknown counter", (long long)h.arg0, wire_actor(log, h.arg1).c_str());
+  } else if (h.status == AM_U_INC_VALUE) {
+    e.msg = am_message_for(AM_U_INC_VALUE, 0, 0, "");
   } else {
     e.msg = fmt("automerge_amd: the patch is not supported for this document (code %u)", h.status);
   }
@@ -2180,8 +2219,11 @@ static int apply_finish(am_doc* d, std::vector<std::vector<uint8_t>>& orig, bool
       // there too, am_diff.h) -- fails the call either way and leaves the handle unchanged. Only the
       // engine's own pool limit lets a patchless call commit: its objectMeta is then resynchronised
       // to documentPatch's of the new state (as after save + load), never left unusable.
-      if (patch || pe.code != AM_U_CAPACITY) { to_c(pe, err); return 1; }
-      lost = true;
+      if (patch || (pe.code != AM_U_CAPACITY && pe.code != AM_U_INC_VALUE)) { to_c(pe, err); return 1; }
+      // AM_U_INC_VALUE: a non-integer counter increment, which the reference adds as JS does
+      // (new.js:958); only the patch value depends on it, so a patchless call commits with the
+      // snapshots the replay left
+      lost = pe.code == AM_U_CAPACITY;
     }
     if (patch) patch->swap(res.patch);
   }

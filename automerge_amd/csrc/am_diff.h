@@ -940,8 +940,12 @@ struct Diff {
       DCs& c = w.cs[w.cm[q].state];
       const uint32_t t15 = (uint32_t)(tag & 15);
       int64_t iv;
-      if (tag < 16 || !(t15 == 3 || t15 == 4 || t15 == 8 || t15 == 9) || !s.value_int((uint32_t)row, t15 == 3, iv))
-        return fail(PATCH_U_VALUE);
+      if (tag < 16 || !(t15 == 3 || t15 == 4 || t15 == 8 || t15 == 9) || !s.value_int((uint32_t)row, t15 == 3, iv)) {
+        // JS adds it as it is (a float, or a string concatenation, new.js:958): the replay goes on --
+        // objectMeta does not depend on the value -- and the call reports PATCH_U_INC_VALUE at the end
+        inc_nonint = true;
+        iv = 0;
+      }
       c.value += iv;
       c.nleft--;  // delete counterState.succs[opId]
       if (c.nleft == 0) {
@@ -1597,6 +1601,7 @@ struct Diff {
   const uint8_t* meta_in = nullptr;  // the handle's snapshots, null: documentPatch's (load / init)
   uint32_t meta_len = 0;
   bool meta_mode = false;
+  bool inc_nonint = false;  // a non-integer counter increment was met (its patch value is unknown)
 
   AM_PHD bool run() {
     DCHKF(11, s.nrows() ? s.nrows() - 1 : 0);
@@ -1644,6 +1649,7 @@ struct Diff {
     if (!setup_patches()) return false;
     DPROF(4);
     const bool r = emit();
+    if (r && ok && inc_nonint) o.status = PATCH_U_INC_VALUE;
     DPROF(5);
 #if defined(AM_DIFF_CHECK) && defined(__HIP_DEVICE_COMPILE__)
     if (((s.nrows() > 1100 && s.nrows() < 1104) || s.nrows() > 20000) && (!Wide || wave::lane_id() == 0))

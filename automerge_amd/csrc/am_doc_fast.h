@@ -1055,7 +1055,9 @@ __device__ __forceinline__ bool fast_diff(const uint8_t* IN, uint8_t* PS, uint32
             const uint32_t a = P.act[r];
             const bool mk = (a & 1) == 0, visible = SCR[r] == 0;
             if (mk) { exists = true; snap |= 1ull << p; }
-            if (visible) { vis |= 1ull << p; has_child |= mk; }
+            // the snapshot keeps the visible 'set' and make ops only (new.js:919-926): a visible inc
+            // or link row of the key is a visible op but never a child value
+            if (visible) { if (a == 1 || mk) vis |= 1ull << p; has_child |= mk; }
             if (has_child || (exists && snap)) { snap = vis; exists = true; }
           }
           if (!exists) continue;

@@ -1233,7 +1233,7 @@ __device__ static void p8_run(const DiffSrc& src, const P8Args a, PatchOut* po_ 
   const uint64_t wl = patch_pack(po, 0, pw, a.pwire_cap);
   if (!wl) {
     wire_out(po, 0, pw, a.pwire_cap);
-  } else if (a.meta_mode && !po.status) {
+  } else if (a.meta_mode && (!po.status || po.status == PATCH_U_INC_VALUE)) {
     // the snapshots this call leaves, after the stream (PatchHdr2.meta_bytes)
     const uint64_t mb = diff_meta_pack(src, dw, pw + wl, a.pwire_cap - wl);
     if (!mb) {

@@ -837,7 +837,7 @@ void am_fast_slices_host(const DocBounds* db, const am_doc_desc* dd, uint32_t n,
 __global__ void __launch_bounds__(256) k_bounds(const uint8_t* __restrict__ arena, const am_doc_desc* __restrict__ docs, uint32_t ndocs,
                                                 const am_chunk_desc* __restrict__ chunks, const ChunkInfo* __restrict__ info,
                                                 DocBounds* __restrict__ bounds, uint64_t* __restrict__ ws_bytes,
-                                                uint64_t* __restrict__ max_hot, bool compact) {
+                                                uint64_t* __restrict__ max_hot, bool compact, uint32_t fast_cap) {
   const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t h = 0, f = 0;  // k_doc hot set; k_doc_fast LDS slice (0: outside its envelope)
   uint64_t saved = 0;     // the whole plan of a document given the compact one (its overflow reserve)
@@ -890,7 +890,9 @@ __global__ void __launch_bounds__(256) k_bounds(const uint8_t* __restrict__ aren
   h = doc_scattered(b) ? (1ull << 40) : L.hot_total;
   if (fast_eligible(b, dd)) f = fast_layout(b, dd.known_count).total;
   uint64_t total = L.total;
-  if (compact && f) {  // k_doc_fast's document: its compact plan (k_rest re-plans it if the kernel gives up)
+  // k_doc_fast's document: its compact plan (k_rest re-plans it if the kernel gives up). A slice above
+  // the launch's (a pipeline's fixed fast_lds) never runs there: it keeps the whole plan in the scan
+  if (compact && f && f <= fast_cap) {
     b.U |= 4u;
     total = ws_layout(b).total;
     saved = L.total;
@@ -1030,7 +1032,7 @@ void am_launch_bounds(const BatchDev& b, hipStream_t s) {
   if (!b.ndocs) return;
   (void)hipMemsetAsync(b.max_hot, 0, 4 * sizeof(uint64_t), s);
   hipLaunchKernelGGL(k_bounds, dim3((b.ndocs + 255) / 256), dim3(256), 0, s, b.arena, b.docs, b.ndocs, b.chunks, b.info, b.bounds,
-                     b.ws_bytes, b.max_hot, b.compact);
+                     b.ws_bytes, b.max_hot, b.compact, b.fast_cap);
   uint32_t nblk = (b.ndocs + SCAN_T - 1) / SCAN_T;
   hipLaunchKernelGGL(k_scan_blocks, dim3(nblk), dim3(SCAN_T), 0, s, b.ws_bytes, b.ws_off, b.scan_tmp, b.ndocs);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, s, b.scan_tmp, nblk, b.ws_total);

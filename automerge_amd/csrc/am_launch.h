@@ -32,6 +32,8 @@ struct BatchDev {
   bool fast_only;          // every document is in the fast envelope: skip the k_doc launches
   bool any_diff;           // some document asks for its applyChanges patch (k_doc_fast<true>)
   bool compact;            // k_bounds gives k_doc_fast's documents the compact plan (ws_layout, U bit 2)
+  uint32_t fast_cap;       // ... only those whose fast slice fits the launch's (a pipeline's fixed fast_lds;
+                           // a batch sizes its launch from the largest slice, so every one fits)
   uint8_t* ws;
   uint64_t ws_cap;
   am_doc_result* results;

@@ -3,6 +3,7 @@
 // AM_HOST_THREADS threads (default: the machine's, at most 16), in chunks of 64 items.
 #pragma once
 #include <stdlib.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -61,20 +62,40 @@ void am_par_for(size_t n, F f) {
 // workers, as before. The thread is started on first use (never before a fork of the caller's).
 class AmReclaimer {
  public:
+  // at most kMaxQueued batches wait for the thread: a caller that outruns it frees in its own
+  // time (backpressure) instead of letting the queued memory grow without bound
+  static constexpr size_t kMaxQueued = 8;
   static AmReclaimer& get() {
-    static AmReclaimer* r = new AmReclaimer();  // never destroyed: the thread may outlive main()
+    static std::atomic<AmReclaimer*> cur{nullptr};
+    AmReclaimer* r = cur.load();
+    // a forked child inherits the object but not its thread: it starts a reclaimer of its own (the
+    // parent's is leaked in the child; its mutex may have been held at the fork)
+    if (!r || r->pid_ != getpid()) {
+      static std::mutex mk;
+      std::lock_guard<std::mutex> g(mk);
+      r = cur.load();
+      if (!r || r->pid_ != getpid()) {
+        r = new AmReclaimer();  // never destroyed: the thread may outlive main()
+        cur.store(r);
+      }
+    }
     return *r;
   }
   void push(std::function<void()> f) {
     {
-      std::lock_guard<std::mutex> g(m_);
+      std::unique_lock<std::mutex> g(m_);
+      if (q_.size() >= kMaxQueued) {
+        g.unlock();
+        f();  // the queue is full: free inline
+        return;
+      }
       q_.push_back(std::move(f));
     }
     cv_.notify_one();
   }
 
  private:
-  AmReclaimer() { std::thread([this] { run(); }).detach(); }
+  AmReclaimer() : pid_(getpid()) { std::thread([this] { run(); }).detach(); }
   void run() {
     for (;;) {
       std::function<void()> f;
@@ -87,6 +108,7 @@ class AmReclaimer {
       f();
     }
   }
+  const pid_t pid_;
   std::mutex m_;
   std::condition_variable cv_;
   std::deque<std::function<void()>> q_;

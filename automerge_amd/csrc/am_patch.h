@@ -251,6 +251,7 @@ AM_PHD inline uint64_t patch_pack(const PatchOut& o, int64_t max_op, uint8_t* ds
 #define PATCH_E_UNKNOWN_COUNTER 32u  // increment operation arg0@actor(arg1) for unknown counter
 #define PATCH_U_CAPACITY 106u
 #define PATCH_U_VALUE 105u
+#define PATCH_U_INC_VALUE 107u  // a non-integer increment: the replay goes on, the patch value is unknown
 
 // ---- value decode (decodeValue, columnar.js:300-329) ----
 template <class Src>

@@ -5,7 +5,7 @@ columnar.js:659-686, mod N: workload.c4_shard); shard_range is the plain range s
 workloads use. The only exchange is one all-gather of a small per-rank digest after the timed
 region (RCCL over xGMI on the GPU box; gloo in the CPU tests)."""
 
-DIGEST_FIELDS = ("docs", "ops", "errors", "out_bytes", "out_digest")
+DIGEST_FIELDS = ("docs", "ops", "errors", "out_bytes", "out_digest", "patch_digest")
 
 
 def shard_range(rank, world, docs_per_rank):
@@ -61,6 +61,37 @@ def doc_digest_np(index, status, out_len, chk):
         return int(t.sum(dtype=np.uint64)) & 0x7FFFFFFFFFFFFFFF
 
 
+def _hexb(v):
+    return bytes(v).hex()
+
+
+def patch_canon(p):
+    """The part of an applyChanges patch the device writes (new.js:1862-1865: clock and diffs; deps and
+    maxOp follow from the merged document, which its checksum term covers) as canonical JSON."""
+    import json
+    return json.dumps({"clock": p["clock"], "diffs": p["diffs"]}, sort_keys=True, separators=(",", ":"),
+                      default=_hexb).encode()
+
+
+def patch_term(index, p):
+    """Digest term of one document's patch: its global index mixed with the first 8 bytes of the
+    SHA-256 of patch_canon(p) (summed mod 2^63 like the document terms)."""
+    import hashlib
+    h = int.from_bytes(hashlib.sha256(patch_canon(p)).digest()[:8], "little")
+    return _mix64(h ^ _mix64(index & M64))
+
+
+def patch_terms_of_logs(ids, logs):
+    """Sum of patch_term over the engine's wire-form patch logs (automerge_amd/patch.py materializes
+    them; a failed document's term is 0)."""
+    from . import patch as P
+    t = 0
+    for i, log in zip(ids, logs):
+        if log:
+            t += patch_term(int(i), P.materialize(log, [], 0, 0))
+    return t & 0x7FFFFFFFFFFFFFFF
+
+
 def combine(terms):
     """Sum of per-document terms mod 2^63 (order independent; am_batch_digest computes the same)."""
     return sum(terms) & 0x7FFFFFFFFFFFFFFF
@@ -77,5 +108,6 @@ def exchange(dist, digest, device):
         parts = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
         dist.all_gather(parts, t)
         rows = [p.tolist() for p in parts]
-    tot = [sum(r[i] for r in rows) for i in range(len(DIGEST_FIELDS) - 1)]
-    return tot + [combine(r[-1] for r in rows)], rows
+    k = len(digest) - 2  # the last two fields are digests (summed mod 2^63)
+    tot = [sum(r[i] for r in rows) for i in range(k)]
+    return tot + [combine(r[j] for r in rows) for j in range(k, len(digest))], rows

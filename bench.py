@@ -27,6 +27,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -58,6 +60,101 @@ def _oracle_sample(args):
     return n, time.perf_counter() - t0
 
 
+def bind_numa(local):
+    """Binds this rank (and the CPU-baseline workers it forks) to the CPUs of its GPU's NUMA node,
+    before any GPU call: the pinned staging arenas (hipHostMallocNumaUser, am_capi.hip) are then
+    placed on the socket the GPU hangs off. HIP device `local` is the local-th GPU node of the KFD
+    topology (after ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES when they list indices); its PCI
+    address gives the node. Returns what it found (reported in the bench line), never fails."""
+    info = {"gpu": local, "numa_node": None, "bound": False}
+    try:
+        topo = "/sys/class/kfd/kfd/topology/nodes"
+        gpus = []
+        for n in sorted(os.listdir(topo), key=int):
+            props = {}
+            with open(os.path.join(topo, n, "properties")) as f:
+                for ln in f:
+                    k, _, v = ln.partition(" ")
+                    props[k] = v.strip()
+            if int(props.get("simd_count", "0")) > 0:
+                gpus.append(props)
+        idx = local
+        for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+            vis = os.environ.get(var)
+            if vis:
+                ids = [x for x in vis.split(",") if x.strip()]
+                if not all(x.strip().isdigit() for x in ids):
+                    return dict(info, why="%s names devices by id" % var)
+                idx = int(ids[idx])
+        g = gpus[idx]
+        loc, dom = int(g["location_id"]), int(g.get("domain", "0"))
+        bdf = "%04x:%02x:%02x.%x" % (dom, loc >> 8, (loc >> 3) & 31, loc & 7)
+        info["pci"] = bdf
+        with open("/sys/bus/pci/devices/%s/numa_node" % bdf) as f:
+            node = int(f.read())
+        info["numa_node"] = node
+        if node < 0:
+            return info
+        cpus = set()
+        with open("/sys/devices/system/node/node%d/cpulist" % node) as f:
+            for part in f.read().strip().split(","):
+                a, _, b = part.partition("-")
+                cpus.update(range(int(a), int(b or a) + 1))
+        mine = cpus & os.sched_getaffinity(0)
+        if mine:
+            os.sched_setaffinity(0, mine)
+            info.update(bound=True, cpus=len(mine))
+    except (OSError, ValueError, KeyError, IndexError) as e:
+        info["why"] = "%s: %s" % (type(e).__name__, e)
+    return info
+
+
+_PATCH_MODS = None
+
+
+def _patch_part(args):
+    """Sum of shard.patch_term over one slice of the engine's wire-form patch logs, in a CPU-baseline
+    worker (forked before the GPU was touched): automerge_amd/patch.py and shard.py are loaded as
+    plain files, so the worker never loads the HIP library."""
+    global _PATCH_MODS
+    ids, logs = args
+    if _PATCH_MODS is None:
+        import importlib.util
+
+        def load(name):
+            spec = importlib.util.spec_from_file_location("_am_" + name, os.path.join(ROOT, "automerge_amd", name + ".py"))
+            m = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(m)
+            return m
+        _PATCH_MODS = load("patch"), load("shard")
+    P, S = _PATCH_MODS
+    t = 0
+    for i, log in zip(ids, logs):
+        if log:
+            t += S.patch_term(int(i), P.materialize(log, [], 0, 0))
+    return t & 0x7FFFFFFFFFFFFFFF
+
+
+def patch_digest(pool, ids, summ_b, pats_b):
+    """Digest of every document's applyChanges patch of this rank (shard.patch_term summed), from the
+    wire-form logs the pipeline brought home; on the CPU-baseline workers when there are any."""
+    from automerge_amd import shard
+    jobs = []
+    k0 = 0
+    for s_, pb in zip(summ_b, pats_b):
+        off = s_["patch_off"].astype(np.int64)
+        ln = s_["patch_len"].astype(np.int64)
+        ok = s_["status"] == 0
+        raw = pb.tobytes() if len(pb) else b""
+        logs = [raw[o:o + n] if good else b"" for o, n, good in zip(off.tolist(), ln.tolist(), ok.tolist())]
+        for a in range(0, len(logs), 4096):
+            jobs.append((ids[k0 + a:k0 + a + 4096].tolist(), logs[a:a + 4096]))
+        k0 += len(logs)
+    if pool is not None:
+        return shard.combine(pool.map(_patch_part, jobs))
+    return shard.combine(_patch_part(j) for j in jobs)
+
+
 def cpu_pool(procs):
     """The worker processes of the all-cores CPU baseline, forked before this process touches the
     GPU or imports torch (a fork of a GPU-initialised process is not safe on this pool)."""
@@ -82,15 +179,16 @@ def cpu_baseline(pool, procs, wl, seconds=6.0, ops_per_doc=60):
                           "sample": "%d %s documents on %d processes at once, %.1f s" % (nall, name, procs, tall)}}
 
 
-def pinned_digest(docs):
+def pinned_digest(docs, field="digest"):
     """The digest of the whole C4 job of `docs` documents computed by the oracle in the build
-    container (tools/pin_c4_digest.py -> tests/golden/c4_digest.json), or None."""
+    container (tools/pin_c4_digest.py -> tests/golden/c4_digest.json), or None. field: "digest" (the
+    merged documents) or "patch_digest" (their applyChanges patches)."""
     try:
         rec = json.load(open(os.path.join(ROOT, "tests", "golden", "c4_digest.json")))
     except (OSError, ValueError):
         return None
     r = rec.get(str(docs))
-    return int(r["digest"]) if r else None
+    return int(r[field]) if r and field in r else None
 
 
 def decode_alg_bytes(arena, chunks, docs, sample=256):
@@ -184,12 +282,14 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    # the CPU baseline's workers are forked now, before torch is imported or the GPU is touched
-    procs = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16 per GPU
-    pool = cpu_pool(procs) if rank == 0 and not args.no_cpu_baseline else None
     # AM_BENCH_DEVICE / AM_DIST_BACKEND=gloo: every rank on one GPU with a CPU exchange (the N>1
     # rehearsal of tests/test_gpu_bench_ranks.py; RCCL refuses two ranks on one device)
     local = int(os.environ.get("AM_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    # this rank on its GPU's NUMA node before anything touches the GPU (or forks)
+    numa = bind_numa(local)
+    # the CPU baseline's workers are forked now, before torch is imported or the GPU is touched
+    procs = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16 per GPU
+    pool = cpu_pool(procs) if rank == 0 and not args.no_cpu_baseline else None
     backend = os.environ.get("AM_DIST_BACKEND", "nccl")
     import numpy as np
     import torch
@@ -202,6 +302,7 @@ def main():
         else:
             dist.init_process_group(backend=backend)
         dist_info = {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()), "rank": dist.get_rank()}
+    dist_info["numa"] = numa
     torch.cuda.set_device(local)
     xdev = "cuda" if backend == "nccl" else "cpu"
 
@@ -406,7 +507,15 @@ def main():
         return o, (p_ if not args.no_patch else None)
 
     nerr = int((statuses != 0).sum())
-    tot, _ = shard.exchange(dist, [D, ops_rank, nerr, out_bytes, digest or 0], xdev)
+    # every document's patch, materialized after the timed region (the reference's patch objects)
+    t_pd = time.perf_counter()
+    pdig = patch_digest(pool, ids, summ_b, pats_b) if not args.no_patch else 0
+    t_pd = time.perf_counter() - t_pd
+    tot, _ = shard.exchange(dist, [D, ops_rank, nerr, out_bytes, digest or 0, pdig], xdev)
+    if dist is not None:  # rank -> GPU -> NUMA node of every rank, for the line (outside the timed region)
+        allnuma = [None] * world
+        dist.all_gather_object(allnuma, dict(numa, rank=rank))
+        dist_info["numa"] = allnuma
     # correctness spot check against the oracle (outside the timed region): merged bytes and patch
     checked = 0
     if args.check and rank == 0:
@@ -450,9 +559,15 @@ def main():
     cpu = cpu_baseline(pool, procs, args.workload, ops_per_doc=per_doc) if pool is not None else None
     # the whole job against the oracle's digest of every document (tests/golden/c4_digest.json)
     want = pinned_digest(tot[0]) if args.workload == "c4" and digest is not None else None
+    want_p = pinned_digest(tot[0], "patch_digest") if args.workload == "c4" and not args.no_patch else None
     if want is not None:
         extra["digest_pinned"] = {"expected": want, "match": tot[4] == want,
                                   "how": "oracle load + applyChanges + save of all %d documents (tools/pin_c4_digest.py)" % tot[0]}
+        if want_p is not None:
+            extra["digest_pinned"]["patches"] = {
+                "expected": want_p, "got": tot[5], "match": tot[5] == want_p, "materialize_s_rank0": t_pd,
+                "how": "every document's applyChanges patch materialized from the engine's wire form (automerge_amd/patch.py) "
+                       "and hashed (shard.patch_term: clock + diffs), against the oracle's patches of all %d documents" % tot[0]}
     wl = {"c4": "C4 1M-document job: load base doc + applyChanges of 12 concurrent changes (4 actors x 3), 60 ops/doc",
           "c2": "C2: applyChanges of 3 changes (10 map/counter/string sets + 2 concurrent inc/overwrite), 14 ops/doc"}
     what = ("from host memory: H2D + merge + applyChanges patch + D2H (pipelined)" if args.mode == "pipe" else
@@ -475,7 +590,7 @@ def main():
         "errors": tot[2], "verified_docs": checked, "input_bytes_rank0": in_b, "output_bytes_rank0": out_bytes,
         "patch_bytes_rank0": patch_bytes, "workspace_bytes_per_batch": workspace,
         "workspace_bytes_per_doc": workspace / max(1, ncap), "gen_s": t_gen,
-        "docs_per_sec": tot[0] / (elapsed / args.steps), "digest": tot[4],
+        "docs_per_sec": tot[0] / (elapsed / args.steps), "digest": tot[4], "patch_digest": tot[5],
         "cpu_baseline": cpu, "cpu_reference_node": cpu_reference(),
     }
     line.update(extra)
@@ -484,6 +599,8 @@ def main():
         dist.destroy_process_group()
     if want is not None and tot[4] != want:
         sys.exit("bench: the job's digest %d differs from the oracle's %d" % (tot[4], want))
+    if want_p is not None and tot[5] != want_p:
+        sys.exit("bench: the job's patch digest %d differs from the oracle's %d" % (tot[5], want_p))
 
 
 if __name__ == "__main__":

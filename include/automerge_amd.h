@@ -77,6 +77,8 @@ enum am_status {
   AM_U_DEL_SHAPE,           // del op without preds, or inserting del (reference keeps it as a row)
   AM_U_VALUE,               // null action / null pred / mixed map+list object / 2^31+ sizes
   AM_U_CAPACITY,            // workspace bound exceeded (internal)
+  AM_U_INC_VALUE,           // a non-integer counter increment in an applyChanges patch (JS adds it as a
+                            // float / string, new.js:958); loadChanges commits (the patch is dropped)
 };
 
 // ---- host -> device descriptors ----
@@ -326,6 +328,10 @@ int am_pipe_resident_sync(am_pipe *p, float *ms2, am_error *err);
 /* Device time (ms) of the batches retired since the last call (reset on read): [0] their whole
  * compute chains summed, [1] their document kernels (k_doc_fast + k_doc) summed; n = batches. */
 int am_pipe_times(am_pipe *p, float *ms2, uint32_t *n);
+/* Diagnostics: a pipeline created with AM_DEBUG_WS_CANARY=<n> in the environment follows every slot's
+ * workspace with n canary bytes; after am_pipe_drain this returns the offset of the first one a
+ * kernel wrote (any slot), -1 when none, -2 when the pipeline has no canary. */
+int64_t am_pipe_ws_canary(am_pipe *p);
 
 /* ---- per-document backend state (mirrors backend/backend.js over the batch path, n = 1) ---- */
 am_doc *am_doc_init(am_engine *eng);

@@ -1,7 +1,8 @@
 """bench.py's N>1 path on one GPU: two ranks (torch.distributed.run, gloo exchange, both on
 device 0) split the C4 job by document hash (workload.c4_shard), each runs its shard
-through the pipeline, and the all-gathered totals and digest equal the single-rank run's and the
-oracle's pinned digest of the same documents (tests/golden/c4_digest.json)."""
+through the pipeline, and the all-gathered totals and digests -- of the merged documents and of
+their applyChanges patches -- equal the single-rank run's and the oracle's pinned digests of the
+same documents (tests/golden/c4_digest.json)."""
 import json
 import os
 import subprocess
@@ -30,10 +31,13 @@ def test_two_ranks_equal_one_rank():
     two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", "29517"] + args,
                {"AM_DIST_BACKEND": "gloo", "AM_BENCH_DEVICE": "0", "OMP_NUM_THREADS": "4"})
-    pinned = json.load(open(os.path.join(ROOT, "tests", "golden", "c4_digest.json")))[str(DOCS)]["digest"]
+    rec = json.load(open(os.path.join(ROOT, "tests", "golden", "c4_digest.json")))[str(DOCS)]
+    pinned, pinned_p = rec["digest"], rec["patch_digest"]
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
     for r in (one, two):
         assert r["config"]["total_docs"] == DOCS and r["errors"] == 0
         assert r["digest"] == pinned and r["digest_pinned"]["match"]
+        # every document's applyChanges patch against the oracle's (clock + diffs, shard.patch_term)
+        assert r["patch_digest"] == pinned_p and r["digest_pinned"]["patches"]["match"]
     assert two["config"]["docs_rank0"] < DOCS  # rank 0 merged only its shard
     assert one["output_bytes_rank0"] > two["output_bytes_rank0"]

@@ -1,8 +1,9 @@
 """N>1 path of bench.py on CPU: two ranks (gloo, 127.0.0.1) shard the C4 job with bench.py's own
 partition (SHA-256 of the base document, first byte mod N: workload.c4_shard), merge their shard
 (here with the CPU checker; on the GPU box with the engine) and exchange the per-rank digest with
-one all-gather. The gathered totals must equal one process over all documents, and the shards
-must be disjoint and cover the job."""
+one all-gather: documents, ops, errors, output bytes, the merged documents' digest and the
+applyChanges patches' digest. The gathered totals must equal one process over all documents, and
+the shards must be disjoint and cover the job."""
 import os
 import socket
 import sys
@@ -31,16 +32,16 @@ def _merge_shard(world, rank):
     import workload
     ids = workload.c4_shard(0, TOTAL_DOCS, world, rank)
     arena, chunks, docs, ops = workload.c4_list(ids)
-    lens, terms = [], []
+    lens, terms, pterms = [], [], []
     for i, gi in enumerate(ids):
         base, changes = workload.doc_chunks(arena, chunks, docs, i)
         assert shard.shard_of(base, world) == rank
         d = O.Doc.load(base)
-        d.apply(changes)
+        pterms.append(shard.patch_term(int(gi), d.apply_patch(changes)))
         out = d.save()
         lens.append(len(out))
         terms.append(shard.doc_digest(int(gi), 0, out))
-    return [len(ids), ops, 0, sum(lens), shard.combine(terms)], [int(x) for x in ids]
+    return [len(ids), ops, 0, sum(lens), shard.combine(terms), shard.combine(pterms)], [int(x) for x in ids]
 
 
 def _worker(rank, world, port, outdir):
@@ -69,13 +70,13 @@ def test_two_rank_gloo_digest_matches_single_process(tmp_path):
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     got = [np.load(os.path.join(tmp_path, "rank%d.npy" % r)).tolist() for r in range(world)]
-    assert got[0][:5] == got[1][:5]  # every rank sees the same gathered totals
-    ids = sorted(got[0][5:] + got[1][5:])
+    nf = 6
+    assert got[0][:nf] == got[1][:nf]  # every rank sees the same gathered totals
+    ids = sorted(got[0][nf:] + got[1][nf:])
     assert ids == list(range(TOTAL_DOCS))  # disjoint, covering
-    assert got[0][5:] and got[1][5:]
+    assert got[0][nf:] and got[1][nf:]
     single, _ = _merge_shard(1, 0)
-    assert got[0][:4] == single[:4]
-    assert got[0][4] == single[4]
+    assert got[0][:nf] == single[:nf]
 
 
 def test_digest_detects_one_wrong_byte_and_equal_lengths():
@@ -89,3 +90,15 @@ def test_digest_detects_one_wrong_byte_and_equal_lengths():
     assert shard.combine(shard.doc_digest(i, 0, o) for i, o in enumerate(bad)) != base
     swapped = [outs[1], outs[0]] + outs[2:]  # same multiset, wrong owners
     assert shard.combine(shard.doc_digest(i, 0, o) for i, o in enumerate(swapped)) != base
+
+
+def test_patch_term_covers_clock_and_diffs():
+    from automerge_amd import shard
+    p = {"maxOp": 3, "deps": [], "pendingChanges": 0, "clock": {"aa": 1},
+         "diffs": {"objectId": "_root", "type": "map", "props": {"k": {"1@aa": {"type": "value", "value": 1}}}}}
+    t = shard.patch_term(5, p)
+    assert t == shard.patch_term(5, dict(p, maxOp=9, deps=["x"]))  # the document's checksum term covers these
+    assert t != shard.patch_term(6, p)
+    q = dict(p, diffs=dict(p["diffs"], props={"k": {"1@aa": {"type": "value", "value": 2}}}))
+    assert t != shard.patch_term(5, q)
+    assert t != shard.patch_term(5, dict(p, clock={"aa": 2}))

@@ -1,10 +1,11 @@
 #!/bin/bash
-# Round-5 final measurements on the GPU box: the default bench, its rocprofv3 kernel-trace stats,
+# Round-end measurements on the GPU box: the default bench, its rocprofv3 kernel-trace stats,
 # the PMC passes behind roofline.traffic (then the bench again, which reports them), the SQ
-# instruction counters of k_doc_fast, and the host-link copy probe. Outputs under gpurun_out/r5final.
+# instruction counters of k_doc_fast, and the host-link copy probe. Outputs under gpurun_out/<tag>.
+#   gpurun -- bash tools/gpu_round_final.sh <tag>
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r5final
+O=$R/gpurun_out/${1:-final}
 mkdir -p $O
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; exit 1; }

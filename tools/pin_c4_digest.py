@@ -3,8 +3,11 @@
 oracle, in the build container: every document is loaded, merged with its 12 changes and saved by
 oracle/liboracle.so (test infrastructure, pinned to the reference by tests/test_oracle.py), and the
 per-document terms of automerge_amd/shard.py doc_digest (index, container checksum, length, status)
-are summed. bench.py compares the digest its pipeline computes over every merged document with the
-committed value (tests/golden/c4_digest.json).
+are summed, and so are the terms of every document's applyChanges patch (shard.patch_term: SHA-256
+of the canonical JSON of its clock and diffs, from the oracle's applyChanges patch, itself pinned to
+the reference by tests/test_apply_patch_oracle.py). bench.py compares the two digests its pipeline
+computes over every merged document and every patch log with the committed values
+(tests/golden/c4_digest.json).
 
   python tools/pin_c4_digest.py [--docs 1048576] [--procs 8]
 """
@@ -31,18 +34,21 @@ def part(args):
     chk = np.zeros(hi - lo, np.uint64)
     lens = np.zeros(hi - lo, np.uint64)
     status = np.zeros(hi - lo, np.uint64)
+    pterms = 0
     for i in range(hi - lo):
         base, changes = workload.doc_chunks(arena, chunks, docs, i)
         try:
             d = O.Doc.load(base) if base else O.Doc.init()
-            d.apply(changes)
+            pat = d.apply_patch(changes)  # applies the changes and returns the applyChanges patch
             out = d.save()
         except O.OracleError:
             status[i] = 1
             continue
         chk[i] = int.from_bytes(out[4:8], "little")
         lens[i] = len(out)
-    return shard.doc_digest_np(np.arange(lo, hi, dtype=np.uint64), status, lens, chk), int((status != 0).sum())
+        pterms += shard.patch_term(lo + i, pat)
+    return (shard.doc_digest_np(np.arange(lo, hi, dtype=np.uint64), status, lens, chk), int((status != 0).sum()),
+            pterms & 0x7FFFFFFFFFFFFFFF)
 
 
 def main():
@@ -58,9 +64,10 @@ def main():
         res = pool.map(part, ranges)
     digest = shard.combine(r[0] for r in res)
     errors = sum(r[1] for r in res)
-    rec = {"docs": args.docs, "digest": digest, "errors": errors,
+    rec = {"docs": args.docs, "digest": digest, "errors": errors, "patch_digest": shard.combine(r[2] for r in res),
            "how": "oracle/liboracle.so load + applyChanges + save of every C4 document (workload.c4_list), "
-                  "shard.doc_digest terms summed mod 2^63 (tools/pin_c4_digest.py)",
+                  "shard.doc_digest terms summed mod 2^63; patch_digest: shard.patch_term of every document's "
+                  "applyChanges patch (oracle), summed mod 2^63 (tools/pin_c4_digest.py)",
            "seconds": round(time.perf_counter() - t0, 1), "procs": args.procs}
     try:
         pinned = json.load(open(OUT))
