@@ -25,22 +25,19 @@ WANT_DIFF = 4   # AM_DOC_WANT_DIFF: also write the patch applyChanges returns
 
 def pack(docs, device=0, flags=0):
     """docs: iterable of (base_bytes | None, [change bytes]) -> (arena, chunks, docdescs).
-    Compressed change chunks (type 2) are inflated on the GPU when the batch is staged
-    (am_inflate.hip); base documents with DEFLATEd columns go through am_stage_documents (one batch).
+    Compressed inputs go in as they are: the batch stage inflates compressed change chunks (type 2)
+    and the DEFLATEd columns of base documents on the GPU (am_inflate.hip, am_capi.hip inflate_stage).
     flags: WANT_PATCH or WANT_DIFF for every document."""
     parts, chunks, descs = [], [], []
     off = 0
-    docs = list(docs)
-    # every base document's DEFLATEd columns in one GPU checksum + inflate batch
-    staged = iter(N.stage_documents([b for b, _ in docs if b], device))
     for base, changes in docs:
         d = np.zeros((), DOC_DT)
         d["base_chunk"] = -1
         changes = [bytes(c) for c in changes]
         if base:
-            base, verified = next(staged)
+            base = bytes(base)
             d["base_chunk"] = len(chunks)
-            chunks.append((off, len(base), 1 if verified else 0))
+            chunks.append((off, len(base), 0))
             parts.append(base)
             off += len(base)
         d["chg_begin"] = len(chunks)
@@ -171,8 +168,8 @@ class Batch:
         return out.astype(bool)
 
     def inflate_info(self):
-        """(change chunks inflated on the GPU, inflated arena bytes, ms of the two inflate passes)
-        of the last stage."""
+        """(DEFLATE streams inflated on the GPU -- compressed change chunks and DEFLATEd document
+        columns --, bytes of the rebuilt arena, ms of the two inflate passes) of the last stage."""
         n = C.c_uint64()
         nb = C.c_uint64()
         ms = C.c_float()

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <memory>
 #include <functional>
 #include <cstdarg>
 #include <cstdio>
@@ -98,6 +99,7 @@ std::string message_for(uint32_t code, int64_t a0, int64_t a1, const std::string
     case AM_E_DOC_SEQ:
       return "Expected seq " + (a0 == AM_NULL64 ? std::string("NaN") : std::to_string(a0)) + ", got " +
              std::to_string(a1) + " for actor " + actor;
+    case AM_E_INFLATE: return "invalid deflate data";
     case AM_U_HASH_GRAPH: return "automerge_amd: unsupported: needs the change hash graph of a loaded document";
     case AM_U_UNKNOWN_COLUMN: return "automerge_amd: unsupported: column id outside the known column set";
     case AM_U_NONCAUSAL: return "automerge_amd: unsupported: operation ids violate causal (Lamport) order";
@@ -199,6 +201,24 @@ bool zdeflate(const uint8_t* p, size_t n, std::vector<uint8_t>& out) {
   out.resize(got);
   return true;
 }
+
+// AM_SYNC_PROFILE=1: stage wall times of the batched per-handle calls and the host stages on stderr
+struct HostClock {
+  bool on = std::getenv("AM_SYNC_PROFILE") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  std::string line;
+  void mark(const char* what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    char b[64];
+    std::snprintf(b, sizeof b, " %s=%.1fms", what, std::chrono::duration<double, std::milli>(now - t).count());
+    line += b;
+    t = now;
+  }
+  void print(const char* call, size_t n) {
+    if (on) std::fprintf(stderr, "[am_batch] %s n=%zu%s\n", call, n, line.c_str());
+  }
+};
 
 struct ColEnt { uint64_t id; std::vector<uint8_t> data; };
 struct DocParts {
@@ -326,8 +346,38 @@ struct am_engine {
   uint64_t stat_fast = 0;       // of those, merged by k_doc_fast
 };
 
+// A saved document's container and header as the host stage reads them (decodeDocumentHeader,
+// columnar.js:1006-1038): offsets are chunk-relative; columns = the change columns, then the op
+// columns, each with its id, length and data offset; [post, end) = headsIndexes + extra bytes.
+struct DocLayout {
+  uint64_t data_off = 0, end = 0, pre_end = 0, post = 0;
+  uint32_t nc = 0;
+  std::vector<uint64_t> id, len, off;
+  bool deflated = false;
+};
+// The inflate stage's host tables and device buffers, kept by the batch between stages (a batch
+// staged every step reuses their capacity: no page faults, no hipMalloc / hipFree per stage)
+struct InflateScratch {
+  std::vector<uint8_t> kind, hash, blob;
+  std::vector<uint32_t> nzs, dat, z0, ord, zlen, nseg, s0, sha_of;
+  std::vector<int64_t> base_of;
+  std::vector<uint64_t> hoff;
+  std::vector<DocLayout> lay;
+  std::vector<am_zstream> zs;
+  std::vector<am_chunk_desc> nc, sha;
+  std::vector<std::vector<uint8_t>> dhdr;
+  std::vector<std::vector<uint64_t>> dcl;
+  std::vector<am_seg> seg;
+  DevBuf<am_zstream> d_zs;
+  DevBuf<uint32_t> d_zlen, d_ord;
+  DevBuf<am_chunk_desc> d_sha;
+  DevBuf<uint8_t> d_hash, d_arena, d_blob;  // d_arena: the rebuilt arena; swapped with the batch's
+  DevBuf<am_seg> d_seg;
+};
+
 struct am_batch {
   am_engine* eng = nullptr;
+  std::unique_ptr<InflateScratch> zscr;
   DevBuf<uint8_t> arena;
   DevBuf<am_chunk_desc> chunks;
   DevBuf<am_doc_desc> docs;
@@ -424,65 +474,313 @@ extern "C" am_batch* am_batch_create(am_engine* eng) {
   return b;
 }
 
-// DEFLATE-compressed change chunks (type 2, columnar.js:742/784 -> inflateChange :813) are inflated
-// on the GPU (am_inflate.hip) into a new arena: pass 1 sizes every stream, the host lays the chunks
-// out again in index order (a document's chunks stay adjacent), pass 2 writes the inflated chunks
-// and copies the others. Base document chunks are never inflated here (a type-2 chunk is not a
-// document; k_chunks reports it). Streams that do not inflate keep their bytes and type 2, which
-// k_chunks rejects.
+static bool doc_layout(const uint8_t* p, uint64_t n, DocLayout& L) {
+  Container c;
+  if (n < 9 || std::memcmp(p, "\x85\x6f\x4a\x83", 4) != 0 || !read_container(p, n, c) || c.type != 0) return false;
+  HRd r{p, c.end, c.data_off};
+  L.data_off = c.data_off;
+  L.end = c.end;
+  const uint64_t na = r.u();
+  for (uint64_t i = 0; i < na && r.ok; i++) r.raw(r.u());
+  const uint64_t nh = r.u();
+  r.raw(32 * nh);
+  if (!r.ok) return false;
+  L.pre_end = r.off;
+  for (int t = 0; t < 2 && r.ok; t++) {
+    const uint64_t k = r.u();
+    if (k > 4096) return false;
+    if (t == 0) L.nc = (uint32_t)k;
+    for (uint64_t i = 0; i < k && r.ok; i++) {
+      L.id.push_back(r.u());
+      L.len.push_back(r.u());
+    }
+  }
+  for (size_t i = 0; i < L.id.size() && r.ok; i++) {
+    L.off.push_back(r.off);
+    r.raw(L.len[i]);
+    L.deflated |= (L.id[i] & COL_DEFLATE) != 0;
+  }
+  L.post = r.off;
+  return r.ok;
+}
+
+// DEFLATE on the GPU in the batch stage (am_inflate.hip), so compressed inputs need no host staging:
+//  * compressed change chunks (type 2, columnar.js:742/784 -> inflateChange :813): re-wrapped as
+//    magic + the ORIGINAL checksum + type 1 + uleb(length) + inflated data (k_chunks then verifies
+//    the checksum against the inflated chunk);
+//  * saved documents with DEFLATEd columns (inflateColumn, columnar.js:1062-1068; Backend.load):
+//    rebuilt with every column inflated and its column-table entry rewritten (deflate bit cleared,
+//    new length), the ORIGINAL checksum kept and marked verified -- after a GPU SHA-256 of the
+//    compressed chunk has checked it (a mismatch leaves the chunk as it is: k_chunks reports the
+//    checksum error). A column that does not inflate fails the document (AM_E_INFLATE).
+// Pass 1 sizes every stream, the host lays the chunks out again in index order (a document's
+// chunks stay adjacent) with the new headers in a small blob, pass 2 writes the inflated streams in
+// place and k_copy_segs moves everything else. Streams that do not inflate leave their chunk as
+// it is (a type-2 change then fails in k_chunks).
 static bool inflate_stage(am_batch* b, const uint8_t* arena, uint64_t arena_len, const am_chunk_desc* chunks,
                           uint32_t nchunks, const am_doc_desc* docs, uint32_t ndocs) {
-  std::vector<uint8_t> is_base(nchunks, 0);
+  HostClock clk;
+  if (!b->zscr) b->zscr.reset(new InflateScratch());
+  InflateScratch& X = *b->zscr;
+  // per chunk: 0 as it is, 1 compressed change, 2 document with DEFLATEd columns (base chunks first,
+  // in parallel over the documents; then every other chunk, in parallel over the chunks)
+  std::vector<uint8_t>& kind = X.kind;
+  std::vector<uint32_t>& nzs = X.nzs;  // streams of chunk c
+  std::vector<uint32_t>& dat = X.dat;  // kind 2: the document (index into lay)
+  std::vector<int64_t>& base_of = X.base_of;  // the base chunk of document d, for its first document only
+  kind.assign(nchunks, 0);
+  nzs.assign(nchunks + 1, 0);
+  dat.assign(nchunks, 0);
+  base_of.assign(ndocs, -1);
   for (uint32_t d = 0; d < ndocs; d++)
-    if (docs[d].base_chunk >= 0 && (uint64_t)docs[d].base_chunk < nchunks) is_base[docs[d].base_chunk] = 1;
-  std::vector<uint32_t> zidx;
-  for (uint32_t c = 0; c < nchunks; c++) {
+    if (docs[d].base_chunk >= 0 && (uint64_t)docs[d].base_chunk < nchunks && kind[docs[d].base_chunk] != 3) {
+      kind[docs[d].base_chunk] = 3;  // a base chunk (never a compressed change)
+      base_of[d] = docs[d].base_chunk;
+    }
+  auto container_ok = [&](uint32_t c) {
     const am_chunk_desc& k = chunks[c];
-    if (!is_base[c] && !(k.flags & AM_CHUNK_RAW) && k.len > 9 && k.off + k.len <= arena_len && arena[k.off + 8] == 2 &&
-        std::memcmp(arena + k.off, "\x85\x6f\x4a\x83", 4) == 0)
-      zidx.push_back(c);
-  }
-  b->inflated = (uint32_t)zidx.size();
+    return !(k.flags & AM_CHUNK_RAW) && k.len > 9 && k.off + k.len <= arena_len &&
+           std::memcmp(arena + k.off, "\x85\x6f\x4a\x83", 4) == 0;
+  };
+  std::vector<DocLayout>& lay = X.lay;
+  lay.resize(ndocs);
+  for (uint32_t d = 0; d < ndocs; d++)
+    if (base_of[d] >= 0) lay[d] = DocLayout{};
+  am_par_for(ndocs, [&](size_t d) {
+    if (base_of[d] < 0) return;
+    const uint32_t c = (uint32_t)base_of[d];
+    const am_chunk_desc& k = chunks[c];
+    if (!container_ok(c) || arena[k.off + 8] != 0 || (k.flags & 1)) return;
+    DocLayout& L = lay[d];
+    if (!doc_layout(arena + k.off, k.len, L) || !L.deflated) { L = DocLayout{}; return; }
+    uint32_t n = 0;
+    for (uint64_t id : L.id) n += (id & COL_DEFLATE) ? 1u : 0u;
+    nzs[c] = n;
+    dat[c] = (uint32_t)d;
+  });
+  // base chunks that are not staged go back to kind 0; staged ones to 2 (a base chunk shared by
+  // several documents is staged once, through its first document)
+  for (uint32_t d = 0; d < ndocs; d++)
+    if (base_of[d] >= 0 && kind[base_of[d]] == 3) kind[base_of[d]] = nzs[base_of[d]] ? 2 : 0;
+  am_par_for(nchunks, [&](size_t c) {
+    if (kind[c] || !container_ok((uint32_t)c)) return;
+    const uint8_t* p = arena + chunks[c].off;
+    if (p[8] != 2) return;
+    Container ct;
+    if (!read_container(p, chunks[c].len, ct)) return;
+    kind[c] = 1;
+    nzs[c] = 1;
+  });
+  // streams: exclusive scan of the counts, then each chunk fills its own
+  std::vector<uint32_t>& z0 = X.z0;
+  z0.resize(nchunks + 1);
+  z0[0] = 0;
+  for (uint32_t c = 0; c < nchunks; c++) z0[c + 1] = z0[c] + nzs[c];
+  const uint32_t nz = z0[nchunks];
+  b->inflated = nz;
   b->inflate_ms = 0.f;
-  if (zidx.empty()) return true;
+  if (!nz) return true;
+  std::vector<am_zstream>& zs = X.zs;
+  zs.resize(nz);
+  am_par_for(nchunks, [&](size_t c) {
+    if (!nzs[c]) return;
+    const am_chunk_desc& k = chunks[c];
+    am_zstream z{};
+    z.dst = ~0ull;  // set when placed
+    if (kind[c] == 1) {
+      Container ct;
+      read_container(arena + k.off, k.len, ct);
+      z.src = k.off + ct.data_off;
+      z.len = (uint32_t)ct.data_len;
+      zs[z0[c]] = z;
+      return;
+    }
+    const DocLayout& L = lay[dat[c]];
+    uint32_t q = z0[c];
+    for (size_t i = 0; i < L.id.size(); i++)
+      if (L.id[i] & COL_DEFLATE) {
+        z.src = k.off + L.off[i];
+        z.len = (uint32_t)L.len[i];
+        zs[q++] = z;
+      }
+  });
+  clk.mark("scan");
   hipStream_t s = b->eng->stream;
-  const uint32_t nz = (uint32_t)zidx.size();
-  DevBuf<uint32_t> d_zidx, d_zlen;
-  DevBuf<am_chunk_desc> d_new;
-  DevBuf<uint8_t> d_flag, d_arena;
-  if (!d_zidx.ensure(nz) || !d_zlen.ensure(nz) || !d_new.ensure(nchunks) || !d_flag.ensure(nchunks)) return false;
-  HIPCHECK(hipMemcpyAsync(d_zidx.p, zidx.data(), 4ull * nz, hipMemcpyHostToDevice, s));
+  DevBuf<am_zstream>& d_zs = X.d_zs;
+  DevBuf<uint32_t>&d_zlen = X.d_zlen, &d_ord = X.d_ord;
+  DevBuf<am_chunk_desc>& d_sha = X.d_sha;
+  DevBuf<uint8_t>&d_hash = X.d_hash, &d_arena = X.d_arena, &d_blob = X.d_blob;
+  DevBuf<am_seg>& d_seg = X.d_seg;
+  if (!d_zs.ensure(nz) || !d_zlen.ensure(nz) || !d_ord.ensure(nz)) return false;
+  std::vector<uint32_t>& ord = X.ord;
+  ord.resize(nz);
+  const uint32_t nlong = am_inflate_order(zs.data(), nz, ord.data());
+  HIPCHECK(hipMemcpyAsync(d_zs.p, zs.data(), sizeof(am_zstream) * nz, hipMemcpyHostToDevice, s));
+  HIPCHECK(hipMemcpyAsync(d_ord.p, ord.data(), 4ull * nz, hipMemcpyHostToDevice, s));
   (void)hipEventRecord(b->eng->ev[0], s);
-  am_launch_inflate_size(b->arena.p, b->chunks.p, d_zidx.p, nz, d_zlen.p, s);
+  am_launch_inflate_size(b->arena.p, d_zs.p, d_ord.p, nlong, nz, d_zlen.p, s);
   HIPCHECK(hipGetLastError());  // sizes below come from this launch
   (void)hipEventRecord(b->eng->ev[1], s);
-  std::vector<uint32_t> zlen(nz);
-  HIPCHECK(hipMemcpyAsync(zlen.data(), d_zlen.p, 4ull * nz, hipMemcpyDeviceToHost, s));
-  HIPCHECK(hipStreamSynchronize(s));
-  float ms1 = 0.f;
-  // new layout in chunk-index order
-  std::vector<am_chunk_desc> nc(chunks, chunks + nchunks);
-  std::vector<uint8_t> flag(nchunks, 0);
-  for (uint32_t i = 0; i < nz; i++)
-    if (zlen[i] != 0xFFFFFFFFu) {
-      flag[zidx[i]] = 1;
-      uint32_t u = 1;
-      for (uint64_t v = zlen[i]; v >= 0x80; v >>= 7) u++;
-      nc[zidx[i]].len = 9 + u + zlen[i];
+  // the compressed documents' checksums (SHA-256 of everything after the checksum, container end)
+  std::vector<am_chunk_desc>& sha = X.sha;
+  std::vector<uint32_t>& sha_of = X.sha_of;
+  sha.clear();
+  sha_of.assign(ndocs, 0);
+  for (uint32_t d = 0; d < ndocs; d++)
+    if (base_of[d] >= 0 && kind[base_of[d]] == 2 && dat[base_of[d]] == d) {
+      sha_of[d] = (uint32_t)sha.size();
+      sha.push_back({chunks[base_of[d]].off + 8, (uint32_t)(lay[d].end - 8), 0});
     }
+  if (!sha.empty()) {
+    if (!d_sha.ensure(sha.size()) || !d_hash.ensure(32 * sha.size())) return false;
+    HIPCHECK(hipMemcpyAsync(d_sha.p, sha.data(), sizeof(am_chunk_desc) * sha.size(), hipMemcpyHostToDevice, s));
+    am_launch_sha256(b->arena.p, d_sha.p, (uint32_t)sha.size(), d_hash.p, s);
+  }
+  std::vector<uint32_t>& zlen = X.zlen;
+  std::vector<uint8_t>& hash = X.hash;
+  zlen.resize(nz);
+  hash.resize(32 * sha.size());
+  HIPCHECK(hipMemcpyAsync(zlen.data(), d_zlen.p, 4ull * nz, hipMemcpyDeviceToHost, s));
+  if (!sha.empty()) HIPCHECK(hipMemcpyAsync(hash.data(), d_hash.p, hash.size(), hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  clk.mark("h2d+size+sha");
+  // new layout in chunk-index order. Per chunk its new length and its copy segments (a staged
+  // document's new header goes to its own blob, concatenated below); then a scan places the chunks
+  std::vector<am_chunk_desc>& nc = X.nc;
+  nc.assign(chunks, chunks + nchunks);
+  std::vector<uint32_t>& nseg = X.nseg;
+  nseg.assign(nchunks + 1, 0);
+  std::vector<std::vector<uint8_t>>& dhdr = X.dhdr;  // staged documents' headers
+  std::vector<std::vector<uint64_t>>& dcl = X.dcl;  // ... and their column lengths
+  dhdr.resize(ndocs);
+  dcl.resize(ndocs);
+  am_par_for(nchunks, [&](size_t c) {
+    const am_chunk_desc& k = chunks[c];
+    const uint8_t* p = arena + k.off;
+    if (kind[c] == 1 && zlen[z0[c]] != 0xFFFFFFFFu) {
+      // the header travels with the stream (written by the inflate kernel): checksum, type 1, uleb
+      am_zstream& z = zs[z0[c]];
+      std::memcpy(z.hdr, p + 4, 4);
+      z.hdr[4] = 1;
+      uint32_t q = 5;
+      for (uint64_t v = zlen[z0[c]];;) {
+        const uint8_t byte = v & 0x7f;
+        v >>= 7;
+        z.hdr[q++] = byte | (v ? 0x80 : 0);
+        if (!v) break;
+      }
+      z.hlen = (uint8_t)q;
+      nc[c].len = (uint32_t)(4 + q + zlen[z0[c]]);
+      return;
+    }
+    if (kind[c] == 2) {
+      const uint32_t d = dat[c];
+      const DocLayout& L = lay[d];
+      bool inflated = true;
+      for (uint32_t q = z0[c]; q < z0[c + 1]; q++) inflated &= zlen[q] != 0xFFFFFFFFu;
+      if (std::memcmp(hash.data() + 32 * sha_of[d], p + 4, 4) != 0) {
+        kind[c] = 0;  // checksum mismatch: the chunk stays as it is and k_chunks reports it
+      } else if (!inflated) {
+        kind[c] = 0;
+        nc[c].flags |= AM_CHUNK_BADZ;  // the document fails with AM_E_INFLATE (k_chunks)
+      } else {
+        // body: actors + heads, the two column tables with the new lengths, columns, the rest
+        std::vector<uint64_t>& clen = dcl[d];
+        clen.resize(L.id.size());
+        std::vector<uint8_t> tab;
+        uint64_t cols = 0;
+        uint32_t q = z0[c], ncopy = 0;
+        for (size_t i = 0; i < L.id.size(); i++) {
+          clen[i] = (L.id[i] & COL_DEFLATE) ? zlen[q++] : L.len[i];
+          cols += clen[i];
+          ncopy += (!(L.id[i] & COL_DEFLATE) && L.len[i]) ? 1u : 0u;
+        }
+        put_u(tab, L.nc);
+        for (size_t i = 0; i < L.id.size(); i++) {
+          if (i == L.nc) put_u(tab, L.id.size() - L.nc);
+          put_u(tab, L.id[i] & ~(uint64_t)COL_DEFLATE);
+          put_u(tab, clen[i]);
+        }
+        if (L.id.size() == L.nc) put_u(tab, 0);
+        const uint64_t pre = L.pre_end - L.data_off;
+        const uint64_t body = pre + tab.size() + cols + (L.end - L.post);
+        std::vector<uint8_t>& h = dhdr[d];
+        h.assign(p, p + 8);  // magic + the original checksum
+        h.push_back(0);
+        put_u(h, body);
+        h.insert(h.end(), p + L.data_off, p + L.pre_end);
+        h.insert(h.end(), tab.begin(), tab.end());
+        nc[c].len = (uint32_t)(h.size() + cols + (L.end - L.post));
+        nc[c].flags |= 1;  // the checksum was verified above, on the compressed chunk
+        nseg[c] = 1 + ncopy + (L.end > L.post ? 1u : 0u);
+        return;
+      }
+    }
+    nseg[c] = 1;  // the chunk as it is
+  });
   uint64_t off = 0;
-  for (uint32_t c = 0; c < nchunks; c++) { nc[c].off = off; off += nc[c].len; }
-  if (!d_arena.ensure(off + 64)) return false;
-  HIPCHECK(hipMemcpyAsync(d_new.p, nc.data(), sizeof(am_chunk_desc) * nchunks, hipMemcpyHostToDevice, s));
-  HIPCHECK(hipMemcpyAsync(d_flag.p, flag.data(), nchunks, hipMemcpyHostToDevice, s));
+  std::vector<uint32_t>& s0 = X.s0;
+  std::vector<uint64_t>& hoff = X.hoff;
+  s0.assign(nchunks + 1, 0);
+  hoff.assign(ndocs, 0);
+  uint64_t blob_len = 0;
+  for (uint32_t c = 0; c < nchunks; c++) {
+    nc[c].off = off;
+    off += nc[c].len;
+    s0[c + 1] = s0[c] + nseg[c];
+    if (kind[c] == 2) {
+      hoff[dat[c]] = blob_len;
+      blob_len += dhdr[dat[c]].size();
+    }
+  }
+  std::vector<uint8_t>& blob = X.blob;
+  std::vector<am_seg>& seg = X.seg;
+  blob.resize(blob_len);
+  seg.resize(s0[nchunks]);
+  am_par_for(nchunks, [&](size_t c) {
+    const am_chunk_desc& k = chunks[c];
+    if (kind[c] == 1 && zlen[z0[c]] != 0xFFFFFFFFu) {
+      zs[z0[c]].dst = nc[c].off + 4 + zs[z0[c]].hlen;
+      return;
+    }
+    uint32_t g = s0[c];
+    if (kind[c] != 2) {
+      seg[g] = {k.off, nc[c].off, k.len, 0};
+      return;
+    }
+    const uint32_t d = dat[c];
+    const DocLayout& L = lay[d];
+    const std::vector<uint8_t>& h = dhdr[d];
+    std::memcpy(blob.data() + hoff[d], h.data(), h.size());
+    seg[g++] = {hoff[d], nc[c].off, (uint32_t)h.size(), 1};
+    uint64_t at = nc[c].off + h.size();
+    uint32_t q = z0[c];
+    for (size_t i = 0; i < L.id.size(); i++) {
+      if (L.id[i] & COL_DEFLATE) zs[q++].dst = at;
+      else if (L.len[i]) seg[g++] = {k.off + L.off[i], at, (uint32_t)L.len[i], 0};
+      at += dcl[d][i];
+    }
+    if (L.end > L.post) seg[g++] = {k.off + L.post, at, (uint32_t)(L.end - L.post), 0};
+  });
+  clk.mark("layout");
+  if (!d_arena.ensure(off + 64) || !d_seg.ensure(seg.size()) || !d_blob.ensure(blob.size() + 1)) return false;
+  HIPCHECK(hipMemcpyAsync(d_zs.p, zs.data(), sizeof(am_zstream) * nz, hipMemcpyHostToDevice, s));
+  if (!seg.empty()) HIPCHECK(hipMemcpyAsync(d_seg.p, seg.data(), sizeof(am_seg) * seg.size(), hipMemcpyHostToDevice, s));
+  if (!blob.empty()) HIPCHECK(hipMemcpyAsync(d_blob.p, blob.data(), blob.size(), hipMemcpyHostToDevice, s));
   HIPCHECK(hipMemsetAsync(d_arena.p + off, 0, 64, s));
   (void)hipEventRecord(b->eng->ev[2], s);
-  am_launch_inflate_write(b->arena.p, b->chunks.p, d_new.p, d_zidx.p, nz, d_zlen.p, d_flag.p, nchunks, d_arena.p, s);
+  am_launch_copy_segs(b->arena.p, d_blob.p, d_seg.p, (uint32_t)seg.size(), d_arena.p, s);
+  am_launch_inflate_write(b->arena.p, d_zs.p, d_ord.p, nlong, nz, d_zlen.p, d_arena.p, s);
   (void)hipEventRecord(b->eng->ev[3], s);
   HIPCHECK(hipMemcpyAsync(b->chunks.p, nc.data(), sizeof(am_chunk_desc) * nchunks, hipMemcpyHostToDevice, s));
   HIPCHECK(hipStreamSynchronize(s));
   HIPCHECK(hipGetLastError());
-  float ms2 = 0.f;
+  clk.mark("copy+write");
+  char segs[48];
+  std::snprintf(segs, sizeof segs, " streams=%u long=%u segs=%zu", nz, nlong, seg.size());
+  clk.line += segs;
+  clk.print("inflate_stage", nchunks);
+  float ms1 = 0.f, ms2 = 0.f;
   (void)hipEventElapsedTime(&ms1, b->eng->ev[0], b->eng->ev[1]);
   (void)hipEventElapsedTime(&ms2, b->eng->ev[2], b->eng->ev[3]);
   b->inflate_ms = ms1 + ms2;
@@ -522,6 +820,7 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
       !b->fast_done.ensure(ndocs) || !b->rest.ensure(ndocs + 1) || !b->results.ensure(ndocs) ||
       !b->chg_state.ensure(nchunks))
     return false;
+  HostClock clk;
   if (arena_len) HIPCHECK(hipMemcpyAsync(b->arena.p, arena, arena_len, hipMemcpyHostToDevice, s));
   if (nchunks) HIPCHECK(hipMemcpyAsync(b->chunks.p, chunks, sizeof(am_chunk_desc) * nchunks, hipMemcpyHostToDevice, s));
   if (ndocs) HIPCHECK(hipMemcpyAsync(b->docs.p, docs, sizeof(am_doc_desc) * ndocs, hipMemcpyHostToDevice, s));
@@ -530,7 +829,9 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   b->ndocs = ndocs;
   b->any_diff = false;
   for (uint32_t d = 0; d < ndocs && !b->any_diff; d++) b->any_diff = (docs[d].flags & (AM_DOC_WANT_DIFF | AM_DOC_WANT_PATCH)) != 0;
+  clk.mark("h2d-queued");
   if (!inflate_stage(b, arena, arena_len, chunks, nchunks, docs, ndocs)) return false;
+  clk.mark("inflate-stage");
   // k_doc_fast (am_doc_fast.h) for the documents in its envelope; AM_FAST=0 turns it off
   const char* fe = std::getenv("AM_FAST");
   const bool fast_on = !(fe && fe[0] == '0');
@@ -546,6 +847,8 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   if (ndocs) HIPCHECK(hipMemcpyAsync(&saved, b->max_hot.p + 2, sizeof saved, hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
   HIPCHECK(hipGetLastError());
+  clk.mark("sizing");
+  clk.print("stage", ndocs);
   // a batch reserves the whole plan of every compact document as overflow, so none of them can
   // run out of room if the fast kernel gives up on all of them (the pipe reserves a fraction)
   b->ws_plan = total;
@@ -767,64 +1070,56 @@ extern "C" int am_inflate_raw(am_engine* eng, const uint8_t* const* bufs, const 
   auto fail = [&](const char* m) { to_c(Err{AM_U_CAPACITY, false, m}, err); return 1; };
   if (!set_device(eng)) return fail("automerge_amd: no device");
   hipStream_t s = eng->stream;
+  HostClock clk;
   std::vector<uint8_t> arena;
-  std::vector<am_chunk_desc> ch(n);
-  std::vector<uint32_t> zidx(n);
+  std::vector<am_zstream> zs(n);
   for (size_t i = 0; i < n; i++) {
     if (lens[i] > 0xFFFFFF00u) return fail("automerge_amd: buffer too large");
-    const uint8_t hdr[9] = {0x85, 0x6f, 0x4a, 0x83, 0, 0, 0, 0, 2};
-    ch[i].off = arena.size();
-    arena.insert(arena.end(), hdr, hdr + 9);
-    put_u(arena, lens[i]);
+    zs[i] = {arena.size(), 0, (uint32_t)lens[i], 0};
     arena.insert(arena.end(), bufs[i], bufs[i] + lens[i]);
-    ch[i].len = (uint32_t)(arena.size() - ch[i].off);
-    ch[i].flags = 0;
-    zidx[i] = (uint32_t)i;
   }
   if (!n) return 0;
-  DevBuf<uint8_t> d_arena, d_out, d_flag;
-  DevBuf<am_chunk_desc> d_ch, d_new;
-  DevBuf<uint32_t> d_zidx, d_zlen;
-  if (!d_arena.ensure(arena.size() + 64) || !d_ch.ensure(n) || !d_new.ensure(n) || !d_zidx.ensure(n) || !d_zlen.ensure(n) ||
-      !d_flag.ensure(n))
+  DevBuf<uint8_t> d_arena, d_out;
+  DevBuf<am_zstream> d_zs;
+  DevBuf<uint32_t> d_zlen, d_ord;
+  if (!d_arena.ensure(arena.size() + 64) || !d_zs.ensure(n) || !d_zlen.ensure(n) || !d_ord.ensure(n))
     return fail("automerge_amd: device allocation failed");
-  std::vector<uint32_t> zlen(n);
-  std::vector<am_chunk_desc> nc(ch);
-  std::vector<uint8_t> flag(n, 1);
-  uint64_t off = 0;
+  std::vector<uint32_t> zlen(n), ord(n);
+  const uint32_t nlong = am_inflate_order(zs.data(), (uint32_t)n, ord.data());
   bool okc = hipMemcpyAsync(d_arena.p, arena.data(), arena.size(), hipMemcpyHostToDevice, s) == hipSuccess &&
-             hipMemcpyAsync(d_ch.p, ch.data(), sizeof(am_chunk_desc) * n, hipMemcpyHostToDevice, s) == hipSuccess &&
-             hipMemcpyAsync(d_zidx.p, zidx.data(), 4 * n, hipMemcpyHostToDevice, s) == hipSuccess;
+             hipMemcpyAsync(d_zs.p, zs.data(), sizeof(am_zstream) * n, hipMemcpyHostToDevice, s) == hipSuccess &&
+             hipMemcpyAsync(d_ord.p, ord.data(), 4 * n, hipMemcpyHostToDevice, s) == hipSuccess;
   if (okc) {
-    am_launch_inflate_size(d_arena.p, d_ch.p, d_zidx.p, (uint32_t)n, d_zlen.p, s);
+    am_launch_inflate_size(d_arena.p, d_zs.p, d_ord.p, nlong, (uint32_t)n, d_zlen.p, s);
     okc = hipGetLastError() == hipSuccess && hipMemcpyAsync(zlen.data(), d_zlen.p, 4 * n, hipMemcpyDeviceToHost, s) == hipSuccess &&
           hipStreamSynchronize(s) == hipSuccess;
   }
   if (!okc) return fail("automerge_amd: inflate pass 1 failed");
+  clk.mark("pack+h2d+size");
+  uint64_t off = 0;
   for (size_t i = 0; i < n; i++) {
-    uint32_t u = 1;
-    for (uint64_t v = zlen[i] == 0xFFFFFFFFu ? 0 : zlen[i]; v >= 0x80; v >>= 7) u++;
-    nc[i].off = off;
-    nc[i].len = zlen[i] == 0xFFFFFFFFu ? 0 : 9 + u + zlen[i];
-    off += nc[i].len;
+    zs[i].dst = off;
+    off += zlen[i] == 0xFFFFFFFFu ? 0 : zlen[i];
   }
   if (!d_out.ensure(off + 64)) return fail("automerge_amd: device allocation failed");
   std::vector<uint8_t> out(off);
-  okc = hipMemcpyAsync(d_new.p, nc.data(), sizeof(am_chunk_desc) * n, hipMemcpyHostToDevice, s) == hipSuccess &&
-        hipMemcpyAsync(d_flag.p, flag.data(), n, hipMemcpyHostToDevice, s) == hipSuccess;
+  okc = hipMemcpyAsync(d_zs.p, zs.data(), sizeof(am_zstream) * n, hipMemcpyHostToDevice, s) == hipSuccess;
   if (okc) {
-    am_launch_inflate_write(d_arena.p, d_ch.p, d_new.p, d_zidx.p, (uint32_t)n, d_zlen.p, d_flag.p, (uint32_t)n, d_out.p, s);
+    am_launch_inflate_write(d_arena.p, d_zs.p, d_ord.p, nlong, (uint32_t)n, d_zlen.p, d_out.p, s);
     okc = (off == 0 || hipMemcpyAsync(out.data(), d_out.p, off, hipMemcpyDeviceToHost, s) == hipSuccess) &&
           hipStreamSynchronize(s) == hipSuccess && hipGetLastError() == hipSuccess;
   }
   if (!okc) return fail("automerge_amd: inflate pass 2 failed");
+  clk.mark("write+d2h");
   for (size_t i = 0; i < n; i++) {
     ok[i] = zlen[i] != 0xFFFFFFFFu;
     const size_t m = ok[i] ? zlen[i] : 0;
     outs[i] = (uint8_t*)std::malloc(m ? m : 1);
-    if (m) std::memcpy(outs[i], out.data() + nc[i].off + nc[i].len - m, m);
+    if (m) std::memcpy(outs[i], out.data() + zs[i].dst, m);
     out_lens[i] = m;
   }
+  clk.mark("outs");
+  clk.print("inflate_raw", n);
   if (err) err->code = 0;
   return 0;
 }
@@ -1515,7 +1810,7 @@ bool stage_change(const std::vector<uint8_t>& in, std::vector<uint8_t>& out, Err
     }
     std::vector<uint8_t> dec;
     if (!zinflate(in.data() + c.data_off, c.data_len, dec)) {
-      err = {AM_E_SUBARRAY, false, "invalid deflate data"};
+      err = {AM_E_INFLATE, false, message_for(AM_E_INFLATE, 0, 0, "")};
       return false;
     }
     out = make_chunk(in.data() + 4, 1, dec);
@@ -1707,23 +2002,6 @@ struct ManyOut {
   OneResult res;
   Err err;
   bool ok = false;
-};
-// AM_SYNC_PROFILE=1: stage wall times of the batched per-handle calls on stderr
-struct HostClock {
-  bool on = std::getenv("AM_SYNC_PROFILE") != nullptr;
-  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-  std::string line;
-  void mark(const char* what) {
-    if (!on) return;
-    const auto now = std::chrono::steady_clock::now();
-    char b[64];
-    std::snprintf(b, sizeof b, " %s=%.1fms", what, std::chrono::duration<double, std::milli>(now - t).count());
-    line += b;
-    t = now;
-  }
-  void print(const char* call, size_t n) {
-    if (on) std::fprintf(stderr, "[am_batch] %s n=%zu%s\n", call, n, line.c_str());
-  }
 };
 
 bool run_many(am_engine* e, const std::vector<ManyJob>& jobs, std::vector<ManyOut>& outs, Err& err) {
@@ -1960,7 +2238,7 @@ bool stage_doc(am_engine* e, const std::vector<uint8_t>& in, std::vector<uint8_t
     }
     std::free(zo[i]);
   }
-  if (!all_ok) { err = {AM_E_SUBARRAY, false, "invalid deflate data"}; return false; }
+  if (!all_ok) { err = {AM_E_INFLATE, false, message_for(AM_E_INFLATE, 0, 0, "")}; return false; }
   out = make_chunk(in.data() + 4, 0, join_doc(parts));
   verified = true;
   return true;
@@ -1971,6 +2249,7 @@ bool stage_doc(am_engine* e, const std::vector<uint8_t>& in, std::vector<uint8_t
 // chunk (the input itself when it has no compressed column), errs[i].code != 0 on failure.
 void stage_docs(am_engine* e, size_t n, const uint8_t* const* data, const size_t* lens, std::vector<std::vector<uint8_t>>& out,
                 std::vector<uint8_t>& verified, std::vector<Err>& errs) {
+  HostClock clk;
   out.assign(n, {});
   verified.assign(n, 0);
   errs.assign(n, Err{});
@@ -2006,11 +2285,13 @@ void stage_docs(am_engine* e, size_t n, const uint8_t* const* data, const size_t
     whole[k].assign(data[zi[k]] + 8, data[zi[k]] + zd[zi[k]].end);
     wp[k] = &whole[k];
   }
+  clk.mark("split");
   std::vector<std::array<uint8_t, 32>> hh;
   if (!gpu_sha256(e, wp, 0, hh)) {
     for (size_t i : zi) errs[i] = {AM_U_CAPACITY, false, "automerge_amd: GPU hash failed"};
     return;
   }
+  clk.mark("sha");
   std::vector<std::vector<uint8_t>*> zcol;
   std::vector<uint64_t*> zid;
   std::vector<const uint8_t*> zb;
@@ -2036,6 +2317,7 @@ void stage_docs(am_engine* e, size_t n, const uint8_t* const* data, const size_t
   std::vector<size_t> zn(nz, 0);
   std::vector<uint8_t> zok(nz, 0);
   am_error ae;
+  clk.mark("cols");
   if (nz && am_inflate_raw(e, zb.data(), zl.data(), nz, zo.data(), zn.data(), zok.data(), &ae)) {
     for (size_t i : zi)
       if (!errs[i].code) errs[i] = {AM_U_CAPACITY, false, ae.message};
@@ -2046,16 +2328,19 @@ void stage_docs(am_engine* e, size_t n, const uint8_t* const* data, const size_t
       zcol[q]->assign(zo[q], zo[q] + zn[q]);
       *zid[q] ^= COL_DEFLATE;
     } else if (!errs[zdoc[q]].code) {
-      errs[zdoc[q]] = {AM_E_SUBARRAY, false, "invalid deflate data"};
+      errs[zdoc[q]] = {AM_E_INFLATE, false, message_for(AM_E_INFLATE, 0, 0, "")};
     }
     std::free(zo[q]);
   }
+  clk.mark("inflate");
   am_par_for(zi.size(), [&](size_t k) {
     const size_t i = zi[k];
     if (errs[i].code) return;
     out[i] = make_chunk(data[i] + 4, 0, join_doc(zd[i].parts));
     verified[i] = 1;
   });
+  clk.mark("join");
+  clk.print("stage_docs", n);
 }
 
 }  // namespace

@@ -272,6 +272,7 @@ __device__ __forceinline__ void chunk_body(const uint8_t* p, const am_chunk_desc
   ci.ndeps = 0; ci.nactors = 0; ci.strbytes = 0; ci.nheads = 0; ci.arg0 = 0; ci.nunk = 0;
   uint32_t st = AM_OK;
   do {
+    if (cd.flags & AM_CHUNK_BADZ) { st = AM_E_INFLATE; break; }  // the batch stage could not inflate a column
     // decodeContainerHeader (columnar.js:688)
     if (cd.len < 4) { st = AM_E_SUBARRAY; break; }
     if (p[0] != kMagic[0] || p[1] != kMagic[1] || p[2] != kMagic[2] || p[3] != kMagic[3]) { st = AM_E_MAGIC; break; }
@@ -786,10 +787,13 @@ __host__ __device__ inline bool doc_scattered(const DocBounds& b) { return b.spa
 
 extern __shared__ __attribute__((aligned(16))) uint8_t am_lds[];
 
+#ifndef AM_LDS_DOC_T
+#define AM_LDS_DOC_T DOC_T
+#endif
 #define K_DOC_WAVES_ATTR
 namespace lds_mode {
 constexpr bool kHotLds = true;
-constexpr uint32_t kDocT = DOC_T;  // one wave: the hot set is this document's LDS slice
+constexpr uint32_t kDocT = AM_LDS_DOC_T;  // the waves that share this document's LDS slice
 #include "am_doc_impl.h"
 }  // namespace lds_mode
 #undef K_DOC_WAVES_ATTR
@@ -1100,7 +1104,7 @@ void am_launch_doc(const BatchDev& b, hipStream_t s) {
                          b.ws_total, b.max_hot + 3);
       grid = b.ndocs < K_DOC_LOOP_WG ? b.ndocs : K_DOC_LOOP_WG;
     }
-    hipLaunchKernelGGL(lds_mode::k_doc, dim3(grid), dim3(DOC_T), b.lds_bytes, s, b.arena, b.chunks, b.docs, b.known,
+    hipLaunchKernelGGL(lds_mode::k_doc, dim3(grid), dim3(AM_LDS_DOC_T), b.lds_bytes, s, b.arena, b.chunks, b.docs, b.known,
                        b.info, b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd, rest);
     if (b.max_hot_host > b.lds_bytes)
       hipLaunchKernelGGL(glb_mode::k_doc, dim3(b.ndocs), dim3(DOC_T_GLB), 0, s, b.arena, b.chunks, b.docs, b.known, b.info,

@@ -66,12 +66,28 @@ void am_launch_pipe_compact(const BatchDev& b, uint64_t* olen, uint64_t* ooff, u
 // destinations are device pointers of mapped pinned host memory
 void am_launch_copy_home(const void* s0, void* d0, uint64_t n0, const void* s1, void* d1, uint64_t n1, const void* s2, void* d2,
                          uint64_t n2, uint32_t wgs, hipStream_t s);
-// DEFLATE of compressed change chunks (am_inflate.hip): pass 1 sizes, pass 2 writes the new arena
-void am_launch_inflate_size(const uint8_t* arena, const am_chunk_desc* chunks, const uint32_t* zidx, uint32_t nz,
+// DEFLATE on the GPU (am_inflate.hip): raw streams [src, src + len) of a source arena; pass 1 sizes
+// them, pass 2 writes stream i's output at dst + zs[i].dst; k_copy_segs moves byte ranges from the
+// source arena (from = 0) or a header blob (from = 1) to the new arena
+struct am_zstream {
+  uint64_t src, dst;
+  uint32_t len;
+  uint8_t hlen;     // > 0: a chunk header goes before the output: magic + hdr[0, hlen) (checksum, type, uleb)
+  uint8_t hdr[11];
+};
+struct am_seg {
+  uint64_t src, dst;
+  uint32_t len, from;
+};
+// ord: the launch order (am_inflate_order): ord[0, nlong) are the long streams, largest first, decoded
+// with one-lookup code tables; ord[nlong, nz) the rest
+void am_launch_inflate_size(const uint8_t* src, const am_zstream* zs, const uint32_t* ord, uint32_t nlong, uint32_t nz,
                             uint32_t* zlen, hipStream_t s);
-void am_launch_inflate_write(const uint8_t* arena, const am_chunk_desc* chunks, const am_chunk_desc* nchunks,
-                             const uint32_t* zidx, uint32_t nz, const uint32_t* zlen, const uint8_t* inflated,
-                             uint32_t n, uint8_t* dst, hipStream_t s);
+void am_launch_inflate_write(const uint8_t* src, const am_zstream* zs, const uint32_t* ord, uint32_t nlong, uint32_t nz,
+                             const uint32_t* zlen, uint8_t* dst, hipStream_t s);
+// the launch order of am_launch_inflate_*; returns nlong
+uint32_t am_inflate_order(const am_zstream* zs, uint32_t nz, uint32_t* ord);
+void am_launch_copy_segs(const uint8_t* src, const uint8_t* blob, const am_seg* segs, uint32_t n, uint8_t* dst, hipStream_t s);
 
 // engine internals shared with am_sync.hip
 struct am_engine;

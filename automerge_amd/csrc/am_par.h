@@ -22,6 +22,79 @@ inline unsigned am_host_threads() {
   return n ? n : 1;
 }
 
+// Persistent host workers for am_par_for: a call hands its loop to threads that already exist
+// (spawning and joining 15 threads cost a millisecond or more per call, and the batched calls make
+// several). One loop at a time owns the workers; a loop that finds them busy, or that runs on a
+// worker itself (nested), starts threads of its own as before. A forked child gets a pool of its own.
+class AmPool {
+ public:
+  static AmPool& get() {
+    static std::atomic<AmPool*> cur{nullptr};
+    AmPool* p = cur.load();
+    if (!p || p->pid_ != getpid()) {
+      static std::mutex mk;
+      std::lock_guard<std::mutex> g(mk);
+      p = cur.load();
+      if (!p || p->pid_ != getpid()) {
+        p = new AmPool(am_host_threads());  // never destroyed: its threads may outlive main()
+        cur.store(p);
+      }
+    }
+    return *p;
+  }
+  static bool on_worker() { return worker_flag(); }
+  // runs work() on the calling thread and every worker; false when the workers are busy
+  bool run(const std::function<void()>& work) {
+    std::unique_lock<std::mutex> own(owner_, std::try_to_lock);
+    if (!own.owns_lock()) return false;
+    {
+      std::lock_guard<std::mutex> g(m_);
+      work_ = &work;
+      active_ = (unsigned)th_.size();
+      gen_++;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [&] { return active_ == 0; });
+    work_ = nullptr;
+    return true;
+  }
+
+ private:
+  explicit AmPool(unsigned nt) : pid_(getpid()) {
+    for (unsigned t = 1; t < nt; t++) th_.emplace_back([this] { loop(); });
+    for (auto& t : th_) t.detach();
+  }
+  static bool& worker_flag() {
+    static thread_local bool f = false;
+    return f;
+  }
+  void loop() {
+    worker_flag() = true;
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void()>* w;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return gen_ != seen; });
+        seen = gen_;
+        w = work_;
+      }
+      (*w)();
+      std::lock_guard<std::mutex> g(m_);
+      if (--active_ == 0) done_.notify_one();
+    }
+  }
+  const pid_t pid_;
+  std::vector<std::thread> th_;
+  std::mutex owner_, m_;
+  std::condition_variable cv_, done_;
+  const std::function<void()>* work_ = nullptr;
+  unsigned active_ = 0;
+  uint64_t gen_ = 0;
+};
+
 template <class F>
 void am_par_for(size_t n, F f) {
   const unsigned nt = am_host_threads();
@@ -35,7 +108,7 @@ void am_par_for(size_t n, F f) {
   std::atomic<bool> stop{false};
   std::exception_ptr first;
   std::mutex mu;
-  auto work = [&]() {
+  const std::function<void()> work = [&]() {
     for (;;) {
       const size_t i0 = next.fetch_add(64);
       if (i0 >= n || stop.load(std::memory_order_relaxed)) return;
@@ -49,10 +122,12 @@ void am_par_for(size_t n, F f) {
       }
     }
   };
-  std::vector<std::thread> th;
-  for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
-  work();
-  for (auto& x : th) x.join();
+  if (AmPool::on_worker() || !AmPool::get().run(work)) {
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; t++) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+  }
   if (first) std::rethrow_exception(first);
 }
 

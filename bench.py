@@ -60,52 +60,61 @@ def _oracle_sample(args):
     return n, time.perf_counter() - t0
 
 
+def _read(path):
+    with open(path) as f:
+        return f.read()
+
+
 def bind_numa(local):
     """Binds this rank (and the CPU-baseline workers it forks) to the CPUs of its GPU's NUMA node,
     before any GPU call: the pinned staging arenas (hipHostMallocNumaUser, am_capi.hip) are then
     placed on the socket the GPU hangs off. HIP device `local` is the local-th GPU node of the KFD
     topology (after ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES when they list indices); its PCI
-    address gives the node. Returns what it found (reported in the bench line), never fails."""
+    address gives the node (the DRM render node's device link when the topology is not readable).
+    Returns what it found (reported in the bench line), never fails."""
     info = {"gpu": local, "numa_node": None, "bound": False}
+    step = "kfd topology"
     try:
-        topo = "/sys/class/kfd/kfd/topology/nodes"
-        gpus = []
-        for n in sorted(os.listdir(topo), key=int):
-            props = {}
-            with open(os.path.join(topo, n, "properties")) as f:
-                for ln in f:
-                    k, _, v = ln.partition(" ")
-                    props[k] = v.strip()
-            if int(props.get("simd_count", "0")) > 0:
-                gpus.append(props)
-        idx = local
-        for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
-            vis = os.environ.get(var)
-            if vis:
-                ids = [x for x in vis.split(",") if x.strip()]
-                if not all(x.strip().isdigit() for x in ids):
-                    return dict(info, why="%s names devices by id" % var)
-                idx = int(ids[idx])
-        g = gpus[idx]
-        loc, dom = int(g["location_id"]), int(g.get("domain", "0"))
-        bdf = "%04x:%02x:%02x.%x" % (dom, loc >> 8, (loc >> 3) & 31, loc & 7)
+        bdf = None
+        try:
+            topo = "/sys/class/kfd/kfd/topology/nodes"
+            gpus = []
+            for n in sorted(os.listdir(topo), key=int):
+                props = dict(ln.split(" ", 1) for ln in _read(os.path.join(topo, n, "properties")).splitlines() if " " in ln)
+                if int(props.get("simd_count", "0")) > 0:
+                    gpus.append(props)
+            idx = local
+            for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+                vis = os.environ.get(var)
+                if vis and all(x.strip().isdigit() for x in vis.split(",") if x.strip()):
+                    idx = int([x for x in vis.split(",") if x.strip()][idx])
+            loc, dom = int(gpus[idx]["location_id"]), int(gpus[idx].get("domain", "0"))
+            bdf = "%04x:%02x:%02x.%x" % (dom, loc >> 8, (loc >> 3) & 31, loc & 7)
+        except (OSError, ValueError, KeyError, IndexError) as e:
+            info["kfd"] = "%s: %s" % (type(e).__name__, e)
+        if bdf is None:
+            # the render nodes the process can open, in minor order (one GPU per box: the visible one)
+            step = "render nodes"
+            rn = sorted((int(d[7:]), d) for d in os.listdir("/dev/dri") if d.startswith("renderD"))
+            bdf = os.path.basename(os.path.realpath("/sys/class/drm/%s/device" % rn[local][1]))
         info["pci"] = bdf
-        with open("/sys/bus/pci/devices/%s/numa_node" % bdf) as f:
-            node = int(f.read())
+        step = "pci numa_node"
+        node = int(_read("/sys/bus/pci/devices/%s/numa_node" % bdf))
         info["numa_node"] = node
         if node < 0:
             return info
+        step = "node cpulist"
         cpus = set()
-        with open("/sys/devices/system/node/node%d/cpulist" % node) as f:
-            for part in f.read().strip().split(","):
-                a, _, b = part.partition("-")
-                cpus.update(range(int(a), int(b or a) + 1))
+        for part in _read("/sys/devices/system/node/node%d/cpulist" % node).strip().split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
         mine = cpus & os.sched_getaffinity(0)
+        step = "sched_setaffinity"
         if mine:
             os.sched_setaffinity(0, mine)
             info.update(bound=True, cpus=len(mine))
     except (OSError, ValueError, KeyError, IndexError) as e:
-        info["why"] = "%s: %s" % (type(e).__name__, e)
+        info["why"] = "%s: %s: %s" % (step, type(e).__name__, e)
     return info
 
 

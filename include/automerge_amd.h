@@ -69,6 +69,7 @@ enum am_status {
   AM_E_UNKNOWN_COUNTER = 32,// increment operation %a0@%s for unknown counter (getPatch)
   AM_E_HISTORY = 33,        // RangeError of decodeDocument / groupChangeOps / decodeDocumentChanges (message as given)
   AM_E_LOCAL = 34,          // error of encodeChange / applyLocalChange / the sync functions (class + message as given)
+  AM_E_INFLATE = 35,        // invalid deflate data (a DEFLATEd document column, inflateColumn columnar.js:1062)
   AM_U_HASH_GRAPH = 100,    // needs the deferred hash graph of a loaded document (new.js:1826-1832)
   AM_U_UNKNOWN_COLUMN,      // column id outside DOC_OPS_COLUMNS / CHANGE_COLUMNS (new.js:1387-1425)
   AM_U_NONCAUSAL,           // opId counters violate Lamport order (insert after a later element, ...)
@@ -89,6 +90,7 @@ typedef struct am_chunk_desc {      // one binary chunk in the input arena
                             // bit1: AM_CHUNK_RAW -- not a container: a document's objectMeta blob
 } am_chunk_desc;
 #define AM_CHUNK_RAW 2u
+#define AM_CHUNK_BADZ 4u          /* internal (set by the batch stage): a DEFLATEd column does not inflate */
 typedef struct am_doc_desc {
   int64_t base_chunk;       // chunk index of the base document, -1 for Backend.init()
   uint32_t chg_begin, chg_count;   // change chunks [chg_begin, chg_begin + chg_count)

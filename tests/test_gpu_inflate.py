@@ -132,3 +132,101 @@ def test_stage_documents_batch_equals_per_document_stage():
     assert N.C.string_at(outs[0], olens[0]) == one[0][0] and N.C.string_at(outs[2], olens[2]) == one[2][0]
     for i in (0, 2):
         N.lib.am_free(outs[i])
+
+
+def _first_deflated_column(chunk):
+    """Offset of the first data byte of the first DEFLATEd column of a saved document chunk
+    (decodeDocumentHeader, columnar.js:1006-1038)."""
+    pos = [9]
+
+    def u():
+        v = sh = 0
+        while True:
+            b = chunk[pos[0]]
+            pos[0] += 1
+            v |= (b & 0x7F) << sh
+            sh += 7
+            if not b & 0x80:
+                return v
+    u()  # chunk length
+    for _ in range(u()):  # actors
+        n = u()
+        pos[0] += n
+    n = u()  # heads
+    pos[0] += 32 * n
+    cols = []
+    for _ in range(2):
+        for _ in range(u()):
+            cols.append((u(), u()))
+    at = pos[0]
+    for cid, n in cols:
+        if cid & 8 and n:
+            return at
+        at += n
+    raise AssertionError("no DEFLATEd column")
+
+
+def _rechecksum(chunk):
+    """A container chunk with its checksum recomputed (columnar.js:659-686: SHA-256 of the bytes after
+    the checksum, first 4 bytes)."""
+    import hashlib
+    c = bytearray(chunk)
+    c[4:8] = hashlib.sha256(bytes(c[8:])).digest()[:4]
+    return bytes(c)
+
+
+def test_deflated_documents_load_in_the_batch_stage():
+    """Saved documents with DEFLATEd columns (columnar.js:1052-1059) go into a batch as they are:
+    the stage checks their checksum on the GPU and rebuilds them with every column inflated
+    (inflateColumn, columnar.js:1062-1068), so Backend.load + applyChanges needs no host staging.
+    Merged bytes and heads equal the oracle's and the host-staged path's; a wrong checksum fails its
+    document with the checksum error, a column that does not inflate with AM_E_INFLATE."""
+    import oracle_ffi as O
+    import workload as W
+    from automerge_amd import _native as N
+    from automerge_amd.batch import Batch
+    arena, chunks, docs, _ = W.text(11, 8, 60, 40, 4)
+    items = []
+    for i in range(len(docs)):
+        _, chg = W.doc_chunks(arena, chunks, docs, i)
+        d = O.Doc.init()
+        d.apply(chg[:30])
+        items.append((d.save(), chg[30:]))
+    hs = [N.stage_document(s) for s, _ in items]  # the host stage: (chunk, checksum verified)
+    staged = [h[0] for h in hs]
+    assert sum(1 for (s, _), t in zip(items, staged) if s != t) >= len(docs) - 1  # DEFLATEd columns
+    # a wrong checksum; a column that does not inflate (valid checksum)
+    bad_sum = bytearray(items[2][0])
+    bad_sum[5] ^= 0xFF
+    raw = bytearray(items[3][0])
+    raw[_first_deflated_column(raw)] = 0x07  # BFINAL + reserved block type 3: never a valid stream
+    bad_z = _rechecksum(raw)
+    cases = items + [(bytes(bad_sum), items[2][1]), (bad_z, items[3][1])]
+    b = Batch()
+    b.stage_docs(cases)
+    ninf, _, _ = b.inflate_info()
+    nzc = sum(1 for _, ch in cases for c in ch if c[8] == 2)
+    assert ninf > nzc + len(docs)  # compressed changes + the documents' DEFLATEd columns
+    b.run()
+    b.sync()
+    r = b.results()
+    from automerge_amd.batch import pack
+    ra, rc, rd = pack([(t, ch) for t, (_, ch) in zip(staged, items)])
+    rc["flags"][rd["base_chunk"].astype(int)] = [1 if h[1] else 0 for h in hs]  # host-staged: checksum verified
+    ref = Batch()
+    ref.stage(ra, rc, rd)
+    ref.run()
+    ref.sync()
+    rr = ref.results()
+    for i, (s, ch) in enumerate(items):
+        assert int(r[i]["status"]) == 0, (i, int(r[i]["status"]))
+        want = O.Doc.load(s)
+        want.apply(ch)
+        assert b.doc_save(i) == want.save() == ref.doc_save(i), i
+        assert b.doc_heads(i, int(r[i]["nheads"])) == want.heads(), i
+        assert int(rr[i]["status"]) == 0
+    AM_E_CHECKSUM, AM_E_INFLATE = 2, 35
+    assert int(r[len(items)]["status"]) == AM_E_CHECKSUM
+    assert int(r[len(items) + 1]["status"]) == AM_E_INFLATE
+    with pytest.raises(N.AutomergeError, match="invalid deflate data"):
+        N.stage_document(bad_z)
