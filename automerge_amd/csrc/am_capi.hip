@@ -373,6 +373,10 @@ struct InflateScratch {
   DevBuf<am_chunk_desc> d_sha;
   DevBuf<uint8_t> d_hash, d_arena, d_blob;  // d_arena: the rebuilt arena; swapped with the batch's
   DevBuf<am_seg> d_seg;
+  // the device-side stage (inflate_stage_dev)
+  DevBuf<uint8_t> d_isbase;
+  DevBuf<uint64_t> d_cnt, d_z0, d_csrc, d_tmp, d_tot;
+  DevBuf<uint32_t> d_clen, d_zid;
 };
 
 struct am_batch {
@@ -407,6 +411,7 @@ struct am_batch {
   bool timed = false;
   uint32_t inflated = 0;      // change chunks inflated on the GPU by the last stage
   float inflate_ms = 0.f;     // their two inflate passes (HIP events)
+  bool inflate_ev = false;    // inflate_ms still to be read from the events (device-side stage)
   uint64_t inflated_bytes = 0;
 
   BatchDev dev() {
@@ -504,6 +509,72 @@ static bool doc_layout(const uint8_t* p, uint64_t n, DocLayout& L) {
   return r.ok;
 }
 
+// The device-side form of the stage below for a batch whose compressed chunks are all changes (no
+// saved document with DEFLATEd columns): the same classification, stream table, layout and
+// headers, computed by kernels over the chunks (am_launch_zstage_*), so the host reads no chunk
+// byte and waits twice for a total (the streams, the new arena's size). AM_ZSTAGE_DEV=0 keeps the
+// host form; batches under AM_ZSTAGE_DEV_MIN chunks (default 1024) use it too.
+static bool zstage_dev_on(uint32_t nchunks) {
+  const char* e = std::getenv("AM_ZSTAGE_DEV");
+  if (e && e[0] == '0') return false;
+  const char* m = std::getenv("AM_ZSTAGE_DEV_MIN");
+  return nchunks >= (m ? (uint32_t)std::strtoul(m, nullptr, 10) : 1024u);
+}
+static bool inflate_stage_dev(am_batch* b, uint64_t arena_len, uint32_t nchunks, uint32_t ndocs, HostClock& clk) {
+  InflateScratch& X = *b->zscr;
+  hipStream_t s = b->eng->stream;
+  if (!X.d_isbase.ensure(nchunks) || !X.d_cnt.ensure(nchunks) || !X.d_z0.ensure(nchunks) || !X.d_csrc.ensure(nchunks) ||
+      !X.d_clen.ensure(nchunks) || !X.d_zid.ensure(nchunks) || !X.d_tmp.ensure(am_scan_tmp_elems(nchunks)) || !X.d_tot.ensure(1))
+    return false;
+  am_launch_zstage_classify(b->arena.p, arena_len, b->chunks.p, nchunks, b->docs.p, ndocs, X.d_isbase.p, X.d_cnt.p,
+                            X.d_csrc.p, X.d_clen.p, s);
+  am_launch_scan(X.d_cnt.p, X.d_z0.p, X.d_tmp.p, nchunks, X.d_tot.p, s);
+  uint64_t tot = 0;
+  HIPCHECK(hipMemcpyAsync(&tot, X.d_tot.p, sizeof tot, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  HIPCHECK(hipGetLastError());
+  const uint32_t nz = (uint32_t)tot, nlong = (uint32_t)(tot >> 32);
+  clk.mark("classify");
+  b->inflated = nz;
+  b->inflate_ms = 0.f;
+  b->inflate_ev = false;
+  if (!nz) {
+    clk.print("inflate_stage_dev", nchunks);
+    return true;
+  }
+  if (!X.d_zs.ensure(nz) || !X.d_zlen.ensure(nz) || !X.d_ord.ensure(nz)) return false;
+  am_launch_zstage_fill(X.d_cnt.p, X.d_z0.p, nchunks, nlong, X.d_csrc.p, X.d_clen.p, X.d_zs.p, X.d_ord.p, X.d_zid.p, s);
+  (void)hipEventRecord(b->eng->ev[0], s);
+  am_launch_inflate_size(b->arena.p, X.d_zs.p, X.d_ord.p, nlong, nz, X.d_zlen.p, s);
+  (void)hipEventRecord(b->eng->ev[1], s);
+  // new lengths (d_cnt) -> new offsets (d_z0)
+  am_launch_zstage_layout(b->arena.p, b->chunks.p, nchunks, X.d_zid.p, X.d_zlen.p, X.d_zs.p, X.d_cnt.p, s);
+  am_launch_scan(X.d_cnt.p, X.d_z0.p, X.d_tmp.p, nchunks, X.d_tot.p, s);
+  HIPCHECK(hipMemcpyAsync(&tot, X.d_tot.p, sizeof tot, hipMemcpyDeviceToHost, s));
+  HIPCHECK(hipStreamSynchronize(s));
+  HIPCHECK(hipGetLastError());
+  const uint64_t off = tot;
+  clk.mark("size+layout");
+  DevBuf<uint8_t>& d_arena = X.d_arena;
+  if (!d_arena.ensure(off + 64)) return false;
+  HIPCHECK(hipMemsetAsync(d_arena.p + off, 0, 64, s));
+  (void)hipEventRecord(b->eng->ev[2], s);
+  am_launch_zstage_place(b->chunks.p, nchunks, b->arena.p, X.d_zid.p, X.d_zlen.p, X.d_zs.p, X.d_z0.p, X.d_cnt.p, d_arena.p, s);
+  am_launch_inflate_write(b->arena.p, X.d_zs.p, X.d_ord.p, nlong, nz, X.d_zlen.p, d_arena.p, s);
+  (void)hipEventRecord(b->eng->ev[3], s);
+  HIPCHECK(hipGetLastError());
+  clk.mark("queued");
+  char m[48];
+  std::snprintf(m, sizeof m, " streams=%u long=%u", nz, nlong);
+  clk.line += m;
+  clk.print("inflate_stage_dev", nchunks);
+  b->inflate_ev = true;  // read after the stage's next synchronisation
+  b->inflated_bytes = off;
+  std::swap(b->arena.p, d_arena.p);
+  std::swap(b->arena.cap, d_arena.cap);
+  return true;
+}
+
 // DEFLATE on the GPU in the batch stage (am_inflate.hip), so compressed inputs need no host staging:
 //  * compressed change chunks (type 2, columnar.js:742/784 -> inflateChange :813): re-wrapped as
 //    magic + the ORIGINAL checksum + type 1 + uleb(length) + inflated data (k_chunks then verifies
@@ -520,10 +591,13 @@ static bool doc_layout(const uint8_t* p, uint64_t n, DocLayout& L) {
 static bool inflate_stage(am_batch* b, const uint8_t* arena, uint64_t arena_len, const am_chunk_desc* chunks,
                           uint32_t nchunks, const am_doc_desc* docs, uint32_t ndocs) {
   HostClock clk;
+  b->inflate_ev = false;
   if (!b->zscr) b->zscr.reset(new InflateScratch());
   InflateScratch& X = *b->zscr;
-  // per chunk: 0 as it is, 1 compressed change, 2 document with DEFLATEd columns (base chunks first,
-  // in parallel over the documents; then every other chunk, in parallel over the chunks)
+  // per chunk: 0 as it is, 1 compressed change, 2 document with DEFLATEd columns, 4 a base chunk
+  // as it is -- never taken for a compressed change: decodeDocumentHeader rejects its type before
+  // anything inflates it (columnar.js:1011) -- (base chunks first, in parallel over the documents;
+  // then every other chunk, in parallel over the chunks)
   std::vector<uint8_t>& kind = X.kind;
   std::vector<uint32_t>& nzs = X.nzs;  // streams of chunk c
   std::vector<uint32_t>& dat = X.dat;  // kind 2: the document (index into lay)
@@ -558,10 +632,15 @@ static bool inflate_stage(am_batch* b, const uint8_t* arena, uint64_t arena_len,
     nzs[c] = n;
     dat[c] = (uint32_t)d;
   });
-  // base chunks that are not staged go back to kind 0; staged ones to 2 (a base chunk shared by
-  // several documents is staged once, through its first document)
+  // base chunks that are not staged go to kind 4; staged ones to 2 (a base chunk shared by several
+  // documents is staged once, through its first document)
+  bool doc_z = false;
   for (uint32_t d = 0; d < ndocs; d++)
-    if (base_of[d] >= 0 && kind[base_of[d]] == 3) kind[base_of[d]] = nzs[base_of[d]] ? 2 : 0;
+    if (base_of[d] >= 0 && kind[base_of[d]] == 3) {
+      kind[base_of[d]] = nzs[base_of[d]] ? 2 : 4;
+      doc_z |= kind[base_of[d]] == 2;
+    }
+  if (!doc_z && zstage_dev_on(nchunks)) return inflate_stage_dev(b, arena_len, nchunks, ndocs, clk);
   am_par_for(nchunks, [&](size_t c) {
     if (kind[c] || !container_ok((uint32_t)c)) return;
     const uint8_t* p = arena + chunks[c].off;
@@ -847,6 +926,13 @@ static bool stage_impl(am_batch* b, const uint8_t* arena, uint64_t arena_len, co
   if (ndocs) HIPCHECK(hipMemcpyAsync(&saved, b->max_hot.p + 2, sizeof saved, hipMemcpyDeviceToHost, s));
   HIPCHECK(hipStreamSynchronize(s));
   HIPCHECK(hipGetLastError());
+  if (b->inflate_ev) {
+    float ms1 = 0.f, ms2 = 0.f;
+    (void)hipEventElapsedTime(&ms1, e->ev[0], e->ev[1]);
+    (void)hipEventElapsedTime(&ms2, e->ev[2], e->ev[3]);
+    b->inflate_ms = ms1 + ms2;
+    b->inflate_ev = false;
+  }
   clk.mark("sizing");
   clk.print("stage", ndocs);
   // a batch reserves the whole plan of every compact document as overflow, so none of them can
@@ -1881,6 +1967,8 @@ bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified,
   }
   am_batch* b = scratch_batch(e);
   am_error ce;
+  HostClock clk;
+  clk.mark("pack");
   for (;;) {
     if (am_batch_stage(b, arena.data(), arena.size(), cds.data(), (uint32_t)cds.size(), &dd, 1, known.data(),
                        (uint32_t)known.size(), &ce) ||
@@ -1891,6 +1979,15 @@ bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified,
     // invalid UTF-8 in a key or message: run again with room for the U+FFFD replacements
     if (res.r.status != AM_U_UTF8 || (dd.flags & AM_DOC_FIX_UTF8)) break;
     dd.flags |= AM_DOC_FIX_UTF8;
+  }
+  clk.mark("stage+run+sync");
+  if (clk.on) {
+    float t[4] = {0, 0, 0, 0};
+    am_batch_stage_times(b, t);
+    char m[160];
+    std::snprintf(m, sizeof m, " [k_chunks=%.2f bounds=%.2f doc=%.2f out_hash=%.2f ms; arena=%zu B]", t[0], t[1], t[2], t[3],
+                  arena.size());
+    clk.line += m;
   }
   {
     uint8_t f = 0;
@@ -1939,6 +2036,8 @@ bool run_one(am_engine* e, const std::vector<uint8_t>* base, bool base_verified,
     }
     split_meta(res);
   }
+  clk.mark("results-home");
+  clk.print("run_one", arena.size());
   return true;
 }
 
@@ -2460,9 +2559,11 @@ static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* le
       known.push_back(k);
     }
   };
+  HostClock clk;
   fill_known();
   OneResult res;
   std::vector<uint8_t> arena;
+  clk.mark("prep");
   if (!run_one(d->eng, d->state.empty() ? nullptr : &d->state, true, staged, known, d->have_hash_graph, res, arena, e, pmode,
                0, meta)) {
     // a loaded document without its hash graph: compute it and run again (new.js:1826-1832)
@@ -2486,7 +2587,11 @@ static int apply_changes(am_doc* d, const uint8_t* const* bufs, const size_t* le
       return 1;
     }
   }
-  return apply_finish(d, orig, track, res, patch, err);
+  clk.mark("run_one");
+  const int rc = apply_finish(d, orig, track, res, patch, err);
+  clk.mark("finish");
+  clk.print("apply_changes", d->state.size());
+  return rc;
 }
 
 // The end of an applyChanges call whose GPU run succeeded: the patch's errors (an error in it throws

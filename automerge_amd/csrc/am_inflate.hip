@@ -82,7 +82,134 @@ __global__ __launch_bounds__(256) void k_copy_segs(const uint8_t* __restrict__ s
   for (uint32_t q = threadIdx.x; q < g.len; q += blockDim.x) dp[q] = sp[q];
 }
 
+// ---- device-side stage of compressed change chunks (see am_launch.h) ----
+constexpr uint32_t kLongZ = 1024;  // long streams: >= 1 KiB compressed (am_inflate_order)
+constexpr uint32_t kZFail = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(256) void k_zmark_bases(const am_doc_desc* __restrict__ docs, uint32_t ndocs, uint32_t nchunks,
+                                                     uint8_t* __restrict__ isbase) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= ndocs) return;
+  const int64_t c = docs[d].base_chunk;
+  if (c >= 0 && (uint64_t)c < nchunks) isbase[c] = 1;  // a base chunk is never a compressed change
+}
+// unsigned LEB128 as the host stage reads a container length (HRd::u): false when the bytes run out
+__device__ __forceinline__ bool z_uleb(const uint8_t* p, uint64_t n, uint64_t& off, uint64_t& v) {
+  v = 0;
+  int sh = 0;
+  while (off < n) {
+    const uint8_t b = p[off++];
+    if (sh < 64) v |= (uint64_t)(b & 0x7f) << sh;
+    sh += 7;
+    if (!(b & 0x80)) return true;
+  }
+  return false;
+}
+// a compressed change: a container (magic, > 9 bytes, inside the arena) of type 2 whose data fits
+__global__ __launch_bounds__(256) void k_zclass(const uint8_t* __restrict__ arena, uint64_t arena_len,
+                                                const am_chunk_desc* __restrict__ chunks, uint32_t nchunks,
+                                                const uint8_t* __restrict__ isbase, uint64_t* __restrict__ cnt,
+                                                uint64_t* __restrict__ csrc, uint32_t* __restrict__ clen) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nchunks) return;
+  const am_chunk_desc k = chunks[c];
+  uint64_t out = 0;
+  if (!isbase[c] && !(k.flags & AM_CHUNK_RAW) && k.len > 9 && k.off + k.len <= arena_len) {
+    const uint8_t* p = arena + k.off;
+    if (p[0] == 0x85 && p[1] == 0x6f && p[2] == 0x4a && p[3] == 0x83 && p[8] == 2) {
+      uint64_t off = 9, dl = 0;
+      if (z_uleb(p, k.len, off, dl) && dl <= k.len - off) {
+        csrc[c] = k.off + off;
+        clen[c] = (uint32_t)dl;
+        out = (dl >= kLongZ ? (1ull << 32) : 0ull) | 1ull;
+      }
+    }
+  }
+  cnt[c] = out;
+}
+__global__ __launch_bounds__(256) void k_zfill(const uint64_t* __restrict__ cnt, const uint64_t* __restrict__ z0, uint32_t nchunks,
+                                               uint32_t nlong, const uint64_t* __restrict__ csrc, const uint32_t* __restrict__ clen,
+                                               am_zstream* __restrict__ zs, uint32_t* __restrict__ ord, uint32_t* __restrict__ zid) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nchunks) return;
+  const uint64_t k = cnt[c];
+  if (!k) { zid[c] = ~0u; return; }
+  const uint32_t z = (uint32_t)z0[c], lb = (uint32_t)(z0[c] >> 32);
+  am_zstream& o = zs[z];
+  o.src = csrc[c];
+  o.dst = ~0ull;
+  o.len = clen[c];
+  o.hlen = 0;
+  ord[(k >> 32) ? lb : nlong + (z - lb)] = z;
+  zid[c] = z;
+}
+__global__ __launch_bounds__(256) void k_zlayout(const uint8_t* __restrict__ arena, const am_chunk_desc* __restrict__ chunks,
+                                                 uint32_t nchunks, const uint32_t* __restrict__ zid, const uint32_t* __restrict__ zlen,
+                                                 am_zstream* __restrict__ zs, uint64_t* __restrict__ nl) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nchunks) return;
+  const am_chunk_desc k = chunks[c];
+  const uint32_t z = zid[c];
+  if (z == ~0u || zlen[z] == kZFail) { nl[c] = k.len; return; }
+  // the header travels with the stream: the original checksum, type 1, uleb(inflated length)
+  am_zstream& o = zs[z];
+  const uint8_t* p = arena + k.off;
+  o.hdr[0] = p[4]; o.hdr[1] = p[5]; o.hdr[2] = p[6]; o.hdr[3] = p[7];
+  o.hdr[4] = 1;
+  uint32_t q = 5;
+  for (uint32_t v = zlen[z];;) {
+    const uint8_t b = v & 0x7f;
+    v >>= 7;
+    o.hdr[q++] = b | (v ? 0x80 : 0);
+    if (!v) break;
+  }
+  o.hlen = (uint8_t)q;
+  nl[c] = 4ull + q + zlen[z];
+}
+// wave per chunk: its new descriptor, its stream's destination, or its bytes as they are
+__global__ __launch_bounds__(256) void k_zplace(am_chunk_desc* __restrict__ chunks, uint32_t nchunks, const uint8_t* __restrict__ arena,
+                                                const uint32_t* __restrict__ zid, const uint32_t* __restrict__ zlen,
+                                                am_zstream* __restrict__ zs, const uint64_t* __restrict__ noff,
+                                                const uint64_t* __restrict__ nl, uint8_t* __restrict__ dst) {
+  const uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  if (c >= nchunks) return;
+  const am_chunk_desc k = chunks[c];
+  const uint32_t z = zid[c];
+  const uint64_t at = noff[c];
+  if (z != ~0u && zlen[z] != kZFail) {
+    if (l == 0) zs[z].dst = at + 4 + zs[z].hlen;
+  } else {
+    const uint8_t* sp = arena + k.off;
+    uint8_t* dp = dst + at;
+    for (uint32_t q = l; q < k.len; q += 64) dp[q] = sp[q];
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (l == 0) chunks[c] = am_chunk_desc{at, (uint32_t)nl[c], k.flags};
+}
+
 }  // namespace
+
+void am_launch_zstage_classify(const uint8_t* arena, uint64_t arena_len, const am_chunk_desc* chunks, uint32_t nchunks,
+                               const am_doc_desc* docs, uint32_t ndocs, uint8_t* isbase, uint64_t* cnt, uint64_t* csrc,
+                               uint32_t* clen, hipStream_t s) {
+  if (!nchunks) return;
+  (void)hipMemsetAsync(isbase, 0, nchunks, s);
+  if (ndocs) k_zmark_bases<<<(ndocs + 255) / 256, 256, 0, s>>>(docs, ndocs, nchunks, isbase);
+  k_zclass<<<(nchunks + 255) / 256, 256, 0, s>>>(arena, arena_len, chunks, nchunks, isbase, cnt, csrc, clen);
+}
+void am_launch_zstage_fill(const uint64_t* cnt, const uint64_t* z0, uint32_t nchunks, uint32_t nlong, const uint64_t* csrc,
+                           const uint32_t* clen, am_zstream* zs, uint32_t* ord, uint32_t* zid, hipStream_t s) {
+  if (nchunks) k_zfill<<<(nchunks + 255) / 256, 256, 0, s>>>(cnt, z0, nchunks, nlong, csrc, clen, zs, ord, zid);
+}
+void am_launch_zstage_layout(const uint8_t* arena, const am_chunk_desc* chunks, uint32_t nchunks, const uint32_t* zid,
+                             const uint32_t* zlen, am_zstream* zs, uint64_t* nl, hipStream_t s) {
+  if (nchunks) k_zlayout<<<(nchunks + 255) / 256, 256, 0, s>>>(arena, chunks, nchunks, zid, zlen, zs, nl);
+}
+void am_launch_zstage_place(am_chunk_desc* chunks, uint32_t nchunks, const uint8_t* arena, const uint32_t* zid,
+                            const uint32_t* zlen, am_zstream* zs, const uint64_t* noff, const uint64_t* nl, uint8_t* dst,
+                            hipStream_t s) {
+  if (nchunks) k_zplace<<<(nchunks + 3) / 4, 256, 0, s>>>(chunks, nchunks, arena, zid, zlen, zs, noff, nl, dst);
+}
 
 static_assert(kLanes * kSliceFast * sizeof(uint16_t) <= 160 * 1024, "k_inflate LDS exceeds the gfx950 workgroup limit");
 // ord[0, nlong): the long streams (largest first) for the FAST form; ord[nlong, nz): the rest
@@ -107,7 +234,7 @@ void am_launch_inflate_write(const uint8_t* src, const am_zstream* zs, const uin
 // long streams (>= 1 KiB compressed) first, largest first, so each workgroup's lanes carry streams
 // of similar length and the longest start at once; then the others in their order
 uint32_t am_inflate_order(const am_zstream* zs, uint32_t nz, uint32_t* ord) {
-  constexpr uint32_t kLong = 1024;
+  constexpr uint32_t kLong = kLongZ;
   uint32_t k = 0;
   for (uint32_t i = 0; i < nz; i++)
     if (zs[i].len >= kLong) ord[k++] = i;

@@ -88,6 +88,24 @@ void am_launch_inflate_write(const uint8_t* src, const am_zstream* zs, const uin
 // the launch order of am_launch_inflate_*; returns nlong
 uint32_t am_inflate_order(const am_zstream* zs, uint32_t nz, uint32_t* ord);
 void am_launch_copy_segs(const uint8_t* src, const uint8_t* blob, const am_seg* segs, uint32_t n, uint8_t* dst, hipStream_t s);
+// The device-side stage of a batch whose compressed chunks are all changes (no DEFLATEd base
+// document): the classification, stream table, layout and header rewrite of inflate_stage's host
+// code as kernels over the chunks.
+//  classify: cnt[c] = 0, or (long << 32 | 1) for a compressed change (csrc / clen: its stream)
+//  fill:     z0 = exclusive scan of cnt, nlong = its long total: the stream table, the launch order
+//            (long streams first) and zid[c] (the chunk's stream, or ~0u)
+//  layout:   nl[c] = the chunk's new length; the headers of the inflated chunks into zs
+//  place:    new descriptors in place, the streams' destinations, every other chunk copied to dst
+void am_launch_zstage_classify(const uint8_t* arena, uint64_t arena_len, const am_chunk_desc* chunks, uint32_t nchunks,
+                               const am_doc_desc* docs, uint32_t ndocs, uint8_t* isbase, uint64_t* cnt, uint64_t* csrc,
+                               uint32_t* clen, hipStream_t s);
+void am_launch_zstage_fill(const uint64_t* cnt, const uint64_t* z0, uint32_t nchunks, uint32_t nlong, const uint64_t* csrc,
+                           const uint32_t* clen, am_zstream* zs, uint32_t* ord, uint32_t* zid, hipStream_t s);
+void am_launch_zstage_layout(const uint8_t* arena, const am_chunk_desc* chunks, uint32_t nchunks, const uint32_t* zid,
+                             const uint32_t* zlen, am_zstream* zs, uint64_t* nl, hipStream_t s);
+void am_launch_zstage_place(am_chunk_desc* chunks, uint32_t nchunks, const uint8_t* arena, const uint32_t* zid,
+                            const uint32_t* zlen, am_zstream* zs, const uint64_t* noff, const uint64_t* nl, uint8_t* dst,
+                            hipStream_t s);
 
 // engine internals shared with am_sync.hip
 struct am_engine;

@@ -230,3 +230,69 @@ def test_deflated_documents_load_in_the_batch_stage():
     assert int(r[len(items) + 1]["status"]) == AM_E_INFLATE
     with pytest.raises(N.AutomergeError, match="invalid deflate data"):
         N.stage_document(bad_z)
+
+
+def _stage_both_forms(arena, chunks, docs):
+    """Stages and runs one batch with the host form of the inflate stage and again with its
+    device-side form (AM_ZSTAGE_DEV, AM_ZSTAGE_DEV_MIN are read per stage)."""
+    import os
+    from automerge_amd.batch import Batch
+    out = []
+    for dev in ("0", "1"):
+        keep = {k: os.environ.get(k) for k in ("AM_ZSTAGE_DEV", "AM_ZSTAGE_DEV_MIN")}
+        os.environ["AM_ZSTAGE_DEV"] = dev
+        os.environ["AM_ZSTAGE_DEV_MIN"] = "0"
+        try:
+            b = Batch()
+            b.stage(arena, chunks, docs)
+            ninf, nbytes, _ = b.inflate_info()
+            b.run()
+            b.sync()
+            r = b.results()
+            h, st, cs = b.chunk_results()
+            docs_out = [b.doc_output(i, r[i]) if int(r[i]["status"]) == 0 else None for i in range(len(docs))]
+            out.append(((ninf, nbytes), r, h, st, cs, docs_out))
+        finally:
+            for k, v in keep.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    return out
+
+
+def test_device_side_stage_equals_host_stage():
+    """A batch whose compressed chunks are all changes is staged by kernels (inflate_stage_dev:
+    classification, stream table, layout and the re-wrapped headers on the device). It must stage
+    exactly what the host form does -- inflated counts and bytes, every document's status and merged
+    bytes, every chunk's hash, state and status -- including base documents (never a compressed
+    change), a corrupted and a truncated compressed change, and a compressed change given as a base."""
+    import oracle_ffi as O
+    import workload as W
+    from automerge_amd.batch import pack
+    arena, chunks, docs, _ = W.text(11, 8, 40, 50, 4)
+    items = [W.doc_chunks(arena, chunks, docs, i) for i in range(len(docs))]
+    a4, c4, d4, _ = W.c4(3, 6)
+    items += [W.doc_chunks(a4, c4, d4, i) for i in range(len(d4))]
+    zi = [k for k, c in enumerate(items[0][1]) if c[8] == 2]
+    assert len(zi) >= 3
+    bad = [bytearray(c) for c in items[0][1]]
+    mid = len(bad[zi[1]]) // 2
+    for q in range(mid, mid + 6):
+        bad[zi[1]][q] ^= 0x5A  # DEFLATE data corrupted
+    items.append((None, [bytes(c) for c in bad]))
+    trunc = list(items[1][1])
+    z1 = [k for k, c in enumerate(trunc) if c[8] == 2][0]
+    trunc[z1] = trunc[z1][:-3]  # the container's data runs past the chunk
+    items.append((None, trunc))
+    items.append((items[0][1][zi[0]], []))  # a compressed change as the base document
+    arena2, chunks2, docs2 = pack(items)
+    host, dev = _stage_both_forms(arena2, chunks2, docs2)
+    assert host[0] == dev[0] and host[0][0] > 200
+    for f in ("status", "err_change", "arg0", "arg1", "out_len", "nheads", "napplied", "nchanges", "max_op"):
+        assert (host[1][f] == dev[1][f]).all(), f
+    for k in (2, 3, 4):
+        assert (host[k] == dev[k]).all(), k
+    assert host[5] == dev[5]
+    st = host[1]["status"]
+    assert (st[:len(items) - 3] == 0).all() and (st[-3:] != 0).all(), st
