@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "am_common.h"
 #include "am_launch.h"
@@ -36,13 +37,14 @@ using namespace amz;
 
 // pass 1: zlen[s] = inflated length of raw DEFLATE stream s = ord[i], or 0xFFFFFFFF when it does not
 // inflate. FAST: the long-stream form (one-lookup code tables, kSliceFast per lane)
+// spw: streams per workgroup (one wave): lanes [0, spw) decode one stream each
 template <bool FAST>
 __global__ __launch_bounds__(kLanes) void k_inflate_size(const uint8_t* __restrict__ src, const am_zstream* __restrict__ zs,
                                                          const uint32_t* __restrict__ ord, uint32_t nz,
-                                                         uint32_t* __restrict__ zlen) {
+                                                         uint32_t* __restrict__ zlen, uint32_t spw) {
   extern __shared__ uint16_t lds_inf[];
-  const uint32_t i = blockIdx.x * kLanes + threadIdx.x;
-  if (i >= nz) return;
+  const uint32_t i = blockIdx.x * spw + threadIdx.x;
+  if (threadIdx.x >= spw || i >= nz) return;
   const uint32_t s = ord[i];
   const am_zstream z = zs[s];
   const int64_t n =
@@ -54,10 +56,11 @@ __global__ __launch_bounds__(kLanes) void k_inflate_size(const uint8_t* __restri
 template <bool FAST>
 __global__ __launch_bounds__(kLanes) void k_inflate_write(const uint8_t* __restrict__ src, const am_zstream* __restrict__ zs,
                                                           const uint32_t* __restrict__ ord, uint32_t nz,
-                                                          const uint32_t* __restrict__ zlen, uint8_t* __restrict__ dst) {
+                                                          const uint32_t* __restrict__ zlen, uint8_t* __restrict__ dst,
+                                                          uint32_t spw) {
   extern __shared__ uint16_t lds_inf[];
-  const uint32_t i = blockIdx.x * kLanes + threadIdx.x;
-  if (i >= nz) return;
+  const uint32_t i = blockIdx.x * spw + threadIdx.x;
+  if (threadIdx.x >= spw || i >= nz) return;
   const uint32_t s = ord[i];
   if (zlen[s] == 0xFFFFFFFFu) return;
   const am_zstream z = zs[s];
@@ -212,24 +215,36 @@ void am_launch_zstage_place(am_chunk_desc* chunks, uint32_t nchunks, const uint8
 }
 
 static_assert(kLanes * kSliceFast * sizeof(uint16_t) <= 160 * 1024, "k_inflate LDS exceeds the gfx950 workgroup limit");
-// ord[0, nlong): the long streams (largest first) for the FAST form; ord[nlong, nz): the rest
+// ord[0, nlong): the long streams (largest first) for the FAST form; ord[nlong, nz): the rest.
+// A long stream decodes in a wave of its own (AM_INFLATE_LONG_SPW streams per wave, default 1): its
+// lane's dependent chain then runs without the other lanes' divergent paths, and many such waves
+// per SIMD overlap their chains (64 long streams per wave held a CU's whole LDS for one wave); the
+// short streams keep 64 per wave.
+static uint32_t long_spw() {
+  const char* e = std::getenv("AM_INFLATE_LONG_SPW");
+  const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1u;
+  return v >= 1 && v <= (uint32_t)kLanes ? v : 1u;
+}
 void am_launch_inflate_size(const uint8_t* src, const am_zstream* zs, const uint32_t* ord, uint32_t nlong, uint32_t nz,
                             uint32_t* zlen, hipStream_t s) {
-  if (nlong)
-    k_inflate_size<true><<<(nlong + kLanes - 1) / kLanes, kLanes, kLanes * kSliceFast * sizeof(uint16_t), s>>>(src, zs, ord, nlong,
-                                                                                                             zlen);
+  if (nlong) {
+    const uint32_t spw = long_spw();
+    k_inflate_size<true><<<(nlong + spw - 1) / spw, kLanes, spw * kSliceFast * sizeof(uint16_t), s>>>(src, zs, ord, nlong, zlen, spw);
+  }
   if (nz > nlong)
     k_inflate_size<false><<<(nz - nlong + kLanes - 1) / kLanes, kLanes, kLanes * kSlice * sizeof(uint16_t), s>>>(
-        src, zs, ord + nlong, nz - nlong, zlen);
+        src, zs, ord + nlong, nz - nlong, zlen, (uint32_t)kLanes);
 }
 void am_launch_inflate_write(const uint8_t* src, const am_zstream* zs, const uint32_t* ord, uint32_t nlong, uint32_t nz,
                              const uint32_t* zlen, uint8_t* dst, hipStream_t s) {
-  if (nlong)
-    k_inflate_write<true><<<(nlong + kLanes - 1) / kLanes, kLanes, kLanes * kSliceFast * sizeof(uint16_t), s>>>(src, zs, ord, nlong,
-                                                                                                              zlen, dst);
+  if (nlong) {
+    const uint32_t spw = long_spw();
+    k_inflate_write<true><<<(nlong + spw - 1) / spw, kLanes, spw * kSliceFast * sizeof(uint16_t), s>>>(src, zs, ord, nlong, zlen,
+                                                                                                      dst, spw);
+  }
   if (nz > nlong)
     k_inflate_write<false><<<(nz - nlong + kLanes - 1) / kLanes, kLanes, kLanes * kSlice * sizeof(uint16_t), s>>>(
-        src, zs, ord + nlong, nz - nlong, zlen, dst);
+        src, zs, ord + nlong, nz - nlong, zlen, dst, (uint32_t)kLanes);
 }
 // long streams (>= 1 KiB compressed) first, largest first, so each workgroup's lanes carry streams
 // of similar length and the longest start at once; then the others in their order

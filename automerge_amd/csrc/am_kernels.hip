@@ -383,46 +383,35 @@ __device__ __forceinline__ void chunk_body(const uint8_t* p, const am_chunk_desc
 #define KC_STAGE 12288  // bytes of LDS per wave for its 64 chunks
 #define KC_BIG 16384     // a document chunk this large has its columns counted by the whole wave
 
-// ---- wave-cooperative counting of a large document's columns: every lane runs the same parse
-// over a window of the chunk in the wave's LDS slice, refilled with 16-byte loads of all 64 lanes
-// when the parse leaves it, so the long dependent chain of LEB128 reads hits LDS instead of global
-// memory. Same results and status codes as rle_count_sum (the LEB readers mirror leb_u64 /
-// leb_i64 / rd_u53 / rd_i53). ----
-#define KC_WIN 8192
-struct WinRd {
-  const uint8_t* g;  // chunk start (global)
-  uint8_t* win;      // the wave's LDS window
-  uint64_t lim;      // readable bytes from g (chunk length)
-  uint64_t wb;       // window start (offset from g); ~0: empty
+// ---- counting of a large document's columns (k_chunks): the column parse of rle_count_sum with
+// the LEB readers of leb_u64 / leb_i64 / rd_u53 / rd_i53 (same results and status codes) over a
+// byte reader, one lane per column. ----
+// One lane's reader over global memory with a 16-byte line in registers (arena-aligned loads: the
+// arena is 16-aligned and carries >= 16 bytes of slack past its last chunk): each lane counts a
+// column of its own, so a large document's columns are counted side by side
+struct LineRd {
+  const uint8_t* arena;
+  uint64_t goff;  // chunk start (arena offset)
+  uint64_t line;  // arena offset of the line held; ~0: none
+  uint4 buf;
 };
-__device__ __forceinline__ uint8_t win_byte(WinRd& w, uint64_t k) {
-  if (k < w.wb || k >= w.wb + KC_WIN) {  // wave-uniform: every lane parses the same bytes
-    const uint64_t nb = k & ~(uint64_t)15;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t l = threadIdx.x & 63;
-    for (uint32_t q = 16 * l; q < KC_WIN; q += 1024) {
-      if (nb + q < w.lim) {
-        // 16 B per lane; the arena carries >= 16 bytes of slack past its last chunk
-        const uint8_t* src = w.g + nb + q;
-        uint32_t v[4];
-        for (int b = 0; b < 4; b++) v[b] = (uint32_t)src[4 * b] | (uint32_t)src[4 * b + 1] << 8 | (uint32_t)src[4 * b + 2] << 16 | (uint32_t)src[4 * b + 3] << 24;
-        uint32_t* d = reinterpret_cast<uint32_t*>(w.win + q);
-        d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    w.wb = nb;
+__device__ __forceinline__ uint8_t rd_byte(LineRd& r, uint64_t k) {
+  const uint64_t a = r.goff + k, la = a & ~15ull;
+  if (la != r.line) {
+    r.buf = *reinterpret_cast<const uint4*>(r.arena + la);
+    r.line = la;
   }
-  return w.win[k - w.wb];
+  const uint32_t q = (uint32_t)(a & 15);
+  const uint32_t w = q < 8 ? (q < 4 ? r.buf.x : r.buf.y) : (q < 12 ? r.buf.z : r.buf.w);
+  return (uint8_t)(w >> (8 * (q & 3)));
 }
 struct WinCur { uint64_t off, n; };  // a column: [off, off + n) of the chunk
-__device__ static uint32_t win_leb_u64(WinRd& w, WinCur& d, uint32_t& hi, uint32_t& lo) {
+template <class Rd_>
+__device__ static uint32_t win_leb_u64(Rd_& w, WinCur& d, uint32_t& hi, uint32_t& lo) {
   uint32_t low = 0, high = 0;
   int shift = 0;
   while (d.off < d.n && shift <= 28) {
-    const uint8_t b = win_byte(w, d.off);
+    const uint8_t b = rd_byte(w, d.off);
     low |= (uint32_t)(b & 0x7f) << shift;
     if (shift == 28) high = (b & 0x70) >> 4;
     shift += 7;
@@ -431,7 +420,7 @@ __device__ static uint32_t win_leb_u64(WinRd& w, WinCur& d, uint32_t& hi, uint32
   }
   shift = 3;
   while (d.off < d.n) {
-    const uint8_t b = win_byte(w, d.off);
+    const uint8_t b = rd_byte(w, d.off);
     if (shift == 31 && (b & 0xfe) != 0) return AM_E_LEB_RANGE;
     high |= (uint32_t)(b & 0x7f) << shift;
     shift += 7;
@@ -440,12 +429,13 @@ __device__ static uint32_t win_leb_u64(WinRd& w, WinCur& d, uint32_t& hi, uint32
   }
   return AM_E_LEB_INCOMPLETE;
 }
-__device__ static uint32_t win_leb_i64(WinRd& w, WinCur& d, int32_t& hi, uint32_t& lo) {
+template <class Rd_>
+__device__ static uint32_t win_leb_i64(Rd_& w, WinCur& d, int32_t& hi, uint32_t& lo) {
   uint32_t low = 0;
   int32_t high = 0;
   int shift = 0;
   while (d.off < d.n && shift <= 28) {
-    const uint8_t b = win_byte(w, d.off);
+    const uint8_t b = rd_byte(w, d.off);
     low |= (uint32_t)(b & 0x7f) << shift;
     if (shift == 28) high = (b & 0x70) >> 4;
     shift += 7;
@@ -462,7 +452,7 @@ __device__ static uint32_t win_leb_i64(WinRd& w, WinCur& d, int32_t& hi, uint32_
   }
   shift = 3;
   while (d.off < d.n) {
-    const uint8_t b = win_byte(w, d.off);
+    const uint8_t b = rd_byte(w, d.off);
     if (shift == 31 && b != 0 && b != 0x7f) return AM_E_LEB_RANGE;
     high |= (int32_t)((uint32_t)(b & 0x7f) << shift);
     shift += 7;
@@ -475,14 +465,16 @@ __device__ static uint32_t win_leb_i64(WinRd& w, WinCur& d, int32_t& hi, uint32_
   }
   return AM_E_LEB_INCOMPLETE;
 }
-__device__ __forceinline__ uint32_t win_u53(WinRd& w, WinCur& d, int64_t& v) {
+template <class Rd_>
+__device__ __forceinline__ uint32_t win_u53(Rd_& w, WinCur& d, int64_t& v) {
   uint32_t hi, lo;
   TRY(win_leb_u64(w, d, hi, lo));
   if (hi > 0x1fffff) return AM_E_LEB_RANGE;
   v = (int64_t)hi * 4294967296LL + lo;
   return AM_OK;
 }
-__device__ __forceinline__ uint32_t win_i53(WinRd& w, WinCur& d, int64_t& v) {
+template <class Rd_>
+__device__ __forceinline__ uint32_t win_i53(Rd_& w, WinCur& d, int64_t& v) {
   int32_t hi;
   uint32_t lo;
   TRY(win_leb_i64(w, d, hi, lo));
@@ -491,7 +483,8 @@ __device__ __forceinline__ uint32_t win_i53(WinRd& w, WinCur& d, int64_t& v) {
   return AM_OK;
 }
 // rle_count_sum over the window (same record rules, same errors)
-__device__ __forceinline__ uint32_t win_count_sum(WinRd& w, uint64_t off, uint64_t n, bool is_str, bool is_signed, uint64_t& count, uint64_t& sum) {
+template <class Rd_>
+__device__ __forceinline__ uint32_t win_count_sum(Rd_& w, uint64_t off, uint64_t n, bool is_str, bool is_signed, uint64_t& count, uint64_t& sum) {
   WinCur d{off, off + n};
   count = 0;
   sum = 0;
@@ -582,42 +575,60 @@ __global__ void __launch_bounds__(256) k_chunks(const uint8_t* __restrict__ aren
     if (staged) chunk_body(stage[w] + (cd.off - lo16), cd, i, info, hdr, false, dcols);
     else chunk_body(arena + cd.off, cd, i, info, hdr, defer, dcols);
   }
-  // the large documents of this wave, one at a time, counted by all 64 lanes over an LDS window
-  // (their chunk_body stopped before the counts when its header parse succeeded)
+  // the large documents of this wave (at most two): lanes 8j + k count column k of the j-th one, each
+  // over its own line of global memory, so the six chains of dependent reads run side by side
+  // (their chunk_body stopped before the counts when its header parse succeeded). The first failing
+  // column in the order below gives the status, as counting them one after another would.
   uint64_t big = __ballot(defer && dcols[1] + dcols[3] + dcols[5] + dcols[7] + dcols[9] + dcols[11] + dcols[0] > 0);
-  while (big) {
-    const int j = __builtin_ctzll(big);
-    big &= big - 1;
-    const uint64_t goff = __shfl(cd.off, j, 64);
-    const uint64_t glen = __shfl((uint64_t)cd.len, j, 64);
-    const uint32_t o0 = __shfl(dcols[0], j, 64), n0 = __shfl(dcols[1], j, 64), o1 = __shfl(dcols[2], j, 64), n1 = __shfl(dcols[3], j, 64);
-    const uint32_t o2 = __shfl(dcols[4], j, 64), n2 = __shfl(dcols[5], j, 64), o3 = __shfl(dcols[6], j, 64), n3 = __shfl(dcols[7], j, 64);
-    const uint32_t o4 = __shfl(dcols[8], j, 64), n4 = __shfl(dcols[9], j, 64), o5 = __shfl(dcols[10], j, 64), n5 = __shfl(dcols[11], j, 64);
-    WinRd wr{arena + goff, stage[w], glen, ~0ull};
-    uint64_t nchg = 0, ndeps = 0, nops = 0, nents = 0, sbytes = 0;
-    uint32_t st = AM_OK;
-#pragma unroll 1
-    for (int k = 0; k < 6 && !st; k++) {
-      const uint32_t o = k == 0 ? o0 : k == 1 ? o1 : k == 2 ? o2 : k == 3 ? o3 : k == 4 ? o4 : o5;
-      const uint32_t n = k == 0 ? n0 : k == 1 ? n1 : k == 2 ? n2 : k == 3 ? n3 : k == 4 ? n4 : n5;
-      uint64_t c, sm;
-      st = win_count_sum(wr, o, n, k >= 4, k == 2, c, sm);
-      if (k == 0) nchg = c;
-      else if (k == 1) ndeps = sm;
-      else if (k == 2) nops = c;
-      else if (k == 3) nents = sm;
-      else sbytes += sm;
+  if (big) {
+    const int j0 = __builtin_ctzll(big);
+    const uint64_t rest = big & (big - 1);
+    const int j1 = rest ? __builtin_ctzll(rest) : -1;
+    const uint32_t grp = l >> 3, k = l & 7;
+    const int j = grp == 0 ? j0 : grp == 1 ? j1 : -1;
+    // every lane reads its document's column table entries (shuffles are wave-wide)
+    const int js = j < 0 ? 0 : j;
+    uint32_t o = 0, n = 0;
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      const uint32_t oq = __shfl(dcols[2 * q], js, 64), nq = __shfl(dcols[2 * q + 1], js, 64);
+      if ((int)k == q) { o = oq; n = nq; }
     }
-    if ((int)l == j) {
-      ChunkInfo& ci = info[i];
-      if (st) {
-        ci.status = st;
-      } else {
-        ci.nchg = (uint32_t)nchg;
-        ci.ndeps = (uint32_t)ndeps;
-        ci.nops = (uint32_t)nops;
-        ci.nents = (uint32_t)nents;
-        ci.strbytes = (uint32_t)sbytes;
+    const uint64_t goff = __shfl(cd.off, js, 64);
+    uint64_t c = 0, sm = 0;
+    uint32_t st = AM_OK;
+    if (j >= 0 && k < 6) {
+      LineRd rd{arena, goff, ~0ull, make_uint4(0, 0, 0, 0)};
+      st = win_count_sum(rd, o, n, k >= 4, k == 2, c, sm);
+    }
+    // gather per document: lanes 8g .. 8g + 5
+#pragma unroll
+    for (int g = 0; g < 2; g++) {
+      const int jg = g == 0 ? j0 : j1;
+      if (jg < 0) continue;
+      uint64_t v[6], w6[6];
+      uint32_t e[6];
+#pragma unroll
+      for (int q = 0; q < 6; q++) {
+        v[q] = __shfl(c, 8 * g + q, 64);
+        w6[q] = __shfl(sm, 8 * g + q, 64);
+        e[q] = __shfl(st, 8 * g + q, 64);
+      }
+      if ((int)l == jg) {
+        uint32_t first = AM_OK;
+#pragma unroll
+        for (int q = 0; q < 6; q++)
+          if (!first) first = e[q];
+        ChunkInfo& ci = info[i];
+        if (first) {
+          ci.status = first;
+        } else {
+          ci.nchg = (uint32_t)v[0];
+          ci.ndeps = (uint32_t)w6[1];
+          ci.nops = (uint32_t)v[2];
+          ci.nents = (uint32_t)w6[3];
+          ci.strbytes = (uint32_t)(w6[4] + w6[5]);
+        }
       }
     }
   }
