@@ -137,6 +137,8 @@ __device__ static void plan_lookups(DocShared& s, const am_doc_desc& dd, const C
   }
 }
 
+__device__ static bool plan_heads(DocShared& s, uint32_t nheads, uint32_t nall, uint32_t nq);
+
 // ---- P2b: causal queue, clock, actor table, heads (one lane; integer work only) ----
 __device__ static void plan_doc(DocShared& s, const am_doc_desc& dd, const ChunkInfo* info, int32_t* chg_state) {
   const WsLayout& L = s.L;
@@ -144,7 +146,6 @@ __device__ static void plan_doc(DocShared& s, const am_doc_desc& dd, const Chunk
   ActorRef* actors = hp<ActorRef>(s, L.actors);
   int64_t* clock = hp<int64_t>(s, L.clock);
   int32_t* docpos = hp<int32_t>(s, L.docpos);
-  uint8_t* heads = hp<uint8_t>(s, L.heads);
   int32_t* head_ref = hp<int32_t>(s, L.head_ref);
   ChgRow* chg = hp<ChgRow>(s, L.chg);
   int64_t* deps = hp<int64_t>(s, L.deps);
@@ -307,7 +308,25 @@ __device__ static void plan_doc(DocShared& s, const am_doc_desc& dd, const Chunk
       deps[cr.deps_off + di] = r >= 0 ? (int64_t)(s.nbc + applied[r]) : dref_idx[dbase[c] + di];
     }
   }
-  // heads (sorted, new.js:1593) with their headsIndexes
+  if (!plan_heads(s, nheads, nall, nq)) return;
+  s.napplied = nall;
+  s.nqueued = nq;
+  s.nactors = na;
+  s.nrows = nrow;
+  s.nents = nent;
+  s.nchg = s.nbc + nall;
+  s.ndeps = ndep;
+  s.max_op = max_op;
+}
+
+// heads (sorted, new.js:1593) with their headsIndexes, from head_ref[0, nheads): false on an error
+__device__ static bool plan_heads(DocShared& s, uint32_t nheads, uint32_t nall, uint32_t nq) {
+  const WsLayout& L = s.L;
+  const APtr A = AV(s);
+  uint8_t* heads = hp<uint8_t>(s, L.heads);
+  const int32_t* head_ref = hp<int32_t>(s, L.head_ref);
+  const uint8_t* hashes = hp<uint8_t>(s, L.hashes);
+  const int32_t* applied = hp<int32_t>(s, L.applied);
   int64_t* hidx = hp<int64_t>(s, L.hidx);
   for (uint32_t q = 0; q < nheads; q++) {
     int32_t r = head_ref[q];
@@ -322,16 +341,180 @@ __device__ static void plan_doc(DocShared& s, const am_doc_desc& dd, const Chunk
     }
   if (nall > 0 || nq > 0)
     for (uint32_t q = 0; q < nheads; q++)
-      if (hidx[q] < 0) { set_err(s, AM_U_HASH_GRAPH); return; }
-  s.napplied = nall;
-  s.nqueued = nq;
-  s.nactors = na;
+      if (hidx[q] < 0) { set_err(s, AM_U_HASH_GRAPH); return false; }
   s.nheads = nheads;
-  s.nrows = nrow;
-  s.nents = nent;
-  s.nchg = s.nbc + nall;
-  s.ndeps = ndep;
-  s.max_op = max_op;
+  return true;
+}
+
+// ---- P2b, closed form: when every change of the call applies in the first pass of the queue in
+// list order -- no duplicate, every dependency an earlier change of the call or a base head /
+// host-known hash with its index, each author's seq the next one, every actor of a change known by
+// then, messages valid UTF-8 -- applyChanges' loop (new.js:1550-1597) reduces to prefix sums and
+// per-change counts, computed by the whole workgroup (a lane per change) instead of plan_doc's one
+// lane over chains of dependent loads. Returns false (nothing the queue reads written) when the
+// call is not of that shape: plan_doc then runs the queue and reports the reference's errors. ----
+__device__ static bool plan_fast(DocShared& s, const am_doc_desc& dd, const ChunkInfo* info, int32_t* chg_state) {
+  const WsLayout& L = s.L;
+  const APtr A = AV(s);
+  const uint32_t t = threadIdx.x, T = blockDim.x;
+  const uint32_t N = dd.chg_count;
+  const uint32_t NB = s.has_base ? s.dh.nactors : 0;
+  const uint32_t HB = s.has_base ? s.dh.nheads : 0;
+  if (N == 0 || HB > T) return false;
+  ActorRef* actors = hp<ActorRef>(s, L.actors);
+  int64_t* clock = hp<int64_t>(s, L.clock);
+  int32_t* docpos = hp<int32_t>(s, L.docpos);
+  int32_t* head_ref = hp<int32_t>(s, L.head_ref);
+  ChgRow* chg = hp<ChgRow>(s, L.chg);
+  int64_t* deps = hp<int64_t>(s, L.deps);
+  const ChgHdr* ch = hp<ChgHdr>(s, L.chghdr);
+  uint32_t* order = hp<uint32_t>(s, L.order);
+  uint32_t* rowbase = hp<uint32_t>(s, L.rowbase);
+  uint32_t* entbase = hp<uint32_t>(s, L.entbase);
+  uint32_t* ambase_out = hp<uint32_t>(s, L.amb_out);
+  uint32_t* amap = hp<uint32_t>(s, L.amap);
+  uint32_t* refd = hp<uint32_t>(s, L.queue);  // change j is some change's dependency
+  const uint32_t* dup_of = hp<uint32_t>(s, L.dup_of);
+  const int64_t* self_idx = hp<int64_t>(s, L.self_idx);
+  const int32_t* aut = hp<int32_t>(s, L.aut);
+  const int32_t* can = hp<int32_t>(s, L.can);
+  const int32_t* dref = hp<int32_t>(s, L.dref);
+  const int64_t* dref_idx = hp<int64_t>(s, L.dref_idx);
+  const uint32_t* ambase = hp<uint32_t>(s, L.ambase);
+  const uint32_t* dbase = hp<uint32_t>(s, L.dbase);
+  int32_t* applied = hp<int32_t>(s, L.applied);
+  // the base document's actors and clock (readDocumentChanges, new.js:1645-1675), as plan_doc
+  if (t == 0) {
+    s.pf_ok = 1;
+    s.pf_nheads = HB;
+    s.pf_maxop = 0;
+    if (s.has_base) {
+      Rd r{A + s.dh.base + s.dh.actors_off, (uint64_t)1 << 40, 0};
+      for (uint32_t i = 0; i < NB; i++) {
+        int64_t l;
+        rd_u53(r, l);
+        actors[i].off = s.dh.base + s.dh.actors_off + r.off;
+        actors[i].len = (uint32_t)l;
+        r.off += (uint64_t)l;
+        docpos[i] = (int32_t)i;
+      }
+    }
+    for (uint32_t i = 0; i < NB + N; i++) clock[i] = 0;
+    for (uint32_t i = 0; i < s.nbc && s.pf_ok; i++) {
+      const int64_t a = chg[i].actor, seq = chg[i].seq;
+      if (a == AM_NULL64 || a < 0 || a >= (int64_t)NB || seq == AM_NULL64 || (seq != 1 && seq != clock[a] + 1)) s.pf_ok = 0;
+      else clock[a] = seq;
+    }
+  }
+  __syncthreads();
+  if (!s.pf_ok) return false;  // plan_doc reports the base document's error
+  // the shape checks, a lane per change
+  bool ok = true;
+  for (uint32_t c = t; c < N && ok; c += T) {
+    const ChgHdr& h = ch[c];
+    ok = dup_of[c] == c && self_idx[c] == -2;
+    for (uint32_t di = 0; di < h.ndeps && ok; di++) {
+      const int32_t r = dref[dbase[c] + di];
+      ok = r >= 0 ? (uint32_t)r < c : (r != -1 && dref_idx[dbase[c] + di] != -1);
+    }
+    const int32_t a = aut[c];
+    uint32_t prior = 0;
+    for (uint32_t j = 0; j < c; j++) prior += aut[j] == a ? 1u : 0u;
+    ok = ok && a >= 0 && h.seq == (a < (int32_t)NB ? clock[a] : 0) + (int64_t)prior + 1;
+    for (uint32_t k = 0; k < h.nactors && ok; k++) {
+      const int32_t x = can[ambase[c] + k];
+      ok = x >= 0 && (x < (int32_t)NB || (uint32_t)(x - (int32_t)NB) <= c);
+    }
+    ok = ok && utf8_valid_dev(A + h.base + h.msg_off, h.msg_len);
+  }
+  if (!ok) atomicAnd(&s.pf_ok, 0u);
+  __syncthreads();
+  if (!s.pf_ok) return false;
+  // per-change counts -> prefix sums (rows, entries, new authors)
+  for (uint32_t c = t; c < N; c += T) {
+    const ChunkInfo& ci = info[dd.chg_begin + c];
+    rowbase[c] = ci.nops;
+    entbase[c] = ci.nents;
+    order[c] = aut[c] == (int32_t)(NB + c) ? 1u : 0u;  // the first change of a new author
+    refd[c] = 0;
+  }
+  __syncthreads();
+  const uint32_t nrow = block_excl_scan(rowbase, N, s.tmp);
+  const uint32_t nent = block_excl_scan(entbase, N, s.tmp);
+  const uint32_t nnew = block_excl_scan(order, N, s.tmp);
+  // new authors in application order (getActorTable, new.js:1435-1441)
+  for (uint32_t c = t; c < N; c += T) {
+    const bool isnew = aut[c] == (int32_t)(NB + c);
+    const uint32_t dp = NB + order[c];
+    docpos[NB + c] = isnew ? (int32_t)dp : -1;
+    if (isnew) {
+      actors[dp].off = ch[c].base + ch[c].actor_off;
+      actors[dp].len = ch[c].actor_len;
+    }
+  }
+  __syncthreads();
+  uint32_t* bref = s.tmp;  // base head h is some change's dependency (HB <= T)
+  if (t < HB) bref[t] = 0;
+  __syncthreads();
+  for (uint32_t c = t; c < N; c += T) {
+    const ChgHdr& h = ch[c];
+    const ChunkInfo& ci = info[dd.chg_begin + c];
+    const int32_t a = aut[c];
+    bool last = true;
+    for (uint32_t j = c + 1; j < N && last; j++) last = aut[j] != a;
+    if (last) clock[a] = h.seq;
+    ambase_out[c] = ambase[c];
+    for (uint32_t k = 0; k < h.nactors; k++) amap[ambase[c] + k] = (uint32_t)docpos[can[ambase[c] + k]];
+    for (uint32_t di = 0; di < h.ndeps; di++) {
+      const int32_t r = dref[dbase[c] + di];
+      if (r >= 0) refd[r] = 1;
+      else if (r <= -10) bref[-10 - r] = 1;
+      deps[s.nbd + dbase[c] + di] = r >= 0 ? (int64_t)(s.nbc + (uint32_t)r) : dref_idx[dbase[c] + di];
+    }
+    applied[c] = (int32_t)c;
+    chg_state[dd.chg_begin + c] = (int32_t)c;
+    rowbase[c] += s.nb;
+    entbase[c] += s.nbe;
+    // appendChange row (new.js:1680-1692)
+    ChgRow& cr = chg[s.nbc + c];
+    cr.actor = docpos[a];
+    cr.seq = h.seq;
+    cr.max_op = h.start_op + (int64_t)ci.nops - 1;
+    cr.time = h.time;
+    cr.msg_off = h.base + h.msg_off;
+    cr.msg_len = h.msg_len;
+    cr.ndeps = h.ndeps;
+    cr.deps_off = s.nbd + dbase[c];
+    cr.extra_len = h.has_extra ? (int64_t)(((uint64_t)h.extra_len << 4) | 7) : 7;
+    cr.extra_off = h.base + h.extra_off;
+    cr.extra_raw_len = h.has_extra ? h.extra_len : 0;
+    if (ci.nops > 0 && cr.max_op > 0) atomicMax(&s.pf_maxop, (unsigned long long)cr.max_op);
+  }
+  __syncthreads();
+  // heads: the base heads and changes nothing in the call depends on (new.js:1581-1583)
+  if (t < HB && !bref[t]) head_ref[atomicAdd(&s.pf_nheads, 1u) - HB] = -10 - (int32_t)t;
+  __syncthreads();
+  for (uint32_t c = t; c < N; c += T) {
+    order[c] = c;
+    if (!refd[c]) head_ref[atomicAdd(&s.pf_nheads, 1u) - HB] = (int32_t)c;
+  }
+  __syncthreads();
+  if (t == 0) {
+    // pf_nheads counted from HB: the base heads kept and the change heads
+    const uint32_t nheads = s.pf_nheads - HB;
+    if (s.b.P == 2) reinterpret_cast<uint32_t*>(s.ws + L.passend)[s.npass++] = nrow;
+    if (plan_heads(s, nheads, N, 0)) {
+      s.napplied = N;
+      s.nqueued = 0;
+      s.nactors = NB + nnew;
+      s.nrows = s.nb + nrow;
+      s.nents = s.nbe + nent;
+      s.nchg = s.nbc + N;
+      s.ndeps = s.nbd + (N ? dbase[N - 1] + ch[N - 1].ndeps : 0);
+      s.max_op = (int64_t)s.pf_maxop;
+    }
+  }
+  return true;
 }
 
 // ---- P4: column decode. Every lane runs the same stream decoder over one (source, column)
@@ -1369,15 +1552,14 @@ __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restric
     ChgHdr& h = hp<ChgHdr>(s, L.chghdr)[k];
     parse_change_hdr(AV(s) + cd.off + ci.data_off, ci.data_len, cd.off + ci.data_off, h);
   }
-  if (t == 0) {  // prefix offsets of the change actor lists and deps
-    uint32_t am = 0, db = 0;
-    for (uint32_t k = 0; k < dd.chg_count; k++) {
-      hp<uint32_t>(s, L.ambase)[k] = am;
-      hp<uint32_t>(s, L.dbase)[k] = db;
-      am += info[dd.chg_begin + k].nactors;
-      db += info[dd.chg_begin + k].ndeps;
-    }
+  // prefix offsets of the change actor lists and deps
+  for (uint32_t k = t; k < dd.chg_count; k += T) {
+    hp<uint32_t>(s, L.ambase)[k] = info[dd.chg_begin + k].nactors;
+    hp<uint32_t>(s, L.dbase)[k] = info[dd.chg_begin + k].ndeps;
   }
+  __syncthreads();
+  block_excl_scan(hp<uint32_t>(s, L.ambase), dd.chg_count, s.tmp);
+  block_excl_scan(hp<uint32_t>(s, L.dbase), dd.chg_count, s.tmp);
   __syncthreads();
   if (s.has_base)
     for (uint32_t c = t; c < DC_NCOLS; c += T) decode_base_chg_col(s, c);
@@ -1390,7 +1572,7 @@ __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restric
   __syncthreads();
   if (s.status) goto done;
   PH(2);
-  if (t == 0) plan_doc(s, dd, info, chg_state);
+  if (!plan_fast(s, dd, info, chg_state) && t == 0) plan_doc(s, dd, info, chg_state);
   __syncthreads();
   if (s.status) goto done;
   {

@@ -751,6 +751,8 @@ struct DocShared {
   uint32_t nrows, nents, nchg, ndeps;     // totals after planning
   uint32_t nout, nnew;
   uint32_t npass;                         // applyChanges passes that applied changes (P == 2)
+  uint32_t pf_ok, pf_nheads;              // plan_fast: the closed form applies; heads collected
+  unsigned long long pf_maxop;            // plan_fast: maxOp of the applied changes
   uint32_t nb_act;                        // values in the base document's action column: the ops
                                           // readNextDocOp sees (new.js:658-670), normally nb
   int64_t max_op;

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--text", type=int, default=0, help="C3 text histories of this many changes instead of C4")
     ap.add_argument("--patch", action="store_true", help="stage with AM_DOC_WANT_DIFF (the applyChanges patch)")
     ap.add_argument("--c5", action="store_true", help="C5 pairs merged: base + both sides' 10 changes (~100 rows)")
+    ap.add_argument("--mid", action="store_true", help="mid-size documents (workload.mid: 48 changes, ~1,154 ops)")
     args = ap.parse_args()
     import workload
     from automerge_amd import _native
@@ -33,7 +34,9 @@ def main():
     lib = _native.lib
     f = lib.amx_phase_cycles
     f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-    if args.c5:
+    if args.mid:
+        arena, chunks, docs, ops = workload.mid(0, args.docs)
+    elif args.c5:
         arena, chunks, docs, ops = workload.c5(0, args.docs)
         docs = docs.copy()
     elif args.text:
