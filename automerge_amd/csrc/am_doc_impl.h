@@ -56,17 +56,40 @@ __device__ static int64_t base_head_index(DocShared& s, uint32_t h) {
 // Canonical actor ids: base actors 0..NB-1, the author of change j (first occurrence) NB + j.
 // Dependency refs: >= 0 change index (first occurrence of that hash in the list),
 // <= -10: base head (-10 - h), -2: host-known hash, -1: missing.
+// first 8 bytes of a hash / id, little-endian (byte loads: any alignment)
+__device__ __forceinline__ uint64_t pre8(const uint8_t* p) {
+  uint64_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) v |= (uint64_t)p[k] << (8 * k);
+  return v;
+}
+// Candidates are found by comparing 8-byte prefixes (one load per candidate, independent of the
+// others: the loop keeps several in flight); only a prefix hit compares the whole hash / id.
 __device__ static void plan_lookups(DocShared& s, const am_doc_desc& dd, const ChunkInfo* info, const am_known_hash* known) {
   const WsLayout& L = s.L;
   const uint32_t N = dd.chg_count, t = threadIdx.x, T = blockDim.x;
   const ChgHdr* ch = hp<ChgHdr>(s, L.chghdr);
   uint8_t* hashes = hp<uint8_t>(s, L.hashes);
+  const uint64_t* hw = reinterpret_cast<const uint64_t*>(hashes);  // 32-byte aligned entries
   const APtr A = AV(s);
   const uint32_t NB = s.has_base ? s.dh.nactors : 0;
+  // each change's author id: 8-byte prefix and length, in tables P2b rewrites (queue, applied,
+  // order are not read before it)
+  uint32_t* apl = hp<uint32_t>(s, L.queue);
+  uint32_t* aph = reinterpret_cast<uint32_t*>(hp<int32_t>(s, L.applied));
+  uint32_t* alen = hp<uint32_t>(s, L.order);
   for (uint32_t c = t; c < N; c += T) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(info[dd.chg_begin + c].hash);
     uint32_t* dst = reinterpret_cast<uint32_t*>(hashes + 32 * c);
     for (int k = 0; k < 8; k++) dst[k] = src[k];
+    const ChgHdr& h = ch[c];
+    uint8_t b8[8];
+    for (uint32_t k = 0; k < 8; k++) b8[k] = k < h.actor_len ? A[h.base + h.actor_off + k] : 0;
+    uint64_t v = 0;
+    for (int k = 0; k < 8; k++) v |= (uint64_t)b8[k] << (8 * k);
+    apl[c] = (uint32_t)v;
+    aph[c] = (uint32_t)(v >> 32);
+    alen[c] = h.actor_len;
   }
   __syncthreads();
   uint32_t* dup_of = hp<uint32_t>(s, L.dup_of);
@@ -91,9 +114,39 @@ __device__ static void plan_lookups(DocShared& s, const am_doc_desc& dd, const C
   auto author_canon = [&](uint64_t off, uint32_t len, uint32_t upto) -> int32_t {
     int32_t a = base_actor(off, len);
     if (a >= 0) return a;
-    for (uint32_t j = 0; j < upto; j++) {
-      const ChgHdr& hj = ch[j];
-      if (hj.actor_len == len && bytes_eq(A + hj.base + hj.actor_off, A + off, len)) return (int32_t)(NB + j);
+    uint8_t b8[8];
+    for (uint32_t k = 0; k < 8; k++) b8[k] = k < len ? A[off + k] : 0;
+    uint64_t v = 0;
+    for (int k = 0; k < 8; k++) v |= (uint64_t)b8[k] << (8 * k);
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    for (uint32_t j0 = 0; j0 < upto; j0 += 8) {
+      uint32_t m = 0;  // candidates among j0 .. j0 + 7: their loads issue together
+#pragma unroll
+      for (uint32_t u = 0; u < 8; u++) {
+        const uint32_t j = j0 + u;
+        if (j < upto && apl[j] == lo && aph[j] == hi && alen[j] == len) m |= 1u << u;
+      }
+      for (; m; m &= m - 1) {
+        const uint32_t j = j0 + (uint32_t)__builtin_ctz(m);
+        const ChgHdr& hj = ch[j];
+        if (bytes_eq(A + hj.base + hj.actor_off, A + off, len)) return (int32_t)(NB + j);
+      }
+    }
+    return -1;
+  };
+  // first change j < n whose hash is h (its 8-byte prefix p): -1 if none
+  auto find_hash = [&](const uint8_t* h, uint64_t p, uint32_t n) -> int32_t {
+    for (uint32_t j0 = 0; j0 < n; j0 += 8) {
+      uint32_t m = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < 8; u++) {
+        const uint32_t j = j0 + u;
+        if (j < n && hw[4 * j] == p) m |= 1u << u;
+      }
+      for (; m; m &= m - 1) {
+        const uint32_t j = j0 + (uint32_t)__builtin_ctz(m);
+        if (hash_eq(hashes + 32 * j, h)) return (int32_t)j;
+      }
     }
     return -1;
   };
@@ -101,16 +154,30 @@ __device__ static void plan_lookups(DocShared& s, const am_doc_desc& dd, const C
     if (s.has_base)
       for (uint32_t k = 0; k < s.dh.nheads; k++)
         if (hash_eq(A + s.dh.base + s.dh.heads_off + 32 * k, h)) { ref = -10 - (int32_t)k; idx = base_head_index(s, k); return true; }
-    for (uint32_t k = 0; k < dd.known_count; k++)
-      if (hash_eq(known[dd.known_begin + k].hash, h)) { ref = -2; idx = known[dd.known_begin + k].index; return true; }
+    const uint64_t p = pre8(h);
+    const am_known_hash* kn = known + dd.known_begin;
+    for (uint32_t k0 = 0; k0 < dd.known_count; k0 += 8) {
+      uint32_t m = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < 8; u++)
+        if (k0 + u < dd.known_count && *reinterpret_cast<const uint64_t*>(kn[k0 + u].hash) == p) m |= 1u << u;
+      for (; m; m &= m - 1) {
+        const uint32_t k = k0 + (uint32_t)__builtin_ctz(m);
+        if (hash_eq(kn[k].hash, h)) {
+          ref = -2;
+          idx = kn[k].index;
+          return true;
+        }
+      }
+    }
     return false;
   };
   for (uint32_t c = t; c < N; c += T) {
     const ChgHdr& h = ch[c];
     const uint8_t* hc = hashes + 32 * c;
-    uint32_t d = c;
-    for (uint32_t j = 0; j < c; j++) if (hash_eq(hashes + 32 * j, hc)) { d = j; break; }
-    dup_of[c] = d;
+    const uint64_t pc = hw[4 * c];
+    const int32_t dj = find_hash(hc, pc, c);
+    dup_of[c] = dj >= 0 ? (uint32_t)dj : c;
     int32_t ref;
     int64_t idx;
     self_idx[c] = match_base(hc, ref, idx) ? idx : (int64_t)-2;
@@ -128,9 +195,7 @@ __device__ static void plan_lookups(DocShared& s, const am_doc_desc& dd, const C
       const uint8_t* dep = A + h.base + h.deps_off + 32 * di;
       int32_t r = -1;
       int64_t x = 0;
-      if (!match_base(dep, r, x)) {
-        for (uint32_t j = 0; j < N; j++) if (hash_eq(hashes + 32 * j, dep)) { r = (int32_t)j; break; }
-      }
+      if (!match_base(dep, r, x)) r = find_hash(dep, pre8(dep), N);
       dref[dbase[c] + di] = r;
       dref_idx[dbase[c] + di] = x;
     }
