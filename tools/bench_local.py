@@ -83,8 +83,10 @@ def main():
                 ms.append(dt)
             assert patch["diffs"]["objectId"] == "_root"
         ms.sort()
-        res.append({"ops": int(p["maxOp"]), "changes": len(h), "calls": len(ms), "median_ms": ms[len(ms) // 2],
-                    "min_ms": ms[0], "max_ms": ms[-1]})
+        # "ops": the history's size as requested (the reference side's label, tools/cpu_reference_local.js);
+        # max_op: the document's maxOp (two actors that never meet: about half of it)
+        res.append({"ops": n, "max_op": int(p["maxOp"]), "changes": len(h), "calls": len(ms),
+                    "median_ms": ms[len(ms) // 2], "min_ms": ms[0], "max_ms": ms[-1]})
         print(json.dumps(res[-1]), flush=True)
     print(json.dumps({"what": "Backend.applyLocalChange per call (one inserted character) on text documents, "
                               "am_doc_apply_local_change: host encodeChange + GPU re-merge of the whole document "
