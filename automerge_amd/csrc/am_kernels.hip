@@ -825,6 +825,23 @@ constexpr uint32_t kDocT = DOC_T_GLB;
 #include "am_doc_impl.h"
 #undef K_DOC_WAVES_ATTR
 }  // namespace glb_mode
+// The same kernel at eight waves per SIMD (64 VGPRs, more of its state in scratch) for batches of many
+// documents: their resident waves hide more of the global-memory latency than they lose to the
+// spills (8,192 mid documents: k_doc 20.9 -> 17.4 ms; C3's 1,000 100k-op documents 208.5 / 209.9
+// ms either way; one 100k-op document alone, the per-handle call, is 3% slower at eight:
+// profiles/r6/r6t_ab_glb_waves.txt). Launched for batches of AM_GLB8_MIN documents or more
+// (environment; default 1024).
+static uint32_t glb8_min() {
+  const char* e = std::getenv("AM_GLB8_MIN");
+  return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1024u;
+}
+namespace glb8_mode {
+constexpr bool kHotLds = false;
+constexpr uint32_t kDocT = DOC_T_GLB;
+#define K_DOC_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+#include "am_doc_impl.h"
+#undef K_DOC_WAVES_ATTR
+}  // namespace glb8_mode
 // P8 of the global-mode documents (glb_mode::k_diff_one): one wave per document. Wide: all lanes run
 // the replay (scans and searches spread over them: few, large documents); else lane 0 alone (many
 // documents: the waves themselves fill the machine). The chain is dependent loads: resident waves hide
@@ -1120,7 +1137,7 @@ void am_launch_doc(const BatchDev& b, hipStream_t s) {
     hipLaunchKernelGGL(lds_mode::k_doc, dim3(grid), dim3(AM_LDS_DOC_T), b.lds_bytes, s, b.arena, b.chunks, b.docs, b.known,
                        b.info, b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd, rest);
     if (b.max_hot_host > b.lds_bytes)
-      hipLaunchKernelGGL(glb_mode::k_doc, dim3(b.ndocs), dim3(DOC_T_GLB), 0, s, b.arena, b.chunks, b.docs, b.known, b.info,
+      hipLaunchKernelGGL(b.ndocs >= glb8_min() ? glb8_mode::k_doc : glb_mode::k_doc, dim3(b.ndocs), dim3(DOC_T_GLB), 0, s, b.arena, b.chunks, b.docs, b.known, b.info,
                          b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd, nullptr);
     {
       if (b.any_diff) {

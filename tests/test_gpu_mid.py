@@ -18,8 +18,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CASES = json.load(open(os.path.join(HERE, "golden", "mid.json")))
 
 
+@pytest.mark.parametrize("glb8", [False, True], ids=["glb4", "glb8"])
 @pytest.mark.parametrize("cs", CASES, ids=[c["name"] for c in CASES])
-def test_mid_documents_match_reference(cs):
+def test_mid_documents_match_reference(cs, glb8, monkeypatch):
+    """glb8: the global-mode k_doc built for eight waves per SIMD (AM_GLB8_MIN=0: every batch; by
+    default only batches of 1,024+ documents take it) must give the same documents and patches."""
+    if glb8:
+        monkeypatch.setenv("AM_GLB8_MIN", "0")
     from automerge_amd import patch as P
     import workload as W
     from automerge_amd.batch import WANT_PATCH
