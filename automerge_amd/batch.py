@@ -53,8 +53,10 @@ def pack(docs, device=0, flags=0):
 
 
 class Batch:
-    def __init__(self, device=0):
-        self._eng = N.engine(device)
+    def __init__(self, device=0, engine=None):
+        """engine: an am_engine of one's own (N.lib.am_engine_create) -- its own HIP stream, so two
+        batches on two engines overlap one's stage with the other's kernels; default the process's."""
+        self._eng = engine if engine is not None else N.engine(device)
         self._b = N.lib.am_batch_create(self._eng)
         self.ndocs = 0
         self.nchunks = 0

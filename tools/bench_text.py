@@ -94,9 +94,34 @@ def main():
         b.run()
         b.sync()
     elapsed_full = (time.perf_counter() - t0) / args.steps
+    # the same steps pipelined over two batches on two engines (two HIP streams): step k's stage (H2D,
+    # checksums, inflate, sizing) runs while step k-1's kernels do, as the C4 pipeline overlaps its
+    # batches; every step still moves and inflates all of its inputs
+    from automerge_amd import _native as N
+    err = N.Error()
+    eng2 = N.lib.am_engine_create(0, N.C.byref(err))
+    if not eng2:
+        N.raise_for(err)
+    b2 = Batch(engine=eng2)
+    pair = [b, b2]
+    b2.stage(arena2, chunks2, docs2)
+    b2.run()
+    b2.sync()
+    npipe = max(2, args.steps)
+    t0 = time.perf_counter()
+    for k in range(npipe):
+        cur = pair[k % 2]
+        cur.stage(arena2, chunks2, docs2)
+        cur.run()
+        if k:
+            pair[(k - 1) % 2].sync()
+    pair[(npipe - 1) % 2].sync()
+    elapsed_pipe = (time.perf_counter() - t0) / npipe
+    pipe_err = int((b.results()["status"] != 0).sum()) + int((b2.results()["status"] != 0).sum())
+    del b2
+    N.lib.am_engine_destroy(eng2)
     # the same with the bases staged beforehand on the host path (am_stage_documents), untimed: the
     # stage then moves uncompressed bases and inflates only the changes
-    from automerge_amd import _native as N
     hs = N.stage_documents(bases)
     arena4, chunks4, docs4 = pack([(h[0], r_) for h, r_ in zip(hs, rest)])
     chunks4["flags"][docs4["base_chunk"].astype(np.int64)] = [1 if h[1] else 0 for h in hs]
@@ -151,6 +176,8 @@ def main():
         "what": "per step from host memory: H2D of the saved bases and the compressed changes, GPU checksums of "
                 "the compressed bases, GPU inflate of their DEFLATEd columns and of the changes, pipeline",
         "stage_ms_per_step": st_s * 1e3 / k,
+        "pipelined_ops_per_s": ops_applied / elapsed_pipe, "pipelined_ms_per_step": elapsed_pipe * 1e3,
+        "pipelined_steps": npipe, "pipelined_errors": pipe_err,
         "staged_bases_ops_per_s": ops_applied / elapsed_h2d, "staged_bases_ms_per_step": elapsed_h2d * 1e3,
         "kernel_resident_ops_per_s": ops_applied / elapsed, "kernel_resident_ms_per_step": elapsed * 1e3,
         "patch_100k_doc_k_doc_ms": min(patch_ms),
