@@ -304,7 +304,9 @@ def main():
     import torch
     dist = None
     dist_info = {"world_size": 1, "backend": None}
-    if world > 1:
+    # AM_DIST_FORCE=1: the process group even for one rank (tests/test_gpu_bench_ranks.py runs the
+    # nccl branch -- RCCL init, the device all-gather -- on a one-GPU box this way)
+    if world > 1 or os.environ.get("AM_DIST_FORCE") == "1":
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))

@@ -41,3 +41,15 @@ def test_two_ranks_equal_one_rank():
         assert r["patch_digest"] == pinned_p and r["digest_pinned"]["patches"]["match"]
     assert two["config"]["docs_rank0"] < DOCS  # rank 0 merged only its shard
     assert one["output_bytes_rank0"] > two["output_bytes_rank0"]
+
+
+def test_nccl_branch_on_one_rank():
+    """bench.py's RCCL path (init_process_group('nccl') bound to the device, the digest all-gather of
+    device tensors, the NUMA report's all_gather_object) on one rank of one GPU: the driver's
+    multi-GPU run takes this branch with N ranks."""
+    args = ["bench.py", "--docs", str(DOCS), "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--check", "4"]
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+              "--master-addr", "127.0.0.1", "--master-port", "29519"] + args, {"AM_DIST_FORCE": "1"})
+    rec = json.load(open(os.path.join(ROOT, "tests", "golden", "c4_digest.json")))[str(DOCS)]
+    assert r["dist"]["backend"] == "nccl" and r["dist"]["world_size"] == 1
+    assert r["errors"] == 0 and r["digest"] == rec["digest"] and r["patch_digest"] == rec["patch_digest"]
