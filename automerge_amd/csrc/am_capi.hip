@@ -314,12 +314,15 @@ struct PinBuf {
   bool ensure(size_t n) {
     if (n <= cap && p) return true;
     const size_t want = std::max<size_t>(n ? n : 1, cap + cap / 2);
+    HostClock clk;
     if (p) { (void)hipHostFree(p); p = nullptr; cap = 0; }
     if (hipHostMalloc(reinterpret_cast<void**>(&p), want * sizeof(T), pinned_flags()) != hipSuccess) {
       p = nullptr;
       return false;
     }
     cap = want;
+    clk.mark("alloc");
+    clk.print("pinned", want * sizeof(T));
     return true;
   }
   ~PinBuf() { if (p) (void)hipHostFree(p); }
