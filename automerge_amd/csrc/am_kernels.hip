@@ -759,7 +759,7 @@ struct DocShared {
   uint32_t col_len[OC_NCOLS + DC_NCOLS];
   uint32_t col_pos[OC_NCOLS + DC_NCOLS];
   uint64_t out_len;
-  uint32_t tmp[DOC_T_GLB + 1];
+  uint32_t* tmp;                          // block scans' scratch: blockDim.x + 1 entries (k_doc_one)
   uint64_t ph_last;
   uint32_t xs_used;                       // bytes of replaced strings after the staged input (b.U)
   uint32_t nunk_inst, nunk_ids;           // unknown op columns: instances, distinct output columns
@@ -842,6 +842,22 @@ constexpr uint32_t kDocT = DOC_T_GLB;
 #include "am_doc_impl.h"
 #undef K_DOC_WAVES_ATTR
 }  // namespace glb8_mode
+// A batch of a few large documents (a per-handle call on one 100k-op text, say) leaves most of the
+// GPU idle: each document gets a 16-wave workgroup, so its sorts, scans, gathers and list ranking
+// run on four times the lanes (the column decode and encode keep their lane / wave per column).
+// Launched for batches of at most AM_GLB16_MAX documents (environment; default 8).
+#define DOC_T_GLB16 1024
+static uint32_t glb16_max() {
+  const char* e = std::getenv("AM_GLB16_MAX");
+  return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 8u;
+}
+namespace glb16_mode {
+constexpr bool kHotLds = false;
+constexpr uint32_t kDocT = DOC_T_GLB16;
+#define K_DOC_WAVES_ATTR
+#include "am_doc_impl.h"
+#undef K_DOC_WAVES_ATTR
+}  // namespace glb16_mode
 // P8 of the global-mode documents (glb_mode::k_diff_one): one wave per document. Wide: all lanes run
 // the replay (scans and searches spread over them: few, large documents); else lane 0 alone (many
 // documents: the waves themselves fill the machine). The chain is dependent loads: resident waves hide
@@ -1137,7 +1153,8 @@ void am_launch_doc(const BatchDev& b, hipStream_t s) {
     hipLaunchKernelGGL(lds_mode::k_doc, dim3(grid), dim3(AM_LDS_DOC_T), b.lds_bytes, s, b.arena, b.chunks, b.docs, b.known,
                        b.info, b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd, rest);
     if (b.max_hot_host > b.lds_bytes)
-      hipLaunchKernelGGL(b.ndocs >= glb8_min() ? glb8_mode::k_doc : glb_mode::k_doc, dim3(b.ndocs), dim3(DOC_T_GLB), 0, s, b.arena, b.chunks, b.docs, b.known, b.info,
+      hipLaunchKernelGGL(b.ndocs <= glb16_max() ? glb16_mode::k_doc : b.ndocs >= glb8_min() ? glb8_mode::k_doc : glb_mode::k_doc, dim3(b.ndocs),
+                         dim3(b.ndocs <= glb16_max() ? DOC_T_GLB16 : DOC_T_GLB), 0, s, b.arena, b.chunks, b.docs, b.known, b.info,
                          b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd, nullptr);
     {
       if (b.any_diff) {

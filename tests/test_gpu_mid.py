@@ -18,12 +18,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CASES = json.load(open(os.path.join(HERE, "golden", "mid.json")))
 
 
-@pytest.mark.parametrize("glb8", [False, True], ids=["glb4", "glb8"])
+@pytest.mark.parametrize("build", ["glb4", "glb8", "glb16"])
 @pytest.mark.parametrize("cs", CASES, ids=[c["name"] for c in CASES])
-def test_mid_documents_match_reference(cs, glb8, monkeypatch):
-    """glb8: the global-mode k_doc built for eight waves per SIMD (AM_GLB8_MIN=0: every batch; by
-    default only batches of 1,024+ documents take it) must give the same documents and patches."""
-    if glb8:
+def test_mid_documents_match_reference(cs, build, monkeypatch):
+    """The three builds of the global-mode k_doc must give the same documents and patches: four
+    waves per SIMD, eight (AM_GLB8_MIN=0: every batch; by default batches of 1,024+ documents), and
+    the 16-wave workgroup (AM_GLB16_MAX: by default batches of at most 8 documents)."""
+    monkeypatch.setenv("AM_GLB16_MAX", "1000000" if build == "glb16" else "0")
+    if build == "glb8":
         monkeypatch.setenv("AM_GLB8_MIN", "0")
     from automerge_amd import patch as P
     import workload as W

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--patch", action="store_true", help="stage with AM_DOC_WANT_DIFF (the applyChanges patch)")
     ap.add_argument("--c5", action="store_true", help="C5 pairs merged: base + both sides' 10 changes (~100 rows)")
     ap.add_argument("--mid", action="store_true", help="mid-size documents (workload.mid: 48 changes, ~1,154 ops)")
+    ap.add_argument("--handle", type=int, default=0,
+                    help="the per-handle shape: load(save(text history of this many changes but the last)) + "
+                         "applyChanges(the last change), with the applyChanges patch")
     args = ap.parse_args()
     import workload
     from automerge_amd import _native
@@ -34,7 +37,17 @@ def main():
     lib = _native.lib
     f = lib.amx_phase_cycles
     f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-    if args.mid:
+    if args.handle:
+        from automerge_amd.batch import pack
+        a0, c0, d0, _ = workload.text(0, args.docs, args.handle, 100, 0)
+        hist = [workload.doc_chunks(a0, c0, d0, i)[1] for i in range(args.docs)]
+        prep = Batch(device=0)
+        prep.stage(*pack([(None, h[:-1]) for h in hist]))
+        prep.run(); prep.sync()
+        bases = [prep.doc_save(i) for i in range(args.docs)]
+        arena, chunks, docs = pack([(b_, [h[-1]]) for b_, h in zip(bases, hist)], flags=WANT_DIFF)
+        ops = 100 * args.docs
+    elif args.mid:
         arena, chunks, docs, ops = workload.mid(0, args.docs)
     elif args.c5:
         arena, chunks, docs, ops = workload.c5(0, args.docs)
