@@ -541,15 +541,16 @@ __device__ static uint32_t block_excl_scan(uint32_t* a, uint32_t n, uint32_t* s_
 }
 
 // Stable LSD radix sort of n (key, val) pairs by the low `bits` bits of the keys, 8-bit digits, by
-// the whole block (blockDim.x a multiple of 64, at most 256). k0 / v0 hold the input and on return
+// the whole block (blockDim.x a multiple of 64, at most 64 * MaxW). k0 / v0 hold the input and on return
 // the sorted pairs; k1 / v1 are scratch of n entries. Per digit: an LDS histogram, its exclusive
 // scan, then tiles of blockDim.x pairs scattered in order -- a pair's place is its bucket's base,
 // the same-digit pairs of earlier waves of the tile and its rank among its wave's same-digit lanes
 // (eight ballots). A digit every key shares is skipped. O(n) per digit against bitonic's
 // O(n log^2 n) compare-exchanges, for the large documents' id and document-order sorts.
+template <uint32_t MaxW = 4>  // waves of the block (blockDim.x <= 64 * MaxW)
 __device__ static void block_radix_sort(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, uint32_t n, uint32_t bits) {
   __shared__ uint32_t s_hist[256];
-  __shared__ uint32_t s_wc[4 * 256];
+  __shared__ uint32_t s_wc[MaxW * 256];
   __shared__ uint32_t s_skip;
   const uint32_t T = blockDim.x, t = threadIdx.x, w = t >> 6, lane = t & 63, W = T >> 6;
   uint64_t* ka = k0;

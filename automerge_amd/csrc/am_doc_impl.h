@@ -1246,7 +1246,7 @@ __device__ static bool radix_idk(DocShared& s, IdKey* idk, uint32_t R) {
   const uint32_t bits = rs_bits(s_max);
   __syncthreads();
   if (bad) return false;
-  block_radix_sort(k0, v0, k1, v1, R, bits);
+  block_radix_sort<kDocT / 64>(k0, v0, k1, v1, R, bits);
   for (uint32_t i = t; i < R; i += T) {
     IdKey k;
     k.ctr = (int64_t)(k0[i] >> 16);
@@ -1298,7 +1298,7 @@ __device__ static bool radix_elemk(DocShared& s, ElemKey* ek, uint32_t M, uint32
     __syncthreads();
     const uint32_t bits = rs_bits(s_max);
     __syncthreads();
-    block_radix_sort(k0, v0, k1, v1, M, bits);
+    block_radix_sort<kDocT / 64>(k0, v0, k1, v1, M, bits);
   }
   for (uint32_t i = t; i < M; i += T) tmp[i] = ek[v0[i]];
   __syncthreads();
@@ -1342,7 +1342,7 @@ __device__ static bool radix_newent(DocShared& s, NewEnt* ne, uint32_t N, uint32
     __syncthreads();
     const uint32_t bits = rs_bits(s_max);
     __syncthreads();
-    block_radix_sort(k0, v0, k1, v1, N, bits);
+    block_radix_sort<kDocT / 64>(k0, v0, k1, v1, N, bits);
   }
   for (uint32_t i = t; i < N; i += T) tmp[i] = ne[v0[i]];
   __syncthreads();
@@ -1419,7 +1419,7 @@ __device__ static bool radix_docorder(DocShared& s, SortRec* sr, uint32_t n, uin
     __syncthreads();
     const uint32_t bits = rs_bits(s_max);
     __syncthreads();
-    block_radix_sort(k0, v0, k1, v1, n, bits);
+    block_radix_sort<kDocT / 64>(k0, v0, k1, v1, n, bits);
   }
   for (uint32_t i = t; i < n; i += T) v1[i] = (uint32_t)sr[v0[i]].row;
   __syncthreads();
@@ -1531,12 +1531,14 @@ __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restric
                                           uint64_t ws_cap, uint32_t lds_bytes, am_doc_result* __restrict__ results,
                                           int32_t* __restrict__ chg_state, const uint8_t* __restrict__ fast_done) {
   __shared__ DocShared s;
+  __shared__ uint32_t s_tmp[kDocT + 1];  // block scans' scratch (s.tmp)
   const uint32_t t = threadIdx.x, T = blockDim.x;
   if (fast_done && fast_done[doc]) return;  // merged by k_doc_fast (am_doc_fast.h)
   const am_doc_desc dd = docs[doc];
   uint8_t* const wsg = ws_base + ws_off[doc];  // global (derived from the kernel argument)
   if (t == 0) {
     s.b = bounds[doc];
+    s.tmp = s_tmp;
     s.ws = ws_base + ws_off[doc];
     s.L = ws_layout(s.b);
     // hot working set in LDS when it fits (this namespace's mode decides who runs the document)
@@ -2165,9 +2167,9 @@ __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restric
     auto coln = [&](int c) -> uint32_t {
       return c < OC_GRP_ACTOR ? NOUT : c < OC_NCOLS ? NSUCC : c == OC_NCOLS + DC_DEPS_INDEX ? s.ndeps : NC;
     };
-    // a large document in global mode: each wave encodes a column of its own (waves 1..3 with the
-    // scratch at L.enc_x), four columns at a time
-    const uint32_t NW = (kDocT > 64 && L.enc_x) ? kDocT / 64 : 1u;
+    // a large document in global mode: each of four waves encodes a column of its own (waves 1..3
+    // with the scratch at L.enc_x), four columns at a time; further waves of a 16-wave workgroup wait
+    const uint32_t NW = (kDocT > 64 && L.enc_x) ? (kDocT / 64 < 4 ? kDocT / 64 : 4u) : 1u;
     if (NW > 1) {
       const uint32_t wv = t >> 6, ln = t & 63;
       EncCtx exw = ex;
@@ -2181,7 +2183,7 @@ __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restric
       }
       for (int c0 = 0; c0 < OC_NCOLS + DC_NCOLS; c0 += (int)NW) {
         const int c = c0 + (int)wv;
-        if (c < OC_NCOLS + DC_NCOLS) {
+        if (wv < NW && c < OC_NCOLS + DC_NCOLS) {
           const uint32_t n = coln(c);
           for (uint32_t i = ln; i < n; i += 64) exw.V[i] = colval(c, i);
           wave_sync();
