@@ -636,13 +636,15 @@ __device__ static uint32_t src_of(DocShared& s, uint32_t i, bool ents) {
   return lo - 1;
 }
 
-// one stream: decodes n values into cells (utf8: (offset - span_lo) << 32 | length; boolean 0/1)
-__device__ static void decode_stream(DocShared& s, uint32_t item, int64_t* cells) {
+// one stream: decodes n values into cells (utf8: (offset - span_lo) << 32 | length; boolean 0/1).
+// With `defer`, a stream of am_dec_long values or more is left alone and reported (returns true).
+__device__ static bool decode_stream(DocShared& s, uint32_t item, int64_t* cells, bool defer = false) {
   const uint32_t src = item / DEC_STREAMS, j = item % DEC_STREAMS;
   const uint32_t col = j < OC_VAL_RAW ? j : j + 1;
   const SrcInfo si = src_info(s, src);
-  if (si.is_change && (col == OC_ID_ACTOR || col == OC_ID_CTR)) return;  // ids from the header (new.js:708-709)
+  if (si.is_change && (col == OC_ID_ACTOR || col == OC_ID_CTR)) return false;  // ids from the header (new.js:708-709)
   const uint32_t n = j < DEC_ROWCOLS ? si.nr : si.ne;
+  if (defer && n >= ::am_dec_long) return true;
   int64_t* dst = cells + (uint64_t)DEC_ROWCOLS * si.row0 + 2ull * si.ent0 +
                  (j < DEC_ROWCOLS ? (uint64_t)j * si.nr : (uint64_t)DEC_ROWCOLS * si.nr + (uint64_t)(j - DEC_ROWCOLS) * si.ne);
   const uint8_t type = kOpColDec[col];
@@ -671,9 +673,307 @@ __device__ static void decode_stream(DocShared& s, uint32_t item, int64_t* cells
       else if (type == DT_DELTA) v = (d.absolute += x);
       else v = x;
     }
-    if (e) { set_err(s, e, 0, 0, 0, 0, si.chg); return; }
+    if (e) { set_err(s, e, 0, 0, 0, 0, si.chg); return false; }
     dst[i] = v;
   }
+  return false;
+}
+
+// position of the q-th (from 0) set bit of m; q < popcount(m)
+__device__ __forceinline__ uint32_t nth_bit64(uint64_t m, uint32_t q) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t w = 32; w; w >>= 1) {
+    const uint32_t c = (uint32_t)__popcll(m & ((1ull << w) - 1));
+    if (q >= c) { q -= c; m >>= w; pos += w; }
+  }
+  return pos;
+}
+__device__ __forceinline__ int64_t wave_incl_add64(int64_t x) {
+  uint64_t v = (uint64_t)x;
+  v += ::wave::dpp<::wave::ROW_SHR1>(0ull, v);
+  v += ::wave::dpp<::wave::ROW_SHR2>(0ull, v);
+  v += ::wave::dpp<::wave::ROW_SHR4>(0ull, v);
+  v += ::wave::dpp<::wave::ROW_SHR8>(0ull, v);
+  v += ::wave::dpp<::wave::ROW_BCAST15, 0xa>(0ull, v);
+  v += ::wave::dpp<::wave::ROW_BCAST31, 0xc>(0ull, v);
+  return (int64_t)v;
+}
+
+// global-memory accesses of the global modes as global_* instructions: a flat access also counts
+// against lgkmcnt, so every later LDS access or cross-lane gather would wait for it to complete
+__device__ __forceinline__ void st_cell(int64_t* p, int64_t v) {
+  if constexpr (kHotLds) *p = v;
+  else *(__attribute__((address_space(1))) int64_t*)p = v;
+}
+__device__ __forceinline__ uint32_t ld_byte(const uint8_t* p) {
+  if constexpr (kHotLds) return *p;
+  else return *(const __attribute__((address_space(1))) uint8_t*)p;
+}
+
+// One long stream by the 64 lanes of a wave (a saved document's columns hold a value per op: one
+// lane walking 100k values is the per-handle call's longest chain). The RLEDecoder / DeltaDecoder /
+// BooleanDecoder state is wave-uniform (encoding.js:820-886, 1025-1030, 1171-1183) and the stream
+// is read through a 64-byte window held in the wave's registers, a byte per lane, in which every
+// lane has decoded the varint starting at its byte: a record header or a run value is a readlane,
+// repetition, null and boolean runs are written 64 values a step, and an integer literal run is
+// taken a window at a time (varint ends by ballot, the q-th value gathered to lane q, deltas by a
+// wave scan); a string value is a length from the window and a wave-wide byte compare against the
+// previous one. A varint the window cannot hold (over four bytes, or the stream's truncated end) or any error (a value repeated inside a literal run, a malformed
+// record) sends the stream to lane 0's decode_stream, which writes it again and reports the
+// reference's first error.
+#ifdef AM_PHASE_CLOCK
+#define BADR(c) do { bad = true; if (lane == 0 && (blockIdx.x & 63) == 0) { am_phase_cycles[32] = (c); am_phase_cycles[33] = i; am_phase_cycles[34] = d.r.off; am_phase_cycles[35] = j; am_phase_cycles[36] = (uint64_t)d.count; am_phase_cycles[37] = d.state; } } while (0)
+#else
+#define BADR(c) (bad = true)
+#endif
+// bytes a[0, len) == b[0, len), 64 a step across the wave (len wave-uniform)
+__device__ __forceinline__ bool wave_bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t len) {
+  const uint32_t lane = ::wave::lane_id();
+  for (uint32_t q = 0; q < len; q += 64) {
+    const bool in = q + lane < len;
+    const uint32_t x = in ? ld_byte(a + q + lane) : 0u, y = in ? ld_byte(b + q + lane) : 0u;
+    if (__ballot(x != y)) return false;
+  }
+  return true;
+}
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) { return (uint64_t)rfl((uint32_t)(v >> 32)) << 32 | rfl((uint32_t)v); }
+__device__ __attribute__((noinline)) static void decode_stream_wave(DocShared& s, uint32_t item_, int64_t* cells) {
+  // every quantity of the decoder state is wave-uniform: read once through readfirstlane, the state
+  // and its control flow stay in scalar registers and scalar branches (values loaded through flat
+  // pointers count as per-lane for the compiler, and would drag every step into vector code)
+  const uint32_t lane = ::wave::lane_id();
+  const uint32_t item = rfl(item_);
+  const uint32_t src = item / DEC_STREAMS, j = item % DEC_STREAMS;
+  const uint32_t col = j < OC_VAL_RAW ? j : j + 1;
+  const SrcInfo si = src_info(s, src);
+  const uint32_t n = rfl(j < DEC_ROWCOLS ? si.nr : si.ne);
+  int64_t* dst = reinterpret_cast<int64_t*>(rfl64(reinterpret_cast<uint64_t>(
+      cells + (uint64_t)DEC_ROWCOLS * si.row0 + 2ull * si.ent0 +
+      (j < DEC_ROWCOLS ? (uint64_t)j * si.nr : (uint64_t)DEC_ROWCOLS * si.nr + (uint64_t)(j - DEC_ROWCOLS) * si.ne))));
+  const uint8_t type = (uint8_t)rfl(kOpColDec[col]);
+  const uint64_t off = rfl64(si.base + si.coff[col]);
+  ColDec d;
+  cd_init(d, type, reinterpret_cast<const uint8_t*>(rfl64(reinterpret_cast<uint64_t>(AV(s) + off))), rfl(si.clen[col]));
+  const int64_t sbase = (int64_t)rfl64(off - s.b.span_lo);
+  const bool track_act = rfl(!si.is_change && col == OC_ACTION) != 0;
+  const bool sgn = type == DT_DELTA;
+#ifdef AM_PHASE_CLOCK
+  const uint64_t clk0 = clock64();
+#endif
+  // the window: bytes [p0, p0 + 64); per lane the varint starting at its byte (wl = its length,
+  // 64 when over four bytes or not ended inside the window)
+  uint64_t p0 = ~0ull, endm = 0;
+  uint32_t wu = 0, wl = 64;
+  int32_t ws = 0;
+#ifdef AM_PHASE_CLOCK
+  uint64_t n_reload = 0, n_iter = 0, n_slow = 0, n_lit = 0;  // (n_slow: none since the hand-back)
+#define PCNT(x) (x)++
+#else
+#define PCNT(x) ((void)0)
+#endif
+  auto wload = [&](uint64_t at) {
+    PCNT(n_reload);
+    p0 = at;
+    const uint32_t b = at + lane < d.r.n ? ld_byte(d.r.p + at + lane) : 0x80u;  // past the end: never a varint end
+    endm = __ballot(!(b & 0x80));
+    const uint32_t x1 = ::wave::down1(b, 0x80u), x2 = ::wave::down1(x1, 0x80u), x3 = ::wave::down1(x2, 0x80u);
+    const uint64_t rest = endm >> lane;
+    wl = rest ? (uint32_t)__builtin_ctzll(rest) + 1 : 64;
+    uint32_t u = b & 0x7f, top = b;
+    if (wl > 1) { u |= (x1 & 0x7f) << 7; top = x1; }
+    if (wl > 2) { u |= (x2 & 0x7f) << 14; top = x2; }
+    if (wl > 3) { u |= (x3 & 0x7f) << 21; top = x3; }
+    wu = u;
+    ws = (wl <= 4 && (top & 0x40)) ? (int32_t)(u | (0xffffffffu << (7 * wl))) : (int32_t)u;
+  };
+  // the varint at stream offset `at` (wave-uniform) from the window, reloaded at `at` when the
+  // varint is not inside it; false: the window cannot hold it
+  auto wvar = [&](uint64_t at, uint32_t& u, int32_t& sv, uint32_t& l) -> bool {
+    if (at < p0 || at - p0 >= 64 || (at != p0 && ::wave::bcast(wl, (int)(at - p0)) > 4)) wload(at);
+    const int q = (int)(at - p0);
+    l = ::wave::bcast(wl, q);
+    if (l > 4) return false;
+    u = ::wave::bcast(wu, q);
+    sv = ::wave::bcast(ws, q);
+    return true;
+  };
+  bool bad = false;
+  uint32_t i = 0;
+  // the staged values [sb, i): lane l holds value sb + l
+  uint32_t sb = 0;
+  int64_t sv = 0;
+  auto flush = [&]() {
+    if (lane < i - sb) st_cell(dst + sb + lane, sv);
+    sb = i;
+  };
+  // k values v0 + (q + 1) * step, q = 0..k-1 (step 0: k copies of v0)
+  auto put_run = [&](uint32_t k, int64_t v0, int64_t step) {
+    uint32_t q0 = 0;
+    while (k) {
+      const uint32_t off = i - sb, take = min(k, 64u - off);
+      if (lane >= off && lane < off + take)
+        sv = (int64_t)((uint64_t)v0 + (uint64_t)(lane - off + q0 + 1) * (uint64_t)step);
+      i += take; k -= take; q0 += take;
+      if (i - sb == 64) flush();
+    }
+  };
+  auto put1 = [&](int64_t v) {
+    if (lane == i - sb) sv = v;
+    if (++i - sb == 64) flush();
+  };
+  while (i < n) {
+    PCNT(n_iter);
+    // the loop-carried state back in scalar registers at every step (see above)
+    i = rfl(i); sb = rfl(sb);
+    d.count = (int64_t)rfl64((uint64_t)d.count); d.r.off = rfl64(d.r.off); p0 = rfl64(p0);
+    d.last = (int64_t)rfl64((uint64_t)d.last); d.absolute = (int64_t)rfl64((uint64_t)d.absolute);
+    d.state = (uint8_t)rfl(d.state); d.has_last = (uint8_t)rfl(d.has_last); d.last_null = (uint8_t)rfl(d.last_null);
+    d.blast = (uint8_t)rfl(d.blast); d.bfirst = (uint8_t)rfl(d.bfirst);
+    if (cd_done(d)) {  // the column ran out: nulls (false) for the rest, as cd_next / cd_next_bool
+      if (track_act && lane == 0 && s.nb_act == 0xffffffffu) s.nb_act = i;
+      put_run(n - i, type == DT_BOOL ? 0 : AM_NULL64, 0);
+      break;
+    }
+    uint32_t e = AM_OK, hu, hl;
+    int32_t hs;
+    if (type == DT_BOOL) {
+      while (d.count == 0) {
+        if (wvar(d.r.off, hu, hs, hl)) { d.count = hu; d.r.off += hl; }
+        else { e = AM_E_LEB_INCOMPLETE; break; }  // (or a count over four bytes): the lane decoder's case
+        d.blast = !d.blast;
+        if (d.count == 0 && !d.bfirst) { e = AM_E_BOOL_ZERO_RUN; break; }
+        d.bfirst = 0;
+      }
+      if (e) { BADR(1); break; }
+      const uint32_t k = (uint32_t)min((uint64_t)d.count, (uint64_t)(n - i));
+      put_run(k, d.blast, 0);
+      d.count -= k;
+      continue;
+    }
+    if (d.count == 0) {  // the next record (cd_record)
+      bool done = false;
+      if (wvar(d.r.off, hu, hs, hl)) {
+        const int64_t c = hs;
+        uint32_t vu, vl;
+        int32_t vs;
+        if (c == 1 || (c < 0 && d.state == 2) || (c == 0 && d.state == 3)) { BADR(2); break; }
+        if (c < 0) {
+          d.count = -c; d.state = 2; d.r.off += hl;
+          done = true;
+        } else if (wvar(d.r.off + hl, vu, vs, vl)) {
+          if (c > 1 && type == DT_UTF8) {  // the run's string: its length, then its bytes
+            const uint64_t at = d.r.off + hl + vl;
+            if (at + vu > d.r.n) { BADR(9); break; }  // AM_E_SUBARRAY
+            if ((d.state == 1 || d.state == 2) && d.has_last && !d.last_null && vu == d.last_len &&
+                wave_bytes_eq(d.r.p + at, d.r.p + d.last, vu)) { BADR(3); break; }
+            d.count = c; d.state = 1; d.last = (int64_t)at; d.last_len = vu; d.has_last = 1; d.last_null = 0;
+            d.r.off += vu;  // the bytes (the length and the header below)
+          } else if (c > 1) {
+            const int64_t v = sgn ? (int64_t)vs : (int64_t)vu;
+            if ((d.state == 1 || d.state == 2) && d.has_last && !d.last_null && v == d.last) { BADR(3); break; }
+            d.count = c; d.state = 1; d.last = v; d.last_len = 0; d.has_last = 1; d.last_null = 0;
+          } else {
+            if (vu == 0) { BADR(4); break; }
+            d.count = vu; d.state = 3; d.has_last = 1; d.last_null = 1;
+          }
+          d.r.off += hl + vl;
+          done = true;
+        }
+      }
+      if (!done) { BADR(5); break; }  // a varint the window cannot hold: the lane decoder's case
+    }
+    if (d.state != 2) {  // a repetition or a null run
+      const uint32_t k = (uint32_t)min((uint64_t)d.count, (uint64_t)(n - i));
+      if (d.last_null) {
+        put_run(k, AM_NULL64, 0);
+      } else if (type == DT_UTF8) {
+        put_run(k, ((sbase + d.last) << 32) | (int64_t)d.last_len, 0);
+      } else if (sgn) {
+        put_run(k, d.absolute, d.last);
+        d.absolute = (int64_t)((uint64_t)d.absolute + (uint64_t)k * (uint64_t)d.last);
+      } else {
+        put_run(k, d.last, 0);
+      }
+      d.count -= k;
+      continue;
+    }
+    if (!wvar(d.r.off, hu, hs, hl)) { BADR(7); break; }  // a varint the window cannot hold
+    if (type == DT_UTF8) {  // a string of a literal run: its length, then its bytes
+      const uint64_t at = d.r.off + hl;
+      if (at + hu > d.r.n) { BADR(9); break; }  // AM_E_SUBARRAY
+      if (d.has_last && !d.last_null && hu == d.last_len && wave_bytes_eq(d.r.p + at, d.r.p + d.last, hu)) {
+        BADR(8);  // AM_E_RLE_LIT_REP
+        break;
+      }
+      d.last = (int64_t)at; d.last_len = hu; d.has_last = 1; d.last_null = 0;
+      d.r.off = at + hu;
+      d.count--;
+      put1(((sbase + (int64_t)at) << 32) | (int64_t)hu);
+      continue;
+    }
+    if (d.count <= 4) {  // a short literal: value by value
+      const int64_t v = sgn ? (int64_t)hs : (int64_t)hu;
+      if (d.has_last && !d.last_null && v == d.last) { BADR(8); break; }  // AM_E_RLE_LIT_REP
+      d.last = v; d.last_len = 0; d.has_last = 1; d.last_null = 0;
+      d.r.off += hl;
+      d.count--;
+      put1(sgn ? (d.absolute += v) : v);
+      continue;
+    }
+    {  // an integer literal run: the window's varints
+      PCNT(n_lit);
+      const uint32_t pos = (uint32_t)(d.r.off - p0);
+      const uint64_t startm = (((endm << 1) | 1ull) | (1ull << pos)) & (~0ull << pos);
+      const uint64_t badm = __ballot(((startm >> lane) & 1) && wl > 4);
+      const uint32_t navail = badm ? (uint32_t)__popcll(startm & ((1ull << __builtin_ctzll(badm)) - 1))
+                                   : (uint32_t)__popcll(startm);
+      const uint32_t k = (uint32_t)min(min((uint64_t)navail, (uint64_t)d.count), (uint64_t)(n - i));
+      const uint32_t S = nth_bit64(startm, lane < k ? lane : 0);
+      const int32_t vq = __shfl(sgn ? ws : (int32_t)wu, (int)S);
+      const uint32_t endq = S + (uint32_t)__shfl((int)wl, (int)S);  // window byte after the q-th varint
+      // (the move runs on every lane: inside a lane-dependent branch, lane 0 would be off and lane 1
+      // would read the fill value)
+      const int32_t up = ::wave::up1(vq, 0);
+      const int64_t vq64 = sgn ? (int64_t)vq : (int64_t)(uint32_t)vq;
+      const int64_t prev64 = lane ? (sgn ? (int64_t)up : (int64_t)(uint32_t)up) : d.last;
+      const bool rep = lane < k && (lane || (d.has_last && !d.last_null)) && vq64 == prev64;
+      if (__ballot(rep)) { BADR(6); break; }  // AM_E_RLE_LIT_REP: lane 0 reports it
+      int64_t val = vq64;
+      if (sgn) val = d.absolute + wave_incl_add64(lane < k ? vq64 : 0);
+      d.last = ::wave::bcast(vq64, (int)k - 1);
+      if (sgn) d.absolute = ::wave::bcast(val, (int)k - 1);
+      d.r.off = p0 + ::wave::bcast(endq, (int)k - 1);
+      d.last_len = 0; d.has_last = 1; d.last_null = 0;
+      d.count -= k;
+      // value q to lane off + q: one rotation; the values past lane 63 wrap to lanes 0.. after a flush
+      const uint32_t off = i - sb, from = (lane - off) & 63;
+      const int64_t rot = (int64_t)((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uint64_t)val >> 32), (int)from) << 32 |
+                                    (uint32_t)__shfl((int)(uint32_t)val, (int)from));
+      if (lane >= off && lane < off + k) sv = rot;
+      if (off + k >= 64) {
+        i = sb + 64;
+        flush();
+        const uint32_t rest = off + k - 64;
+        if (lane < rest) sv = rot;
+        i = sb + rest;
+      } else {
+        i += k;
+      }
+      continue;
+    }
+  }
+  if (!bad) flush();
+  else if (lane == 0) decode_stream(s, item, cells);
+#ifdef AM_PHASE_CLOCK
+  // probe builds: the stream's cycles by column (slots 16 + j) and the streams handed back (slot 31)
+  if (lane == 0 && (blockIdx.x & 63) == 0) {
+    atomicAdd(&am_phase_cycles[16 + j], (unsigned long long)(clock64() - clk0));
+    if (bad) atomicAdd(&am_phase_cycles[31], 1ull);
+    if (j == 3) { am_phase_cycles[40] = n_reload; am_phase_cycles[41] = n_iter; am_phase_cycles[42] = n_slow; am_phase_cycles[43] = n_lit; am_phase_cycles[44] = n; }
+  }
+#endif
 }
 
 // row i from the cells (lane per row)
@@ -1657,7 +1957,21 @@ __device__ __forceinline__ void k_doc_one(uint32_t doc, const uint8_t* __restric
 #if defined(AM_STOP_PHASE) && AM_STOP_PHASE == 2
     goto done;
 #endif
-    for (uint32_t it = t; it < nsrc * DEC_STREAMS; it += T) decode_stream(s, it, cells);
+    // a lane per stream; streams of am_dec_long values or more are listed (s.tmp[1..]) and decoded
+    // by a wave each afterwards (a list past its kDocT slots decodes the rest on lanes)
+    if (t == 0) s.tmp[0] = 0;
+    __syncthreads();
+    for (uint32_t it = t; it < nsrc * DEC_STREAMS; it += T)
+      if (decode_stream(s, it, cells, true)) {
+        const uint32_t slot = atomicAdd(&s.tmp[0], 1u);
+        if (slot < kDocT) s.tmp[1 + slot] = it;
+        else decode_stream(s, it, cells);
+      }
+    __syncthreads();
+    {
+      const uint32_t nlong = min(s.tmp[0], kDocT);
+      for (uint32_t q = t / 64; q < nlong; q += T / 64) decode_stream_wave(s, s.tmp[1 + q], cells);
+    }
     for (uint32_t src = t; src < nsrc; src += T) {
       const SrcInfo si = src_info(s, src);
       if (si.nr == 0 && si.ne != 0) set_err(s, AM_U_VALUE);  // group entries without ops

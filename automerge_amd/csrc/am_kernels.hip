@@ -14,11 +14,13 @@
 //              columnar.js:983-1004)
 //   k_out_hash_ws thread per document: container checksum of the merged document (columnar.js:659)
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 
 #include "am_dev_util.h"
 #include "am_layout.h"
+#include "am_wave.h"
 
 // column ids in spec order
 __device__ __constant__ static const uint8_t kChangeColIds[OC_NCOLS] = {0x01, 0x02, 0x11, 0x13, 0x15, 0x21, 0x23, 0x34,
@@ -698,7 +700,7 @@ struct NewEnt { int64_t ctr; int32_t target; int32_t actor; int32_t rank; int32_
 // Optional per-phase cycle counters (probe builds only: -DAM_PHASE_CLOCK). Every 64th document
 // adds the s_memtime delta of each phase; read back with amx_phase_cycles().
 #ifdef AM_PHASE_CLOCK
-__device__ unsigned long long am_phase_cycles[32];
+__device__ unsigned long long am_phase_cycles[48];
 #define PH(k)                                                                  \
   do {                                                                         \
     __syncthreads();                                                           \
@@ -799,6 +801,21 @@ __device__ __forceinline__ int hash_cmp(const uint8_t* a, const uint8_t* b) {
 __host__ __device__ inline bool doc_scattered(const DocBounds& b) { return b.span_hi == b.span_lo && b.B > 0; }
 
 extern __shared__ __attribute__((aligned(16))) uint8_t am_lds[];
+
+// k_doc's P4 decodes a stream of this many values or more with a whole wave (decode_stream_wave),
+// the rest a lane each. AM_DEC_LONG (environment, read at every k_doc launch) moves the threshold:
+// a value past every stream's length keeps them all on lanes (the tests compare the two decoders).
+__device__ uint32_t am_dec_long = 256;
+static void dec_long_sync() {
+  static std::atomic<uint32_t> cur{256};
+  const char* e = std::getenv("AM_DEC_LONG");
+  const uint32_t v = e ? (uint32_t)std::strtoul(e, nullptr, 10) : 256u;
+  if (v != cur.load()) {
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(am_dec_long), &v, sizeof v);
+    cur.store(v);
+  }
+}
 
 #ifndef AM_LDS_DOC_T
 #define AM_LDS_DOC_T DOC_T
@@ -1150,6 +1167,7 @@ void am_launch_doc(const BatchDev& b, hipStream_t s) {
                          b.ws_total, b.max_hot + 3);
       grid = b.ndocs < K_DOC_LOOP_WG ? b.ndocs : K_DOC_LOOP_WG;
     }
+    dec_long_sync();
     hipLaunchKernelGGL(lds_mode::k_doc, dim3(grid), dim3(AM_LDS_DOC_T), b.lds_bytes, s, b.arena, b.chunks, b.docs, b.known,
                        b.info, b.bounds, b.ws_off, b.ws, b.ws_cap, b.lds_bytes, b.results, b.chg_state, fd, rest);
     if (b.max_hot_host > b.lds_bytes)
@@ -1437,9 +1455,9 @@ extern "C" int amx_wave_selftest(const uint64_t* in_host, uint64_t* out_host) {
 
 #ifdef AM_PHASE_CLOCK
 extern "C" int amx_phase_cycles(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(am_phase_cycles), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(am_phase_cycles), sizeof(unsigned long long) * 48) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[32] = {0};
+    unsigned long long z[48] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(am_phase_cycles), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;

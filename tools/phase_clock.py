@@ -23,6 +23,8 @@ FAST = ["F0 status+stage input", "F1 headers+hashes+refs", "F2 canon+actor table
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--docs", type=int, default=65536)
+    ap.add_argument("--streams", action="store_true",
+                    help="print slots 16-31 as the wave-decoded streams' cycles by column (decode_stream_wave)")
     ap.add_argument("--text", type=int, default=0, help="C3 text histories of this many changes instead of C4")
     ap.add_argument("--patch", action="store_true", help="stage with AM_DOC_WANT_DIFF (the applyChanges patch)")
     ap.add_argument("--c5", action="store_true", help="C5 pairs merged: base + both sides' 10 changes (~100 rows)")
@@ -61,7 +63,7 @@ def main():
     b = Batch(device=0)
     b.stage(arena, chunks, docs)
     b.run(); b.sync()
-    buf = (ctypes.c_ulonglong * 32)()
+    buf = (ctypes.c_ulonglong * 48)()
     f(buf, 1)
     b.run(); b.sync()
     f(buf, 1)
@@ -72,6 +74,15 @@ def main():
         tot += c
         print("%-26s %10.0f cycles/doc" % (n, c))
     print("%-26s %10.0f cycles/doc   k_doc stage ms: %s" % ("total", tot, b.stage_times()))
+    if args.streams:
+        cols = ["objActor", "objCtr", "keyActor", "keyCtr", "keyStr", "idActor", "idCtr", "insert", "action",
+                "valLen", "chldActor", "chldCtr", "succNum", "succActor", "succCtr"]
+        for j, c in enumerate(cols):
+            print("wave stream %-10s %12d cycles" % (c, buf[16 + j]))
+        print("streams handed back to the lane decoder: %d" % buf[31])
+        print("last hand-back: reason %d at value %d, offset %d, column %d, count %d, state %d" % tuple(buf[32:38]))
+        print("keyCtr: window loads %d, loop steps %d, sequential records %d, literal windows %d, values %d" % tuple(buf[40:45]))
+        return
     # k_doc_fast: lane 0 of every 16th document
     sampled = (args.docs + 15) // 16
     tot = 0
